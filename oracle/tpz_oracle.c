@@ -1,0 +1,443 @@
+/*
+ * tpz_oracle.c — CPU restatement of topazdb's SSTable block decode + checksum path.
+ * TEST INFRASTRUCTURE ONLY (see tpz_oracle.h): the checker and the CPU baseline, never the
+ * product. Built by oracle/Makefile with gcc into oracle/liboracle.so.
+ */
+#define _GNU_SOURCE
+#include "tpz_oracle.h"
+
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+/* bytes::Buf::get_u16 / get_u32 are big-endian (bytes crate; src/block.rs:51,54). */
+static inline uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static inline uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* src/checksum.rs:6-10 — crc32fast::Hasher = CRC-32/ISO-HDLC: reflected polynomial
+ * 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF. Deliberately bit-serial (no tables) so it
+ * shares nothing with the device's table-driven algorithm. */
+uint32_t tpzo_crc32(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) {
+    c ^= p[i];
+    for (int b = 0; b < 8; b++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+  }
+  return c ^ 0xFFFFFFFFu;
+}
+
+/* One block's decoded view: Block{data, offsets} (src/block.rs:21-24). */
+typedef struct {
+  int status;
+  uint32_t crc_actual, crc_expected;
+  uint32_t n;
+  const uint8_t* offs; /* n big-endian u16 */
+  const uint8_t* data; /* entries region */
+  size_t data_len;
+} blockview;
+
+/* compress::decode (src/block/compress.rs:95-113) + Block::decode (src/block.rs:46-65). */
+static void block_decode(const uint8_t* b, size_t len, blockview* v) {
+  memset(v, 0, sizeof(*v));
+  if (len == 0) { v->status = TPZO_EMPTY; return; }             /* compress.rs:96-98 */
+  uint8_t tag = b[len - 1];                                      /* compress.rs:99 */
+  if (tag == 0 || tag > 3) { v->status = TPZO_BAD_TAG; return; } /* compress.rs:44-53,102 */
+  if (tag != 1) { v->status = TPZO_UNSUPPORTED; return; }        /* snappy / lz4 */
+  size_t dlen = len - 1;                                         /* compress.rs:100,103 */
+  if (dlen < 4) { v->status = TPZO_MALFORMED; return; }          /* block.rs:49 split_to */
+  size_t plen = dlen - 4;
+  v->crc_expected = be32(b + plen);                              /* block.rs:51 */
+  v->crc_actual = tpzo_crc32(b, plen);                           /* checksum.rs:13 */
+  if (v->crc_actual != v->crc_expected) { v->status = TPZO_CHECKSUM; return; }
+  if (plen < 2) { v->status = TPZO_MALFORMED; return; }          /* block.rs:54 get_u16 */
+  v->n = be16(b);
+  if (plen < 2 + 2 * (size_t)v->n) { v->status = TPZO_MALFORMED; return; } /* :56-59 */
+  v->offs = b + 2;
+  v->data = b + 2 + 2 * (size_t)v->n;                            /* block.rs:61-64 */
+  v->data_len = plen - 2 - 2 * (size_t)v->n;
+  v->status = TPZO_OK;
+}
+
+/* BlockIterator::seek_to (src/block/iterator.rs:63-83) for index i; returns 0 when the
+ * reference would panic (Buf::get_u16 underflow / slice out of range). */
+static int entry_at(const blockview* v, uint32_t i, const uint8_t** k, uint32_t* kl,
+                    const uint8_t** val, uint32_t* vl) {
+  size_t o = be16(v->offs + 2 * (size_t)i);                      /* :74 */
+  if (o + 2 > v->data_len) return 0;                             /* :75-77 */
+  uint32_t klen = be16(v->data + o);
+  if (o + 2 + klen + 2 > v->data_len) return 0;                  /* :78-81 */
+  uint32_t vlen = be16(v->data + o + 2 + klen);
+  if (o + 4 + klen + vlen > v->data_len) return 0;               /* :82 */
+  *k = v->data + o + 2;
+  *kl = klen;
+  *val = v->data + o + 4 + klen;
+  *vl = vlen;
+  return 1;
+}
+
+/* Decode a block and validate every entry the way an iteration over all indices would.
+ * Sets TPZO_MALFORMED on any panicking entry, TPZO_OVERLAP when the decoded bytes cannot fit
+ * the device slot contract (include/tpz_gpu.h: 6*n, key bytes and value bytes each <= len). */
+static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt, uint64_t* vt) {
+  block_decode(b, len, v);
+  *kt = *vt = 0;
+  if (v->status != TPZO_OK) return;
+  for (uint32_t i = 0; i < v->n; i++) {
+    const uint8_t *k, *val;
+    uint32_t kl, vl;
+    if (!entry_at(v, i, &k, &kl, &val, &vl)) { v->status = TPZO_MALFORMED; *kt = *vt = 0; return; }
+    *kt += kl;
+    *vt += vl;
+  }
+  if (6ull * v->n > len || *kt > len || *vt > len) v->status = TPZO_OVERLAP;
+}
+
+void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
+                      uint64_t* n_entries, uint64_t* key_bytes, uint64_t* val_bytes) {
+  uint64_t ne = 0, kb = 0, vb = 0;
+  for (uint32_t i = 0; i < n_blocks; i++) {
+    blockview v;
+    uint64_t kt, vt;
+    block_full(src + ext[i], ext[i + 1] - ext[i], &v, &kt, &vt);
+    if (v.status == TPZO_OK || v.status == TPZO_OVERLAP) { ne += v.n; kb += kt; vb += vt; }
+  }
+  *n_entries = ne;
+  *key_bytes = kb;
+  *val_bytes = vb;
+}
+
+int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
+                      uint8_t* status, uint32_t* crc_actual, uint32_t* crc_expected,
+                      uint32_t* count, uint32_t* klen, uint32_t* vlen,
+                      uint8_t* keys, uint8_t* vals) {
+  uint64_t e = 0, kp = 0, vp = 0;
+  for (uint32_t i = 0; i < n_blocks; i++) {
+    blockview v;
+    uint64_t kt, vt;
+    block_full(src + ext[i], ext[i + 1] - ext[i], &v, &kt, &vt);
+    status[i] = (uint8_t)v.status;
+    crc_actual[i] = v.crc_actual;
+    crc_expected[i] = v.crc_expected;
+    count[i] = 0;
+    if (v.status != TPZO_OK && v.status != TPZO_OVERLAP) continue;
+    count[i] = v.n;
+    for (uint32_t j = 0; j < v.n; j++, e++) {
+      const uint8_t *k, *val;
+      uint32_t kl, vl;
+      entry_at(&v, j, &k, &kl, &val, &vl);
+      klen[e] = kl;
+      vlen[e] = vl;
+      memcpy(keys + kp, k, kl);
+      memcpy(vals + vp, val, vl);
+      kp += kl;
+      vp += vl;
+    }
+  }
+  return 0;
+}
+
+/* FileObject::open (file_object.rs:57-78): whole-file CRC, size excludes the trailer.
+ * read_bloom (table.rs:75-87) and SsTable::open (table.rs:91-112): bloom_off, meta_off,
+ * decode_block_meta (table.rs:49-59). */
+int tpzo_sst_parse(const uint8_t* f, size_t len, uint64_t* ext, uint32_t ext_cap,
+                   uint32_t* n_blocks, uint64_t* meta_off, uint64_t* bloom_off) {
+  if (len < 4) return -2;
+  size_t size = len - 4;
+  if (tpzo_crc32(f, size) != be32(f + size)) return -1;
+  if (size < 4) return -2;
+  uint64_t bo = be32(f + size - 4);
+  if (bo < 4 || bo + 4 > size) return -2;
+  uint64_t mo = be32(f + bo - 4);
+  if (mo > bo - 4) return -2;
+  uint32_t nb = 0;
+  size_t p = mo, end = bo - 4;
+  while (p < end) {
+    if (p + 6 > end) return -2;
+    uint32_t off = be32(f + p);
+    uint32_t kl = be16(f + p + 4);
+    if (p + 6 + kl > end) return -2;
+    if (nb >= ext_cap) return -3;
+    ext[nb++] = off;
+    p += 6 + kl;
+  }
+  if (nb >= ext_cap) return -3;
+  ext[nb] = mo;
+  *n_blocks = nb;
+  *meta_off = mo;
+  *bloom_off = bo;
+  return 0;
+}
+
+/* ---- iterators ----------------------------------------------------------------------- */
+struct tpzo_sst_iter {
+  const uint8_t* file;
+  uint64_t* ext;
+  uint32_t nb;
+  uint64_t* mk_off; /* first_key positions in the meta region */
+  uint32_t* mk_len;
+  /* SsTableIterator (table/iterator.rs:10-14) */
+  uint32_t idx;
+  /* BlockIterator (block/iterator.rs:9-14) over the current block */
+  blockview blk;
+  uint32_t bidx;
+  uint8_t *key, *val;
+  size_t kl, vl, kcap, vcap;
+};
+
+static void set_bytes(uint8_t** dst, size_t* cap, size_t* len, const uint8_t* s, size_t n) {
+  if (n > *cap) {
+    *cap = n * 2 + 16;
+    *dst = (uint8_t*)realloc(*dst, *cap);
+  }
+  if (n) memcpy(*dst, s, n);
+  *len = n;
+}
+
+/* BlockIterator::seek_to (iterator.rs:63-83). A panicking entry leaves the iterator invalid. */
+static void biter_seek_to(tpzo_sst_iter* it, uint32_t i) {
+  it->kl = it->vl = 0;
+  if (i >= it->blk.n) { it->bidx = it->blk.n; return; }
+  it->bidx = i;
+  const uint8_t *k, *v;
+  uint32_t kl, vl;
+  if (!entry_at(&it->blk, i, &k, &kl, &v, &vl)) return;
+  set_bytes(&it->key, &it->kcap, &it->kl, k, kl);
+  set_bytes(&it->val, &it->vcap, &it->vl, v, vl);
+}
+
+/* BlockIterator::seek_to_key (iterator.rs:91-109): lower-bound binary search. */
+static void biter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
+  uint32_t left = 0, right = it->blk.n;
+  while (left < right) {
+    uint32_t mid = (right - left) / 2 + left;
+    const uint8_t *k, *v;
+    uint32_t kl, vl;
+    if (!entry_at(&it->blk, mid, &k, &kl, &v, &vl)) { it->kl = it->vl = 0; return; }
+    size_t m = kl < klen ? kl : klen;
+    int c = memcmp(k, key, m);
+    if (c == 0) c = (kl > klen) - (kl < klen);
+    if (c > 0) right = mid;
+    else if (c < 0) left = mid + 1;
+    else { biter_seek_to(it, mid); return; }
+  }
+  biter_seek_to(it, left);
+}
+
+/* SsTable::read_block (table.rs:154-164) into the iterator's current block. */
+static int read_block(tpzo_sst_iter* it, uint32_t i) {
+  block_decode(it->file + it->ext[i], it->ext[i + 1] - it->ext[i], &it->blk);
+  return it->blk.status == TPZO_OK ? 0 : -1;
+}
+
+tpzo_sst_iter* tpzo_sst_iter_create(const uint8_t* file, size_t len) {
+  uint32_t cap = (uint32_t)(len / 6 + 2), nb;
+  uint64_t mo, bo;
+  uint64_t* ext = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+  if (tpzo_sst_parse(file, len, ext, cap, &nb, &mo, &bo) != 0 || nb == 0) { free(ext); return NULL; }
+  tpzo_sst_iter* it = (tpzo_sst_iter*)calloc(1, sizeof(*it));
+  it->file = file;
+  it->ext = ext;
+  it->nb = nb;
+  it->mk_off = (uint64_t*)malloc(sizeof(uint64_t) * nb);
+  it->mk_len = (uint32_t*)malloc(sizeof(uint32_t) * nb);
+  size_t p = mo;
+  for (uint32_t i = 0; i < nb; i++) {
+    it->mk_len[i] = be16(file + p + 4);
+    it->mk_off[i] = p + 6;
+    p += 6 + it->mk_len[i];
+  }
+  return it;
+}
+
+void tpzo_sst_iter_destroy(tpzo_sst_iter* it) {
+  if (!it) return;
+  free(it->ext);
+  free(it->mk_off);
+  free(it->mk_len);
+  free(it->key);
+  free(it->val);
+  free(it);
+}
+
+/* seek_to_first_inner (table/iterator.rs:39-42) */
+static int seek_first_inner(tpzo_sst_iter* it, uint32_t idx) {
+  if (read_block(it, idx) != 0) return -1;
+  biter_seek_to(it, 0);
+  return 0;
+}
+
+int tpzo_sst_iter_seek_to_first(tpzo_sst_iter* it) { /* table/iterator.rs:28-37 */
+  it->idx = 0;
+  return seek_first_inner(it, 0);
+}
+
+/* SsTable::find_block_idx (table.rs:178-182): partition_point(first_key <= key) - 1, sat. */
+static uint32_t find_block_idx(const tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
+  uint32_t lo = 0, hi = it->nb;
+  while (lo < hi) {
+    uint32_t mid = lo + (hi - lo) / 2;
+    const uint8_t* fk = it->file + it->mk_off[mid];
+    size_t fl = it->mk_len[mid], m = fl < klen ? fl : klen;
+    int c = memcmp(fk, key, m);
+    if (c == 0) c = (fl > klen) - (fl < klen);
+    if (c <= 0) lo = mid + 1; else hi = mid;
+  }
+  return lo ? lo - 1 : 0;
+}
+
+int tpzo_sst_iter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
+  uint32_t idx = find_block_idx(it, key, klen);                   /* :55 */
+  if (read_block(it, idx) != 0) return -1;                        /* :56 */
+  biter_seek_to_key(it, key, klen);                               /* :57 */
+  if (it->kl == 0 && idx + 1 < it->nb) {                          /* :58-61 */
+    idx += 1;
+    if (seek_first_inner(it, idx) != 0) return -1;
+  }
+  it->idx = idx;
+  return 0;
+}
+
+int tpzo_sst_iter_next(tpzo_sst_iter* it) { /* table/iterator.rs:88-95 */
+  biter_seek_to(it, it->bidx + 1);
+  if (it->kl == 0 && it->idx < it->nb - 1) {
+    it->idx += 1;
+    return seek_first_inner(it, it->idx);
+  }
+  return 0;
+}
+
+int tpzo_sst_iter_is_valid(const tpzo_sst_iter* it) { return it->kl != 0; }
+const uint8_t* tpzo_sst_iter_key(const tpzo_sst_iter* it, size_t* len) { *len = it->kl; return it->key; }
+const uint8_t* tpzo_sst_iter_value(const tpzo_sst_iter* it, size_t* len) { *len = it->vl; return it->val; }
+uint32_t tpzo_sst_iter_block_idx(const tpzo_sst_iter* it) { return it->idx; }
+
+/* ---- CPU baseline ------------------------------------------------------------------------ */
+typedef struct {
+  int fd;
+  uint64_t* ext;
+  uint32_t nb;
+} sstfile;
+
+/* FileObject::open + SsTable::open on a path: whole-file read and CRC (file_object.rs:57-78). */
+static int sst_file_open(const char* path, sstfile* s) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  off_t len = lseek(fd, 0, SEEK_END);
+  uint8_t* buf = (uint8_t*)malloc((size_t)len);
+  if (pread(fd, buf, (size_t)len, 0) != len) { free(buf); close(fd); return -1; }
+  uint32_t cap = (uint32_t)(len / 6 + 2);
+  s->ext = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+  uint64_t mo, bo;
+  int rc = tpzo_sst_parse(buf, (size_t)len, s->ext, cap, &s->nb, &mo, &bo);
+  free(buf);
+  if (rc) { close(fd); free(s->ext); return -1; }
+  s->fd = fd;
+  return 0;
+}
+
+/* One `create_and_read` pass (benches/sstable_iter_read.rs:70-76): for every block a fresh
+ * Vec + pread (file_object.rs:23-27), the codec's BytesMut copy (compress.rs:103), CRC
+ * (block.rs:52), offsets Vec (block.rs:56-59); per entry key/value to_vec (iterator.rs:78,82).
+ * The per-block and per-entry allocations are kept: they are what the reference spends. */
+static uint64_t iter_read_pass(const sstfile* s, volatile uint64_t* sink, uint64_t* bytes) {
+  uint64_t ents = 0, by = 0, acc = 0;
+  for (uint32_t b = 0; b < s->nb; b++) {
+    size_t len = s->ext[b + 1] - s->ext[b];
+    uint8_t* raw = (uint8_t*)malloc(len ? len : 1);
+    if (pread(s->fd, raw, len, (off_t)s->ext[b]) != (ssize_t)len) { free(raw); return ents; }
+    by += len;
+    if (len == 0 || raw[len - 1] != 1 || len < 5) { free(raw); continue; }
+    uint8_t* data = (uint8_t*)malloc(len - 1);
+    memcpy(data, raw, len - 1);
+    free(raw);
+    size_t plen = len - 5;
+    if (tpzo_crc32(data, plen) != be32(data + plen) || plen < 2) { free(data); continue; }
+    uint32_t n = be16(data);
+    if (plen < 2 + 2 * (size_t)n) { free(data); continue; }
+    uint16_t* offs = (uint16_t*)malloc(sizeof(uint16_t) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; i++) offs[i] = (uint16_t)be16(data + 2 + 2 * i);
+    const uint8_t* d = data + 2 + 2 * (size_t)n;
+    size_t dl = plen - 2 - 2 * (size_t)n;
+    for (uint32_t i = 0; i < n; i++) {
+      size_t o = offs[i];
+      if (o + 2 > dl) break;
+      uint32_t kl = be16(d + o);
+      if (o + 4 + kl > dl) break;
+      uint32_t vl = be16(d + o + 2 + kl);
+      if (o + 4 + kl + vl > dl) break;
+      if (kl == 0) break; /* is_valid == key non-empty (iterator.rs:50-52) */
+      uint8_t* k = (uint8_t*)malloc(kl);
+      memcpy(k, d + o + 2, kl);
+      uint8_t* v = (uint8_t*)malloc(vl ? vl : 1);
+      memcpy(v, d + o + 4 + kl, vl);
+      acc += k[0] + (vl ? v[vl - 1] : 0);
+      free(k);
+      free(v);
+      ents++;
+    }
+    free(offs);
+    free(data);
+  }
+  *sink += acc;
+  *bytes = by;
+  return ents;
+}
+
+typedef struct {
+  const sstfile* files;
+  uint32_t first, step, n, iters;
+  uint64_t bytes, entries;
+} worker;
+
+static volatile uint64_t g_sink;
+
+static void* worker_main(void* arg) {
+  worker* w = (worker*)arg;
+  for (uint32_t it = 0; it < w->iters; it++)
+    for (uint32_t f = w->first; f < w->n; f += w->step) {
+      uint64_t by = 0;
+      uint64_t e = iter_read_pass(&w->files[f], &g_sink, &by);
+      if (it == 0) { w->bytes += by; w->entries += e; }
+    }
+  return NULL;
+}
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+double tpzo_bench_iter_read(const char* const* paths, uint32_t n_paths, uint32_t threads,
+                            uint32_t iters, uint64_t* bytes, uint64_t* entries) {
+  sstfile* files = (sstfile*)calloc(n_paths, sizeof(sstfile));
+  for (uint32_t i = 0; i < n_paths; i++)
+    if (sst_file_open(paths[i], &files[i]) != 0) { free(files); return -1.0; }
+  if (threads == 0) threads = 1;
+  worker* ws = (worker*)calloc(threads, sizeof(worker));
+  pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  double t0 = now_s();
+  for (uint32_t t = 0; t < threads; t++) {
+    ws[t] = (worker){files, t, threads, n_paths, iters, 0, 0};
+    pthread_create(&th[t], NULL, worker_main, &ws[t]);
+  }
+  uint64_t by = 0, en = 0;
+  for (uint32_t t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    by += ws[t].bytes;
+    en += ws[t].entries;
+  }
+  double dt = now_s() - t0;
+  for (uint32_t i = 0; i < n_paths; i++) { close(files[i].fd); free(files[i].ext); }
+  free(files);
+  free(ws);
+  free(th);
+  *bytes = by;
+  *entries = en;
+  return dt;
+}

@@ -1,0 +1,86 @@
+/*
+ * tpz_oracle.h — CPU restatement of topazdb's SSTable block decode + checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the checker for the HIP path, not part of the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it
+ * (oracle/liboracle.so). The product library (topazdb_amd/libtpz_gpu.so) never links it.
+ *
+ * Parity pinning: the reference is Rust and cannot be built here (no cargo), so
+ * this restatement is pinned by (1) the reference's own generator-based known-answer tests
+ * restated in tests/test_oracle.py, (2) CRC-32 known answers from zlib.crc32 and
+ * (3) fixtures from an independent pure-Python restatement (tests/golden/make_golden.py).
+ *
+ * Every function cites the reference file:line it restates (paths relative to the reference).
+ */
+#ifndef TPZ_ORACLE_H
+#define TPZ_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-block outcome; numbering is shared with include/tpz_gpu.h (tpz_block_status). */
+enum {
+  TPZO_OK = 0,          /* Block::decode Ok                                   */
+  TPZO_EMPTY = 1,       /* Err("data is empty")      src/block/compress.rs:96-98 */
+  TPZO_BAD_TAG = 2,     /* Err("invaild data")       src/block/compress.rs:102   */
+  TPZO_UNSUPPORTED = 3, /* tag 2/3: snappy / lz4     src/block/compress.rs:104-111 */
+  TPZO_CHECKSUM = 4,    /* Err("checksum: ...")      src/checksum.rs:12-21       */
+  TPZO_MALFORMED = 5,   /* the reference panics      src/block.rs:49-59, iterator.rs:74-82 */
+  TPZO_OVERLAP = 6      /* decodes in the reference; exceeds the device's per-block slot */
+};
+
+/* CRC-32/ISO-HDLC bit by bit (crc32fast's function): src/checksum.rs:6-10. */
+uint32_t tpzo_crc32(const uint8_t* p, size_t n);
+
+/* Count pass: entries / key bytes / value bytes the decode pass will emit. */
+void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
+                      uint64_t* n_entries, uint64_t* key_bytes, uint64_t* val_bytes);
+
+/* Block::decode (src/block.rs:46-65) + BlockIterator::seek_to for every index
+ * (src/block/iterator.rs:63-83) over blocks [ext[i], ext[i+1]). Dense outputs in block order:
+ * entries are emitted for TPZO_OK and TPZO_OVERLAP blocks. crc_actual is the CRC the reference
+ * computes over the payload (0 when it never gets that far). Returns 0. */
+int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
+                      uint8_t* status, uint32_t* crc_actual, uint32_t* crc_expected,
+                      uint32_t* count, uint32_t* klen, uint32_t* vlen,
+                      uint8_t* keys, uint8_t* vals);
+
+/* FileObject::open (src/table/file_object.rs:57-78) + SsTable::open (src/table.rs:75-112).
+ * Verifies the whole-file CRC, walks the trailer chain and returns the data-block extents
+ * (ext[0..n_blocks], last = meta_off, src/table.rs:154-161). Returns 0 on success,
+ * -1 file checksum mismatch, -2 malformed trailer, -3 ext_cap too small. */
+int tpzo_sst_parse(const uint8_t* file, size_t len, uint64_t* ext, uint32_t ext_cap,
+                   uint32_t* n_blocks, uint64_t* meta_off, uint64_t* bloom_off);
+
+/* ---- iterator restatement (src/block/iterator.rs, src/table/iterator.rs) ---------------- */
+typedef struct tpzo_sst_iter tpzo_sst_iter;
+
+/* SsTableIterator over an in-memory SST file image (the caller keeps `file` alive). */
+tpzo_sst_iter* tpzo_sst_iter_create(const uint8_t* file, size_t len);
+void tpzo_sst_iter_destroy(tpzo_sst_iter* it);
+int tpzo_sst_iter_seek_to_first(tpzo_sst_iter* it);                      /* :18-42 */
+int tpzo_sst_iter_seek_to_key(tpzo_sst_iter* it, const uint8_t* k, size_t kl); /* :44-72 */
+int tpzo_sst_iter_next(tpzo_sst_iter* it);                               /* :88-95 */
+int tpzo_sst_iter_is_valid(const tpzo_sst_iter* it);                     /* :84-86 */
+const uint8_t* tpzo_sst_iter_key(const tpzo_sst_iter* it, size_t* len);
+const uint8_t* tpzo_sst_iter_value(const tpzo_sst_iter* it, size_t* len);
+uint32_t tpzo_sst_iter_block_idx(const tpzo_sst_iter* it);
+
+/* ---- CPU baseline: benches/sstable_iter_read.rs:60-79 restated --------------------------
+ * SsTableIterator::create_and_seek_to_first + `while is_valid { next }` over SST files on
+ * disk: one pread per block (file_object.rs:23-27), codec copy (compress.rs:103), CRC verify,
+ * offsets Vec, and a malloc+memcpy per key and per value (iterator.rs:78,82). `paths` are
+ * independent SSTs; `threads` workers each own whole files (Arc<SsTable> sharing in the
+ * reference). Returns wall seconds for `iters` full passes; *bytes = encoded block bytes read
+ * per pass, *entries = entries visited per pass. */
+double tpzo_bench_iter_read(const char* const* paths, uint32_t n_paths, uint32_t threads,
+                            uint32_t iters, uint64_t* bytes, uint64_t* entries);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

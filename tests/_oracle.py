@@ -1,0 +1,165 @@
+"""ctypes binding of oracle/liboracle.so (the CPU restatement) — test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+OK, EMPTY, BAD_TAG, UNSUPPORTED, CHECKSUM, MALFORMED, OVERLAP = range(7)
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO) and os.path.exists("/usr/bin/gcc"):
+            build()
+        L = C.CDLL(ORACLE_SO)
+        u8p, u32p, u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+        L.tpzo_crc32.argtypes = [C.c_void_p, C.c_size_t]
+        L.tpzo_crc32.restype = C.c_uint32
+        L.tpzo_batch_sizes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, u64p, u64p, u64p]
+        L.tpzo_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 8
+        L.tpzo_sst_parse.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
+                                     u32p, u64p, u64p]
+        L.tpzo_sst_iter_create.argtypes = [C.c_void_p, C.c_size_t]
+        L.tpzo_sst_iter_create.restype = C.c_void_p
+        for f in ("destroy", "seek_to_first", "next", "is_valid", "block_idx"):
+            getattr(L, "tpzo_sst_iter_" + f).argtypes = [C.c_void_p]
+        L.tpzo_sst_iter_seek_to_key.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.tpzo_sst_iter_key.argtypes = [C.c_void_p, C.POINTER(C.c_size_t)]
+        L.tpzo_sst_iter_key.restype = C.c_void_p
+        L.tpzo_sst_iter_value.argtypes = [C.c_void_p, C.POINTER(C.c_size_t)]
+        L.tpzo_sst_iter_value.restype = C.c_void_p
+        L.tpzo_bench_iter_read.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
+                                           C.c_uint32, u64p, u64p]
+        L.tpzo_bench_iter_read.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def crc32(b: bytes) -> int:
+    buf = np.frombuffer(b, np.uint8) if b else np.zeros(1, np.uint8)
+    return lib().tpzo_crc32(_ptr(buf), len(b))
+
+
+class Decoded:
+    """Dense decode of a batch: per-block status/crc/count, per-entry lengths and bytes."""
+
+    def __init__(self, status, crc_actual, crc_expected, count, klen, vlen, keys, vals):
+        self.status, self.crc_actual, self.crc_expected = status, crc_actual, crc_expected
+        self.count, self.klen, self.vlen, self.keys, self.vals = count, klen, vlen, keys, vals
+        self.entry_base = np.zeros(len(count) + 1, np.int64)
+        np.cumsum(count, out=self.entry_base[1:])
+        self.kpos = np.zeros(len(klen) + 1, np.int64)
+        np.cumsum(klen, out=self.kpos[1:])
+        self.vpos = np.zeros(len(vlen) + 1, np.int64)
+        np.cumsum(vlen, out=self.vpos[1:])
+
+    def entries(self, b: int) -> list[tuple[bytes, bytes]]:
+        out = []
+        for e in range(self.entry_base[b], self.entry_base[b + 1]):
+            out.append((self.keys[self.kpos[e]:self.kpos[e + 1]].tobytes(),
+                        self.vals[self.vpos[e]:self.vpos[e + 1]].tobytes()))
+        return out
+
+
+def decode_batch(src: np.ndarray, ext: np.ndarray) -> Decoded:
+    L = lib()
+    src = np.ascontiguousarray(src, np.uint8)
+    if src.size == 0:
+        src = np.zeros(1, np.uint8)
+    ext = np.ascontiguousarray(ext, np.uint64)
+    nb = len(ext) - 1
+    ne, kb, vb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    L.tpzo_batch_sizes(_ptr(src), _ptr(ext), nb, C.byref(ne), C.byref(kb), C.byref(vb))
+    st = np.zeros(max(nb, 1), np.uint8)
+    ca = np.zeros(max(nb, 1), np.uint32)
+    ce = np.zeros(max(nb, 1), np.uint32)
+    cnt = np.zeros(max(nb, 1), np.uint32)
+    kl = np.zeros(max(ne.value, 1), np.uint32)
+    vl = np.zeros(max(ne.value, 1), np.uint32)
+    keys = np.zeros(max(kb.value, 1), np.uint8)
+    vals = np.zeros(max(vb.value, 1), np.uint8)
+    L.tpzo_decode_batch(_ptr(src), _ptr(ext), nb, _ptr(st), _ptr(ca), _ptr(ce), _ptr(cnt),
+                        _ptr(kl), _ptr(vl), _ptr(keys), _ptr(vals))
+    return Decoded(st[:nb], ca[:nb], ce[:nb], cnt[:nb], kl[:ne.value], vl[:ne.value],
+                   keys[:kb.value], vals[:vb.value])
+
+
+def sst_parse(f: bytes):
+    L = lib()
+    buf = np.frombuffer(f, np.uint8)
+    cap = len(f) // 6 + 2
+    ext = np.zeros(cap, np.uint64)
+    nb, mo, bo = C.c_uint32(), C.c_uint64(), C.c_uint64()
+    rc = L.tpzo_sst_parse(_ptr(buf), len(f), _ptr(ext), cap, C.byref(nb), C.byref(mo), C.byref(bo))
+    if rc != 0:
+        raise ValueError(f"sst_parse failed: {rc}")
+    return ext[:nb.value + 1].copy(), mo.value, bo.value
+
+
+class SstIter:
+    """SsTableIterator restatement over an in-memory SST file (src/table/iterator.rs)."""
+
+    def __init__(self, f: bytes):
+        self._buf = np.frombuffer(f, np.uint8).copy()
+        self._it = lib().tpzo_sst_iter_create(_ptr(self._buf), len(f))
+        assert self._it, "tpzo_sst_iter_create failed"
+
+    def __del__(self):
+        if getattr(self, "_it", None):
+            lib().tpzo_sst_iter_destroy(self._it)
+            self._it = None
+
+    def seek_to_first(self):
+        assert lib().tpzo_sst_iter_seek_to_first(self._it) == 0
+
+    def seek_to_key(self, k: bytes):
+        kb = np.frombuffer(k, np.uint8) if k else np.zeros(1, np.uint8)
+        assert lib().tpzo_sst_iter_seek_to_key(self._it, _ptr(kb), len(k)) == 0
+
+    def next(self):
+        assert lib().tpzo_sst_iter_next(self._it) == 0
+
+    def is_valid(self) -> bool:
+        return bool(lib().tpzo_sst_iter_is_valid(self._it))
+
+    def _get(self, fn) -> bytes:
+        n = C.c_size_t()
+        p = fn(self._it, C.byref(n))
+        return C.string_at(p, n.value) if n.value else b""
+
+    def key(self) -> bytes:
+        return self._get(lib().tpzo_sst_iter_key)
+
+    def value(self) -> bytes:
+        return self._get(lib().tpzo_sst_iter_value)
+
+
+def bench_iter_read(paths: list[str], threads: int, iters: int):
+    """CPU baseline (benches/sstable_iter_read.rs:60-79 restated). Returns (s, bytes, entries)."""
+    arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+    by, en = C.c_uint64(), C.c_uint64()
+    dt = lib().tpzo_bench_iter_read(arr, len(paths), threads, iters, C.byref(by), C.byref(en))
+    if dt < 0:
+        raise RuntimeError("tpzo_bench_iter_read failed")
+    return dt, by.value, en.value

@@ -1,0 +1,468 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures for the SSTable block decode + checksum path.
+
+TEST INFRASTRUCTURE ONLY. This is an independent, pure-Python restatement of topazdb's
+*write* side (it produces the bytes) plus an expectation computed from a pure-Python
+restatement of the *read* side. The C oracle (`oracle/tpz_oracle.c`) and the HIP path are
+both checked against these files, so the fixtures pin the oracle.
+
+Why generated here and not taken from the reference: topazdb is Rust, there is no cargo in
+this image, and the reference's own tests pin behaviour with generators, not
+stored bytes. The generators below are the reference's generators
+(`key_of`/`value_of`, block sizes 10000/128/16, the bench's 1000-key set) re-run on this
+restatement. CRC-32 comes from `zlib.crc32` (CRC-32/ISO-HDLC, the algorithm `crc32fast`
+implements), xxh3_64 from the `xxhash` package (same function as `xxhash-rust` 0.8.5's
+`xxh3_64`), so neither is restated by hand.
+
+Format restated (all integers big-endian unless noted):
+  entry   = u16 klen | key | u16 vlen | value                 src/block/builder.rs:72-81
+  payload = u16 n | u16 off[n] | entries                      src/block.rs:31-40
+  block   = payload | u32 crc32(payload) | u8 tag(=1)          src/block.rs:41-43, src/block/compress.rs:82-89
+  sst     = blocks | meta{u32 off|u16 klen|first_key}* | u32 meta_off
+            | bloom bits | u8 k | u32 bloom_off | u32 crc32(all) src/table/builder.rs:97-141, file_object.rs:33-48
+
+Run:  python tests/golden/make_golden.py   (rewrites tests/golden/*.sst|*.bin|*.json)
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+import random
+import struct
+import zlib
+
+import xxhash
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+TAG_NONE, TAG_SNAPPY, TAG_LZ4 = 1, 2, 3  # src/block/compress.rs:30-35
+
+
+def crc32(b: bytes) -> int:
+    """src/checksum.rs:6-10 (crc32fast) == zlib.crc32."""
+    return zlib.crc32(b) & 0xFFFFFFFF
+
+
+# --------------------------------------------------------------------------- write side
+class BlockBuilder:
+    """src/block/builder.rs:6-57."""
+
+    def __init__(self, target_size: int):
+        self.target = target_size
+        self.data = bytearray()
+        self.offsets: list[int] = []
+        self.size = 0
+
+    def add(self, key: bytes, value: bytes) -> bool:
+        assert len(key) > 0, "key must not be empty"           # :27
+        enc_len = 2 + len(key) + 2 + len(value)                  # :83-85
+        if enc_len + self.size + 2 > self.target:               # :32 fill rule
+            return False
+        self.data += struct.pack(">H", len(key) & 0xFFFF) + key  # :76-77 (as u16 truncation)
+        self.data += struct.pack(">H", len(value) & 0xFFFF) + value
+        self.offsets.append(self.size & 0xFFFF)                  # :37
+        self.size += enc_len
+        return True
+
+    def is_empty(self) -> bool:
+        return self.size == 0
+
+    def build(self) -> tuple[list[int], bytes]:
+        assert not self.is_empty(), "block must be not empty"   # :50
+        return list(self.offsets), bytes(self.data)
+
+
+def block_payload(offsets: list[int], data: bytes) -> bytes:
+    """Block::encode before codec: src/block.rs:31-40."""
+    out = bytearray(struct.pack(">H", len(offsets) & 0xFFFF))
+    for o in offsets:
+        out += struct.pack(">H", o)
+    out += data
+    return bytes(out)
+
+
+def encode_block(offsets: list[int], data: bytes, tag: int = TAG_NONE) -> bytes:
+    """Block::encode (src/block.rs:31-44) with the Uncompress codec (compress.rs:85-89)."""
+    p = block_payload(offsets, data)
+    return p + struct.pack(">I", crc32(p)) + bytes([tag])
+
+
+def bloom_from_keys(hashes: list[int], fpp: float) -> bytes:
+    """src/bloom.rs:48-70 (f64 arithmetic is IEEE in both languages)."""
+    assert 0.0 <= fpp < 1.0
+    n = float(len(hashes))
+    ln2sq = math.log(2.0) * math.log(2.0)        # LN_2.powi(2)
+    m = -(n * math.log(fpp)) / ln2sq
+    k = m / n * ln2sq
+    k = max(1, min(15, int(math.ceil(k)) & 0xFF))
+    filt = bytearray((int(math.ceil(m)) + 7) // 8 + 1)
+    filt[-1] = k
+    limit = (len(filt) - 1) * 8
+    for h in hashes:
+        delta = ((h >> 34) | (h << 30)) & 0xFFFFFFFFFFFFFFFF   # :44-46
+        for _ in range(k):
+            pos = h % limit
+            filt[pos // 8] |= 1 << (pos % 8)
+            h = (h + delta) & 0xFFFFFFFFFFFFFFFF
+    return bytes(filt)
+
+
+def bloom_may_contain(filt: bytes, h: int) -> bool:
+    """src/bloom.rs:72-84."""
+    delta = ((h >> 34) | (h << 30)) & 0xFFFFFFFFFFFFFFFF
+    k = filt[-1]
+    limit = (len(filt) - 1) * 8
+    for _ in range(k):
+        pos = h % limit
+        if not (filt[pos // 8] >> (pos % 8)) & 1:
+            return False
+        h = (h + delta) & 0xFFFFFFFFFFFFFFFF
+    return True
+
+
+class SsTableBuilder:
+    """src/table/builder.rs:17-141 (fpp default 0.1, src/opt.rs:50)."""
+
+    def __init__(self, block_size: int, fpp: float = 0.1, tag: int = TAG_NONE):
+        self.block_size = block_size
+        self.fpp = fpp
+        self.tag = tag
+        self.meta: list[tuple[int, bytes]] = []   # (offset, first_key)
+        self.data = bytearray()
+        self.bb = BlockBuilder(block_size)
+        self.base_key = b""
+        self.hashes: list[int] | None = [] if fpp > 0 else None
+
+    def add(self, key: bytes, value: bytes) -> None:  # :49-64
+        if not self.base_key:
+            self.base_key = bytes(key)
+        if not self.bb.add(key, value):
+            self._block_build()
+            return self.add(key, value)
+        if self.hashes is not None:
+            self.hashes.append(xxhash.xxh3_64_intdigest(key))
+
+    def _block_build(self) -> None:  # :66-85
+        if self.bb.is_empty():
+            return
+        offs, data = self.bb.build()
+        self.bb = BlockBuilder(self.block_size)
+        self.meta.append((len(self.data), self.base_key))
+        self.base_key = b""
+        self.data += encode_block(offs, data, self.tag)
+
+    def build(self) -> bytes:  # :97-130 + FileObject::create_new (file_object.rs:33-48)
+        self._block_build()
+        meta_off = len(self.data)
+        for off, fk in self.meta:                          # table.rs:33-46
+            self.data += struct.pack(">IH", off, len(fk)) + fk
+        self.data += struct.pack(">I", meta_off)
+        if self.hashes is not None:                        # :110-113, :132-141
+            bloom_off = len(self.data)
+            self.data += bloom_from_keys(self.hashes, self.fpp)
+            self.data += struct.pack(">I", bloom_off)
+        body = bytes(self.data)
+        return body + struct.pack(">I", crc32(body))
+
+
+# --------------------------------------------------------------------------- read side
+ST_OK, ST_EMPTY, ST_BAD_TAG, ST_UNSUPPORTED, ST_CHECKSUM, ST_MALFORMED, ST_OVERLAP = range(7)
+
+
+def decode_block(blk: bytes) -> dict:
+    """Block::decode (src/block.rs:46-65) + BlockIterator::seek_to for every idx
+    (src/block/iterator.rs:63-83). `status` names the reference's outcome:
+    Err("data is empty") / Err("invaild data") / snappy-lz4 / Err(checksum) / panic."""
+    r = {"status": ST_OK, "crc_expected": 0, "crc_actual": 0, "entries": []}
+    if len(blk) == 0:
+        r["status"] = ST_EMPTY                             # compress.rs:96-98
+        return r
+    tag = blk[-1]
+    if tag not in (1, 2, 3):
+        r["status"] = ST_BAD_TAG                           # compress.rs:102
+        return r
+    if tag != TAG_NONE:
+        r["status"] = ST_UNSUPPORTED
+        return r
+    data = blk[:-1]
+    if len(data) < 4:                                      # block.rs:49 split_to underflow panics
+        r["status"] = ST_MALFORMED
+        return r
+    payload, crc_e = data[:-4], struct.unpack(">I", data[-4:])[0]
+    r["crc_expected"], r["crc_actual"] = crc_e, crc32(payload)
+    if crc_e != r["crc_actual"]:
+        r["status"] = ST_CHECKSUM                          # checksum.rs:12-21
+        return r
+    if len(payload) < 2:                                   # block.rs:54 get_u16 panics
+        r["status"] = ST_MALFORMED
+        return r
+    n = struct.unpack(">H", payload[:2])[0]
+    if len(payload) < 2 + 2 * n:                           # block.rs:56-59 panics
+        r["status"] = ST_MALFORMED
+        return r
+    offs = [struct.unpack(">H", payload[2 + 2 * i:4 + 2 * i])[0] for i in range(n)]
+    body = payload[2 + 2 * n:]
+    ents = []
+    for o in offs:                                         # iterator.rs:74-82
+        if o + 2 > len(body):
+            r["status"] = ST_MALFORMED
+            break
+        kl = struct.unpack(">H", body[o:o + 2])[0]
+        if o + 2 + kl + 2 > len(body):
+            r["status"] = ST_MALFORMED
+            break
+        key = body[o + 2:o + 2 + kl]
+        vl = struct.unpack(">H", body[o + 2 + kl:o + 4 + kl])[0]
+        if o + 4 + kl + vl > len(body):
+            r["status"] = ST_MALFORMED
+            break
+        ents.append((key, body[o + 4 + kl:o + 4 + kl + vl]))
+    if r["status"] == ST_OK:
+        r["entries"] = ents
+        ktot = sum(len(k) for k, _ in ents)
+        vtot = sum(len(v) for _, v in ents)
+        # Device slot contract (include/tpz_gpu.h): decoded bytes of one block must fit the
+        # block's own extent. Only blocks whose offsets overlap can break it; topazdb's writer
+        # never emits them, the reference iterator decodes them, the device reports OVERLAP.
+        if n * 6 > len(blk) or ktot > len(blk) or vtot > len(blk):
+            r["status"] = ST_OVERLAP
+    return r
+
+
+def sst_open(f: bytes) -> dict:
+    """FileObject::open (file_object.rs:57-78) + SsTable::open (table.rs:75-112)."""
+    body, crc_e = f[:-4], struct.unpack(">I", f[-4:])[0]
+    assert crc32(body) == crc_e, "file checksum"
+    size = len(body)
+    bloom_off = struct.unpack(">I", body[size - 4:])[0]
+    bloom = None if size == bloom_off + 4 else body[bloom_off:size - 4]
+    meta_off = struct.unpack(">I", body[bloom_off - 4:bloom_off])[0]
+    mb = body[meta_off:bloom_off - 4]
+    metas, p = [], 0
+    while p < len(mb):                                     # table.rs:49-59
+        off, kl = struct.unpack(">IH", mb[p:p + 6])
+        metas.append((off, mb[p + 6:p + 6 + kl]))
+        p += 6 + kl
+    ext = [m[0] for m in metas] + [meta_off]               # table.rs:154-161
+    return {"body": body, "metas": metas, "meta_off": meta_off, "ext": ext, "bloom": bloom}
+
+
+def sst_iter_sequence(blocks: list[list[tuple[bytes, bytes]]]) -> list[tuple[bytes, bytes]]:
+    """SsTableIterator::create_and_seek_to_first + next (table/iterator.rs:18-25, 88-95):
+    is_valid == key non-empty (block/iterator.rs:50-52); on an invalid entry move to the next
+    block only if one remains, and stop if that block's first entry is invalid too."""
+    out = []
+    nb = len(blocks)
+    bi, ei = 0, 0
+
+    def valid(b, e):
+        return e < len(blocks[b]) and len(blocks[b][e][0]) > 0
+
+    while valid(bi, ei):
+        out.append(blocks[bi][ei])
+        ei += 1
+        if not valid(bi, ei) and bi < nb - 1:
+            bi, ei = bi + 1, 0
+    return out
+
+
+# --------------------------------------------------------------------------- generators
+def key_of(i: int) -> bytes:        # src/block/tests.rs:22-24, benches/sstable_iter_read.rs:12-14
+    return b"key_%03d" % (i * 5)
+
+
+def value_of(i: int) -> bytes:      # src/block/tests.rs:26-28
+    return b"value_%010d" % i
+
+
+def splitmix64(state: int):
+    while True:
+        state = (state + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        yield z ^ (z >> 31)
+
+
+def rand_bytes(gen, n: int) -> bytes:
+    out = bytearray()
+    while len(out) < n:
+        out += struct.pack("<Q", next(gen))
+    return bytes(out[:n])
+
+
+def zipf_len(rng: random.Random, lo: int, hi: int, s: float) -> int:
+    ws = [1.0 / (k ** s) for k in range(1, hi - lo + 2)]
+    return lo + rng.choices(range(hi - lo + 1), weights=ws)[0]
+
+
+def write(name: str, data: bytes) -> None:
+    with open(os.path.join(HERE, name), "wb") as f:
+        f.write(data)
+
+
+def hexents(ents):
+    return [[k.hex(), v.hex()] for k, v in ents]
+
+
+def digest(ents) -> str:
+    """sha256 over the canonical entry stream: u32le klen | key | u32le vlen | value."""
+    h = hashlib.sha256()
+    for k, v in ents:
+        h.update(struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v)
+    return h.hexdigest()
+
+
+def ents_json(ents):
+    """Full entries for small fixtures, a digest otherwise (keeps each file < 100 KiB)."""
+    return hexents(ents) if sum(len(k) + len(v) for k, v in ents) < 2048 else digest(ents)
+
+
+def sst_fixture(name: str, builder: SsTableBuilder, kvs, probes=()) -> None:
+    for k, v in kvs:
+        builder.add(k, v)
+    f = builder.build()
+    assert len(f) < 100 * 1024, (name, len(f))
+    write(name + ".sst", f)
+    t = sst_open(f)
+    blocks, bl_json = [], []
+    for i in range(len(t["metas"])):
+        blk = t["body"][t["ext"][i]:t["ext"][i + 1]]
+        d = decode_block(blk)
+        assert d["status"] == ST_OK, (name, i, d["status"])
+        blocks.append(d["entries"])
+        bl_json.append({"status": d["status"], "crc": d["crc_actual"], "n": len(d["entries"]),
+                        "entries": ents_json(d["entries"])})
+    seq = sst_iter_sequence(blocks)
+    exp = {
+        "file_len": len(f), "file_crc": struct.unpack(">I", f[-4:])[0],
+        "meta_off": t["meta_off"], "ext": t["ext"],
+        "first_keys": [fk.hex() for _, fk in t["metas"]],
+        "bloom_len": 0 if t["bloom"] is None else len(t["bloom"]),
+        "blocks": bl_json, "sequence": ents_json(seq), "sequence_len": len(seq),
+        "input": ents_json(kvs),
+        "probes": {p.hex(): bloom_may_contain(t["bloom"], xxhash.xxh3_64_intdigest(p))
+                   for p in probes} if t["bloom"] is not None else {},
+    }
+    with open(os.path.join(HERE, name + ".json"), "w") as fj:
+        json.dump(exp, fj, indent=0, sort_keys=True)
+
+
+def main() -> None:
+    # 1. src/block/tests.rs:34-42 — one block, target 10000, 100 generator keys.
+    bb = BlockBuilder(10000)
+    for i in range(100):
+        assert bb.add(key_of(i), value_of(i))
+    offs, data = bb.build()
+    blk = encode_block(offs, data)
+    write("block_100_t10000.bin", blk)
+    d = decode_block(blk)
+    with open(os.path.join(HERE, "block_100_t10000.json"), "w") as fj:
+        json.dump({"offsets": offs, "data": data.hex(), "crc": d["crc_actual"],
+                   "entries": hexents(d["entries"])}, fj, indent=0)
+
+    # 2. src/table/tests.rs:45-55 — block_size 128, 100 keys (+ bloom probes as test_sst_bloom).
+    sst_fixture("sst_100_b128", SsTableBuilder(128),
+                [(key_of(i), value_of(i)) for i in range(100)],
+                probes=[key_of(i) for i in range(0, 120, 7)])
+    # 3. src/table/tests.rs:19-31 and :140-155 — block_size 16, one entry per block.
+    sst_fixture("sst_b16", SsTableBuilder(16),
+                [(b"11", b"11"), (b"22", b"22"), (b"33", b"11"), (b"44", b"22"),
+                 (b"55", b"11"), (b"66", b"22")],
+                probes=[b"11", b"22", b"33", b"44", b"55", b"66"])
+    # 3b. src/table/tests.rs:140-155 (test_sst_bloom): 3 keys in, 44/55/66 must miss.
+    sst_fixture("sst_bloom3", SsTableBuilder(16), [(b"11", b"11"), (b"22", b"22"), (b"33", b"11")],
+                probes=[b"11", b"22", b"33", b"44", b"55", b"66"])
+    # 4. benches/sstable_iter_read.rs:12-38 — 1000 keys, default block_size 4096, Uncompress.
+    sst_fixture("sst_bench_1000", SsTableBuilder(4096),
+                [(key_of(i), value_of(i)) for i in range(1000)])
+    # 5. BASELINE config 2 geometry: 16 B keys (8 B BE counter + 8 B splitmix), 100 B values.
+    g = splitmix64(0x5EED0001)
+    kv = [(struct.pack(">Q", i) + rand_bytes(g, 8), rand_bytes(g, 100)) for i in range(34 * 20)]
+    sst_fixture("sst_4k_k16_v100", SsTableBuilder(4096), kv)
+    # 6. BASELINE config 4: Zipf(1.2) key lengths in [8, 256], 100 B values.
+    rng = random.Random(0x5EED0003)
+    g = splitmix64(0x5EED0003)
+    kv = []
+    for i in range(500):
+        kl = zipf_len(rng, 8, 256, 1.2)
+        kv.append((struct.pack(">Q", i) + rand_bytes(g, kl - 8), rand_bytes(g, 100)))
+    sst_fixture("sst_zipf", SsTableBuilder(4096), kv[:560])
+    # 7. BASELINE config 3: 64 KiB blocks, 32 B keys, 1 KiB values (one block fits < 100 KiB).
+    g = splitmix64(0x5EED0002)
+    kv = [(struct.pack(">Q", i) + rand_bytes(g, 24), rand_bytes(g, 1024)) for i in range(61)]
+    sst_fixture("sst_64k_k32_v1k", SsTableBuilder(65536, fpp=0.1), kv)
+
+    # 8. Negative / edge blocks, one batch with its own extents.
+    cases = []
+    good = blk
+    cases.append(("ok_ref_block", good))
+    flip = bytearray(good)
+    flip[100] ^= 0x10
+    cases.append(("crc_flip_payload", bytes(flip)))
+    flip = bytearray(good)
+    flip[-3] ^= 0x01
+    cases.append(("crc_flip_stored", bytes(flip)))
+    cases.append(("empty", b""))
+    cases.append(("tag0", good[:-1] + b"\x00"))
+    cases.append(("tag4", good[:-1] + b"\x04"))
+    cases.append(("tag255", good[:-1] + b"\xff"))
+    cases.append(("tag_snappy", good[:-1] + b"\x02"))
+    cases.append(("tag_lz4", good[:-1] + b"\x03"))
+    cases.append(("short3", b"\x00\x00\x01"))           # len-1 < 4: split_to panics
+    cases.append(("only_tag", b"\x01"))
+
+    def raw(payload: bytes) -> bytes:
+        return payload + struct.pack(">I", crc32(payload)) + b"\x01"
+
+    cases.append(("n0", raw(b"\x00\x00")))                # zero entries: valid, decodes empty
+    cases.append(("payload1", raw(b"\x00")))              # get_u16 on 1 byte panics
+    cases.append(("n_too_big", raw(struct.pack(">H", 50) + b"\x00" * 20)))
+    e = struct.pack(">H", 3) + b"abc" + struct.pack(">H", 2) + b"xy"
+    cases.append(("off_oob", raw(struct.pack(">HH", 1, 200) + e)))
+    cases.append(("klen_oob", raw(struct.pack(">HH", 1, 0) + struct.pack(">H", 500) + b"abc")))
+    cases.append(("vlen_oob", raw(struct.pack(">HH", 1, 0) + struct.pack(">H", 3) + b"abc"
+                                  + struct.pack(">H", 99) + b"xy")))
+    ents = [(b"k1", b"v1"), (b"", b"empty-key"), (b"k3", b"")]
+    bb2 = bytearray()
+    offs2 = []
+    for k, v in ents:
+        offs2.append(len(bb2))
+        bb2 += struct.pack(">H", len(k)) + k + struct.pack(">H", len(v)) + v
+    cases.append(("empty_key_tombstone", encode_block(offs2, bytes(bb2))))
+    cases.append(("dup_offsets", raw(struct.pack(">H", 6) + struct.pack(">H", 0) * 6
+                                     + struct.pack(">H", 20) + b"K" * 20 + struct.pack(">H", 0))))
+    cases.append(("unsorted_offsets", raw(struct.pack(">HHH", 2, 9, 0) + e + e)))
+    # tiny segments (1-byte keys, empty values) stress segment crossing in 16 B output chunks
+    bb3 = BlockBuilder(4096)
+    for i in range(300):
+        bb3.add(bytes([65 + i % 26]), b"" if i % 3 else bytes([i & 0xFF]))
+    cases.append(("tiny_entries", encode_block(*bb3.build())))
+    # unaligned starts: odd-sized padding block between real blocks
+    cases.append(("ok_again", good))
+
+    src = bytearray()
+    ext = [0]
+    out = []
+    for name, b in cases:
+        src += b
+        ext.append(len(src))
+        d = decode_block(b)
+        out.append({"name": name, "status": d["status"], "crc_expected": d["crc_expected"],
+                    "crc_actual": d["crc_actual"],
+                    "entries": hexents(d["entries"]) if d["status"] in (ST_OK, ST_OVERLAP) else []})
+    write("blocks_edge.bin", bytes(src))
+    with open(os.path.join(HERE, "blocks_edge.json"), "w") as fj:
+        json.dump({"ext": ext, "blocks": out}, fj, indent=0)
+
+    # 9. CRC known answers (pins crc32fast == CRC-32/ISO-HDLC; src/checksum.rs:27-33 string).
+    kat = {s.hex(): crc32(s) for s in [b"", b"a", b"123456789", b"12312nskjdhsdi9823r1y3r9",
+                                        bytes(range(256)) * 5, b"\x00" * 4150, b"\xff" * 17]}
+    with open(os.path.join(HERE, "crc_kat.json"), "w") as fj:
+        json.dump(kat, fj, indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
