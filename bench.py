@@ -1,0 +1,351 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident SSTable block decode + CRC-32 throughput on MI355X.
+
+Metric (BASELINE.json): "GiB/s device-resident SSTable block decode+checksum, 4KiB blocks,
+1 MI355X" = encoded input bytes / decode wall time, inputs already in HBM.
+
+A step = one tpz_decode_blocks call over this rank's whole batch (default 2^20 blocks of the
+"4k" config: block_size 4096, 16 B keys, 100 B values, 4155 B per block; BASELINE.json
+configs[1]). With N GPUs every rank decodes its own 2^20-block shard (round-robin shards of
+one N x 2^20-block data set, no collective on the data path): weak scaling.
+
+Also reported:
+  roofline     algorithmic bytes per step (reads + writes) / kernel time,
+               against the 8.0 TB/s HBM peak; `traffic` from rocprof PMC runs (profiles/),
+               null when not collected in this process.
+  cpu_baseline benches/sstable_iter_read.rs's create_and_read loop restated in C
+               (oracle/liboracle.so, kind "port") over a bounded sample of 64 MiB SST files of
+               the same config, on this host's cores (rank 0, N = 1 only).
+  e2e          H2D + decode + D2H rate from pinned host memory (not the metric).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import struct
+import sys
+import tempfile
+import time
+import zlib
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from topazdb_amd import _lib, synth  # noqa: E402
+from topazdb_amd.batch import DeviceBatch, SlottedColumns, decode_batch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
+GIB = float(1 << 30)
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def block_counts(src: np.ndarray, ext: np.ndarray) -> np.ndarray:
+    """n (u16 BE at the start of each block's payload) for every block."""
+    s = ext[:-1].astype(np.int64)
+    return (src[s].astype(np.int64) << 8) | src[s + 1].astype(np.int64)
+
+
+def algorithmic_bytes(ext: np.ndarray, n_ent: np.ndarray, kbytes: int, vbytes: int) -> int:
+    nb = len(ext) - 1
+    reads = int(ext[-1] - ext[0]) + 8 * nb           # block bytes + extent
+    writes = kbytes + vbytes + 8 * int(n_ent.sum()) + 9 * nb  # columns + kend/vend + count/status/crc
+    return reads + writes
+
+
+def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev) -> None:
+    """Full-size property check on the GPU against the generator's own entries (not the
+    oracle): every block OK, counts, every key/value byte and every end offset."""
+    keys, kpos, vals, vpos = gen
+    nb = len(ext) - 1
+    status = cols.status[:nb]
+    assert int((status != 0).sum()) == 0, "blocks not OK"
+    cnt = cols.count[:nb].cpu().numpy().astype(np.int64)
+    assert (cnt == n_ent).all(), "entry counts"
+    e0 = np.zeros(nb + 1, np.int64)
+    np.cumsum(n_ent, out=e0[1:])
+    bid = np.arange(nb, dtype=np.int64)
+    ext64 = ext[:-1].astype(np.int64)
+    kb = ((ext64 + 63) & ~63) + 128 * bid
+    sb = 16 * (ext64 // 96 + bid)
+    kpos = kpos.astype(np.int64)
+    vpos = vpos.astype(np.int64)
+    step = 65536
+    dkeys = torch.from_numpy(keys[:int(kpos[e0[-1]])]).to(dev)
+    dvals = torch.from_numpy(vals[:int(vpos[e0[-1]])]).to(dev)
+    for lo in range(0, nb, step):
+        hi = min(nb, lo + step)
+        for col, pos, dexp, dend in ((cols.keys, kpos, dkeys, cols.kend),
+                                     (cols.vals, vpos, dvals, cols.vend)):
+            tot = pos[e0[lo + 1:hi + 1]] - pos[e0[lo:hi]]          # bytes per block
+            start_exp = pos[e0[lo:hi]]
+            n = int(tot.sum())
+            if n:
+                t_tot = torch.from_numpy(tot).to(dev)
+                rel = torch.arange(n, device=dev) - torch.repeat_interleave(
+                    torch.cumsum(t_tot, 0) - t_tot, t_tot)
+                got = col[torch.repeat_interleave(torch.from_numpy(kb[lo:hi]).to(dev), t_tot) + rel]
+                exp = dexp[torch.repeat_interleave(torch.from_numpy(start_exp).to(dev), t_tot) + rel]
+                assert torch.equal(got, exp), "column bytes differ"
+            ne = n_ent[lo:hi]
+            m = int(ne.sum())
+            t_ne = torch.from_numpy(ne).to(dev)
+            j = torch.arange(m, device=dev) - torch.repeat_interleave(torch.cumsum(t_ne, 0) - t_ne, t_ne)
+            slot = torch.repeat_interleave(torch.from_numpy(sb[lo:hi]).to(dev), t_ne) + j
+            eidx = torch.repeat_interleave(torch.from_numpy(e0[lo:hi]).to(dev), t_ne) + j
+            tpos = torch.from_numpy(pos).to(dev)
+            exp_end = tpos[eidx + 1] - tpos[torch.repeat_interleave(torch.from_numpy(e0[lo:hi]).to(dev), t_ne)]
+            assert torch.equal(dend[slot].to(torch.int64), exp_end), "end offsets differ"
+
+
+# ------------------------------------------------------------------ CPU baseline
+def write_sst_files(src, ext, gen, n_ent, dirpath, blocks_per_sst, max_files):
+    """Full SST files (blocks | meta | meta_off | bloom | bloom_off | crc32) from the region:
+    SsTableBuilder::build + FileObject::create (src/table/builder.rs:97-141,
+    src/table/file_object.rs:33-48). Bloom = Bloom::from_keys(xxh3_64(key), 0.1)."""
+    import xxhash
+    keys, kpos, _, _ = gen
+    nb = len(ext) - 1
+    e0 = np.zeros(nb + 1, np.int64)
+    np.cumsum(n_ent, out=e0[1:])
+    paths = []
+    for f in range(min(max_files, nb // blocks_per_sst)):
+        lo, hi = f * blocks_per_sst, (f + 1) * blocks_per_sst
+        base = int(ext[lo])
+        body = bytearray(src[base:int(ext[hi])].tobytes())
+        meta_off = len(body)
+        meta = bytearray()
+        for b in range(lo, hi):
+            k0 = e0[b]
+            fk = keys[int(kpos[k0]):int(kpos[k0 + 1])].tobytes()
+            meta += struct.pack(">IH", int(ext[b]) - base, len(fk)) + fk
+        body += meta + struct.pack(">I", meta_off)
+        bloom_off = len(body)
+        hs = np.array([xxhash.xxh3_64_intdigest(keys[int(kpos[e]):int(kpos[e + 1])].tobytes())
+                       for e in range(int(e0[lo]), int(e0[hi]))], np.uint64)
+        n = float(len(hs))
+        ln2sq = np.log(2.0) ** 2
+        m = -(n * np.log(0.1)) / ln2sq
+        k = max(1, min(15, int(np.ceil(m / n * ln2sq))))
+        filt = np.zeros((int(np.ceil(m)) + 7) // 8 + 1, np.uint8)
+        filt[-1] = k
+        limit = np.uint64((len(filt) - 1) * 8)
+        h = hs.copy()
+        delta = (h >> np.uint64(34)) | (h << np.uint64(30))
+        for _ in range(k):
+            pos = (h % limit).astype(np.int64)
+            np.bitwise_or.at(filt, pos // 8, (1 << (pos % 8)).astype(np.uint8))
+            h = h + delta
+        body += filt.tobytes() + struct.pack(">I", bloom_off)
+        body += struct.pack(">I", zlib.crc32(bytes(body)) & 0xFFFFFFFF)
+        p = os.path.join(dirpath, f"{f}.sst")
+        with open(p, "wb") as fh:
+            fh.write(body)
+        paths.append(p)
+    return paths
+
+
+def cpu_baseline(src, ext, gen, n_ent, threads, target_s=12.0):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    tmp = tempfile.mkdtemp(prefix="tpz_cpu_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    per_sst = 16128  # 64 MiB SST (TABLE_CAPACITY, src/table/builder.rs:27) of 4155 B blocks
+    per_sst = min(per_sst, (len(ext) - 1) // max(threads, 1))
+    paths = write_sst_files(src, ext, gen, n_ent, tmp, per_sst, threads)
+    try:
+        dt1, by1, _ = O.bench_iter_read(paths[:1], 1, 1)          # calibrate
+        iters = max(1, int(target_s / max(dt1 * len(paths) / threads, 1e-3)))
+        dt, by, en = O.bench_iter_read(paths, threads, iters)
+        single = by1 / dt1 / GIB
+    finally:
+        for p in paths:
+            os.unlink(p)
+        os.rmdir(tmp)
+    return {"value": round(by * iters / dt / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{len(paths)} SST files x {per_sst} blocks (64 MiB each, 4k config), "
+                      f"{iters} pass(es), one file per thread, {dt:.1f} s; "
+                      f"single-thread {single:.3f} GiB/s",
+            "value_1core": round(single, 3)}
+
+
+# ------------------------------------------------------------------ H2D/D2H-inclusive
+def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
+    """Pinned host blocks -> H2D -> decode -> D2H of all columns, chunked and double-buffered
+    over two streams. Returns GiB/s of encoded input."""
+    nb = len(ext) - 1
+    h_src = torch.from_numpy(src).pin_memory()
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    bufs = []
+    for i in range(2):
+        cb = min(chunk_blocks, nb)
+        cap = int(ext[cb] - ext[0]) + 64 if cb < nb else int(ext[-1])
+        cap = max(cap, int(max(ext[min(k + cb, nb)] - ext[k] for k in range(0, nb, cb))))
+        d_src = torch.empty(cap + 64, dtype=torch.uint8, device=dev)
+        d_ext = torch.empty(cb + 1, dtype=torch.int64, device=dev)
+        cols = SlottedColumns(cb, cap, dev.index)
+        h_cols = {k: torch.empty(getattr(cols, k).numel(), dtype=getattr(cols, k).dtype).pin_memory()
+                  for k in ("keys", "vals", "kend", "vend", "count", "status", "crc")}
+        bufs.append((d_src, d_ext, cols, h_cols))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for ci, lo in enumerate(range(0, nb, chunk_blocks)):
+        hi = min(nb, lo + chunk_blocks)
+        s = streams[ci & 1]
+        d_src, d_ext, cols, h_cols = bufs[ci & 1]
+        base, end = int(ext[lo]), int(ext[hi])
+        e = torch.from_numpy((ext[lo:hi + 1] - ext[lo]).astype(np.int64))
+        with torch.cuda.stream(s):
+            d_src[:end - base].copy_(h_src[base:end], non_blocking=True)
+            d_ext[:hi - lo + 1].copy_(e, non_blocking=True)
+            ctx.decode_ptrs(d_src.data_ptr(), d_ext.data_ptr(), hi - lo, end - base,
+                            cols.ptrs(), s.cuda_stream)
+            kc = _lib.col_capacity(end - base, hi - lo)
+            sc = _lib.slot_capacity(end - base, hi - lo)
+            for k, n in (("keys", kc), ("vals", kc), ("kend", sc), ("vend", sc),
+                         ("count", hi - lo), ("status", hi - lo), ("crc", hi - lo)):
+                h_cols[k][:n].copy_(getattr(cols, k)[:n], non_blocking=True)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    return float(ext[-1] - ext[0]) / dt / GIB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="4k", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    nb = args.blocks or ({"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}[args.config])
+    t0 = time.time()
+    # round-robin shard r of an N x nb data set: each rank generates its own blocks
+    seed = synth.CONFIGS[args.config]["seed"] + 7919 * rank
+    n_gen = (34 * nb) if synth.CONFIGS[args.config]["klen"] is None else None
+    if n_gen is None:
+        cfg = synth.CONFIGS[args.config]
+        n_gen = (cfg["block_size"] - 2) // (4 + cfg["klen"] + cfg["vlen"]) * nb
+    gen = synth.entries(args.config, n_gen, seed)
+    src, ext = synth.build_blocks(*gen, synth.CONFIGS[args.config]["block_size"])
+    ext = ext[:nb + 1].copy()
+    src = src[:int(ext[-1])]
+    n_ent = block_counts(src, ext)
+    kpos, vpos = gen[1], gen[3]
+    etot = int(n_ent.sum())
+    kbytes, vbytes = int(kpos[etot]), int(vpos[etot])
+    log(rank, f"generated {nb} blocks ({src.nbytes / GIB:.2f} GiB) in {time.time() - t0:.1f} s")
+
+    ctx = _lib.Context(local)
+    ctx.reserve(nb)
+    batch = DeviceBatch(src, ext, local)
+    cols = SlottedColumns(nb, batch.src_bytes, local)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        decode_batch(ctx, batch, cols, stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        decode_batch(ctx, batch, cols, stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t_start
+    ev_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([wall, ev_ms], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, ev_ms_max = float(t[0]), float(t[1])
+    in_bytes = float(ext[-1] - ext[0])
+    total_in = in_bytes * world
+    value = total_in * args.steps / wall_max / GIB
+    alg = algorithmic_bytes(ext, n_ent, kbytes, vbytes)
+    achieved = alg / (ev_ms_max * 1e-3) / 1e9
+
+    if not args.no_validate:
+        validate(cols, ext, n_ent, gen, dev)
+        log(rank, "validation: all blocks OK, every key/value byte and end offset matches")
+
+    e2e = None
+    if not args.no_e2e and rank == 0:
+        try:
+            e2e = round(e2e_rate(ctx, src, ext, dev), 2)
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"e2e measurement failed: {ex}")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(src, ext, gen, n_ent, threads)
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("blocks") == nb:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "GiB/s device-resident SSTable block decode+checksum, 4KiB blocks, 1 MI355X",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}: {nb} blocks/GPU x {int(np.median(np.diff(ext)))} B "
+                                   f"median, {n_ent.mean():.1f} entries/block, tag 1 (Uncompress)",
+                       "blocks_per_gpu": nb, "input_bytes_per_gpu": int(in_bytes),
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": alg,
+                         "kernel_ms": round(ev_ms_max, 4)},
+            "cpu_baseline": cpu,
+            "e2e_h2d_d2h_gib_s": e2e,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * tpz_gpu.h — C ABI of the MI355X (gfx950) SSTable block decode + checksum path.
+ *
+ * This is the drop-in boundary for topazdb's read hot path. The reference has no FFI (it is a
+ * plain Rust API); each entry point below replaces the reference items it names, and
+ * INTEGRATION.md shows the `extern "C"` binding a topazdb maintainer adds on the Rust side.
+ *
+ *   tpz_decode_blocks       SsTable::read_block (src/table.rs:154-164) batched over many
+ *                           blocks -> Block::decode (src/block.rs:46-65) -> compress::decode
+ *                           tag dispatch (src/block/compress.rs:95-113) -> checksum::
+ *                           verify_checksum (src/checksum.rs:12-21) -> every
+ *                           BlockIterator::seek_to materialised (src/block/iterator.rs:63-83)
+ *   tpz_format_block_error  the reference's error strings (checksum.rs:18-21, compress.rs:97,102)
+ *
+ * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
+ * device; h_* are host pointers. `stream` is a hipStream_t passed as void* (NULL = default).
+ * Every call is asynchronous on `stream` unless it says otherwise; the library never frees
+ * caller memory and holds no global mutable state (one context per device, many host threads
+ * may share it if each uses its own stream).
+ */
+#ifndef TPZ_GPU_H
+#define TPZ_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- API return codes ------------------------------------------------------------------- */
+typedef enum {
+  TPZ_SUCCESS = 0,
+  TPZ_ERR_INVALID_ARG = -1, /* null pointer, inconsistent sizes                               */
+  TPZ_ERR_HIP = -2,         /* a HIP runtime call failed (tpz_last_error has the text)        */
+  TPZ_ERR_NO_DEVICE = -3,   /* no gfx950 device with that index                               */
+  TPZ_ERR_NOMEM = -4
+} tpz_err;
+
+/* ---- per-block outcome (written to columns.status[i]) ------------------------------------
+ * Maps one-to-one onto what Block::decode + iterating every entry does in the reference. */
+typedef enum {
+  TPZ_BLOCK_OK = 0,                /* Ok(Block); all entries decoded                         */
+  TPZ_BLOCK_EMPTY = 1,             /* Err("data is empty")          compress.rs:96-98        */
+  TPZ_BLOCK_BAD_TAG = 2,           /* Err("invaild data")           compress.rs:102          */
+  TPZ_BLOCK_UNSUPPORTED_CODEC = 3, /* tag 2 (snappy) / 3 (lz4): not decoded on device yet    */
+  TPZ_BLOCK_CHECKSUM_MISMATCH = 4, /* Err("checksum: expected E, actual A") checksum.rs:18-21 */
+  TPZ_BLOCK_MALFORMED = 5,         /* CRC-valid, but the reference panics on it: payload too
+                                      short for n/offsets (block.rs:49-59) or an entry out of
+                                      range (iterator.rs:74-82)                              */
+  TPZ_BLOCK_OVERLAP = 6,           /* CRC-valid and decodable by the reference, but entries
+                                      overlap so the decoded bytes exceed the block's slot:
+                                      6*n > len or key bytes > len or value bytes > len.
+                                      topazdb's BlockBuilder never writes such a block.      */
+  TPZ_BLOCK_TOO_LARGE = 7          /* len > TPZ_MAX_BLOCK_BYTES or n > TPZ_MAX_BLOCK_ENTRIES */
+} tpz_block_status;
+
+#define TPZ_MAX_BLOCK_BYTES 86000u
+#define TPZ_MAX_BLOCK_ENTRIES 2048u
+
+/* ---- batch input -------------------------------------------------------------------------
+ * Encoded blocks back to back in one device buffer (an SST data region [0, meta_off), or the
+ * data regions of many SSTs concatenated). Block i is d_src[d_ext[i] .. d_ext[i+1]); d_ext has
+ * n_blocks+1 entries and is non-decreasing. src_bytes = d_ext[n_blocks] (host copy). */
+typedef struct {
+  const uint8_t* d_src;
+  const uint64_t* d_ext;
+  uint32_t n_blocks;
+  uint64_t src_bytes;
+} tpz_batch;
+
+/* ---- decoded columns (the "slotted" layout) ----------------------------------------------
+ * No global prefix pass: every block owns a slot derived from its input extent, so blocks
+ * decode independently (and shard across GPUs) with no cross-block communication.
+ *   keys / vals : block i's key bytes are packed at keys[tpz_key_base(ext[i], i) ...
+ *                 + key_bytes), same for values at vals[tpz_key_base(ext[i], i) ...]
+ *   kend / vend : entry j of block i (j < count[i]) has its inclusive end offsets, relative to
+ *                 the block's base, at kend[tpz_slot_base(ext[i], i) + j]:
+ *                 key_j = keys[kb + (j ? kend[s+j-1] : 0) .. kb + kend[s+j]]
+ *   count[i]    : entries in block i (n) for OK and OVERLAP, else 0
+ *   status[i]   : tpz_block_status
+ *   crc[i]      : CRC-32 the device computed over the payload (valid for OK, MALFORMED,
+ *                 OVERLAP, CHECKSUM_MISMATCH; the stored one is the payload's trailing u32)
+ * Bytes of a slot beyond the block's own data are unspecified. */
+typedef struct {
+  uint8_t* d_keys;   /* capacity tpz_col_capacity(src_bytes, n_blocks) bytes   */
+  uint8_t* d_vals;   /* same capacity                                          */
+  uint32_t* d_kend;  /* capacity tpz_slot_capacity(src_bytes, n_blocks) u32     */
+  uint32_t* d_vend;  /* same capacity                                          */
+  uint32_t* d_count; /* n_blocks */
+  uint8_t* d_status; /* n_blocks */
+  uint32_t* d_crc;   /* n_blocks */
+} tpz_columns;
+
+static inline uint64_t tpz_key_base(uint64_t ext_i, uint64_t i) {
+  return ((ext_i + 63u) & ~(uint64_t)63u) + 128u * i;
+}
+static inline uint64_t tpz_slot_base(uint64_t ext_i, uint64_t i) {
+  return 16u * (ext_i / 96u + i);
+}
+static inline uint64_t tpz_col_capacity(uint64_t src_bytes, uint64_t n_blocks) {
+  return tpz_key_base(src_bytes, n_blocks) + 64u;
+}
+static inline uint64_t tpz_slot_capacity(uint64_t src_bytes, uint64_t n_blocks) {
+  return tpz_slot_base(src_bytes, n_blocks) + 16u;
+}
+
+/* Exported copies of the layout helpers for FFI callers that cannot use static inline. */
+uint64_t tpz_layout_key_base(uint64_t ext_i, uint64_t i);
+uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i);
+uint64_t tpz_layout_col_capacity(uint64_t src_bytes, uint64_t n_blocks);
+uint64_t tpz_layout_slot_capacity(uint64_t src_bytes, uint64_t n_blocks);
+
+/* ---- context ------------------------------------------------------------------------------ */
+typedef struct tpz_ctx tpz_ctx;
+
+/* Creates a context on HIP device `device` (uploads the CRC tables, sizes the launch grid for
+ * the device's CU count). Fails with TPZ_ERR_NO_DEVICE unless the device is gfx950. */
+tpz_err tpz_ctx_create(int device, tpz_ctx** out);
+void tpz_ctx_destroy(tpz_ctx* ctx);
+
+/* Pre-sizes the context's device workspace for batches of up to max_blocks blocks so that
+ * tpz_decode_blocks never allocates (needed before capturing it in a hipGraph). */
+tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks);
+
+/* ---- the hot path ------------------------------------------------------------------------ */
+/* Checksum-verify and decode every block of `batch` into `out`. Asynchronous on `stream`;
+ * per-block outcomes land in out->d_status (no host sync, no host-visible error for a bad
+ * block: that is data, not an API failure). */
+tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* out,
+                          void* stream);
+
+/* ---- host write side (inputs for benches and the table facade) ---------------------------
+ * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule
+ * (src/block/builder.rs:26-41) and Block::encode + Uncompress (src/block.rs:31-44,
+ * src/block/compress.rs:85-89): packs entries e (key = keys[kpos[e]..kpos[e+1]), value likewise)
+ * into blocks written back to back into h_out, block i = [ext[i], ext[i+1]). Host memory only.
+ * Returns TPZ_ERR_INVALID_ARG for an empty key or an entry no block can hold, TPZ_ERR_NOMEM
+ * when out_cap / ext_cap are too small. */
+int tpz_build_blocks(const uint8_t* h_keys, const uint64_t* h_kpos, const uint8_t* h_vals,
+                     const uint64_t* h_vpos, uint64_t n_entries, uint32_t block_size,
+                     uint8_t* h_out, uint64_t out_cap, uint64_t* h_ext, uint64_t ext_cap,
+                     uint64_t* n_blocks, uint64_t* out_len);
+/* CRC-32/ISO-HDLC on the host (checksum::calculate_checksum, src/checksum.rs:6-10). */
+uint32_t tpz_host_crc32(const uint8_t* h_buf, uint64_t len);
+
+/* ---- errors ------------------------------------------------------------------------------ */
+/* Writes the reference's error text for a block outcome into buf (NUL-terminated):
+ * "data is empty", "invaild data", "checksum: expected E, actual A" (decimal, as Rust's {}),
+ * "unsupported codec", "malformed block", "overlapping entries", "block too large", "" for OK.
+ * Returns the text length. */
+int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actual, char* buf,
+                           size_t cap);
+/* Last HIP error text seen by this thread (empty if none). */
+const char* tpz_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPZ_GPU_H */

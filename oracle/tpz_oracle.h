@@ -36,6 +36,9 @@ enum {
 /* CRC-32/ISO-HDLC bit by bit (crc32fast's function): src/checksum.rs:6-10. */
 uint32_t tpzo_crc32(const uint8_t* p, size_t n);
 
+/* The same CRC via PCLMULQDQ folding (crc32fast's x86 algorithm); used by the CPU baseline. */
+uint32_t tpzo_crc32_fast(const uint8_t* p, size_t n);
+
 /* Count pass: entries / key bytes / value bytes the decode pass will emit. */
 void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint64_t* n_entries, uint64_t* key_bytes, uint64_t* val_bytes);

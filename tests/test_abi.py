@@ -1,0 +1,111 @@
+"""CPU-side checks of the C-ABI library (no GPU compute): it loads, exports every function
+include/tpz_gpu.h declares, its layout helpers and error strings match the contract, and the
+host write path produces the same bytes as the independent Python restatement."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from topazdb_amd import _lib, synth
+
+import importlib.util
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+MG = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(MG)
+
+
+def test_library_exports_every_header_function():
+    L = _lib.lib()
+    names = _lib.header_functions()
+    assert "tpz_decode_blocks" in names and "tpz_ctx_create" in names
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_layout_helpers_match_python():
+    L = _lib.lib()
+    rng = np.random.default_rng(1)
+    for _ in range(200):
+        e, i = int(rng.integers(0, 1 << 40)), int(rng.integers(0, 1 << 24))
+        assert L.tpz_layout_key_base(e, i) == _lib.key_base(e, i)
+        assert L.tpz_layout_slot_base(e, i) == _lib.slot_base(e, i)
+        assert L.tpz_layout_col_capacity(e, i) == _lib.col_capacity(e, i)
+        assert L.tpz_layout_slot_capacity(e, i) == _lib.slot_capacity(e, i)
+
+
+def test_slots_never_overlap():
+    """Worst case a block may emit under the slot contract: 16-byte chunked key/value bytes
+    up to len, and floor(len/6) entries; consecutive slots must stay disjoint."""
+    rng = np.random.default_rng(2)
+    lens = np.concatenate([rng.integers(0, 70000, 3000), rng.integers(0, 40, 3000),
+                           np.full(100, 4155), np.arange(0, 200)])
+    rng.shuffle(lens)
+    ext = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=ext[1:])
+    n = len(lens)
+    for i in range(n):
+        ln = int(lens[i])
+        kb, kb1 = _lib.key_base(int(ext[i]), i), _lib.key_base(int(ext[i + 1]), i + 1)
+        assert kb % 64 == 0
+        assert kb + ((ln + 15) & ~15) <= kb1
+        sb, sb1 = _lib.slot_base(int(ext[i]), i), _lib.slot_base(int(ext[i + 1]), i + 1)
+        assert sb + ln // 6 <= sb1
+    assert _lib.key_base(int(ext[-1]), n) <= _lib.col_capacity(int(ext[-1]), n)
+    assert _lib.slot_base(int(ext[-1]), n) <= _lib.slot_capacity(int(ext[-1]), n)
+
+
+def test_error_strings_match_reference():
+    """src/checksum.rs:17-20, src/block/compress.rs:97,102."""
+    assert _lib.format_block_error(_lib.BLOCK_OK) == ""
+    assert _lib.format_block_error(_lib.BLOCK_EMPTY) == "data is empty"
+    assert _lib.format_block_error(_lib.BLOCK_BAD_TAG) == "invaild data"
+    assert (_lib.format_block_error(_lib.BLOCK_CHECKSUM_MISMATCH, 123, 4294967295)
+            == "checksum: expected 123, actual 4294967295")
+
+
+def test_host_crc_matches_oracle():
+    L = _lib.lib()
+    L.tpz_host_crc32.argtypes = [C.c_void_p, C.c_uint64]
+    L.tpz_host_crc32.restype = C.c_uint32
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 7, 8, 9, 100, 4150, 65000]:
+        b = rng.bytes(n)
+        a = np.frombuffer(b, np.uint8) if n else np.zeros(1, np.uint8)
+        assert L.tpz_host_crc32(a.ctypes.data, n) == O.crc32(b)
+
+
+@pytest.mark.parametrize("block_size", [32, 128, 4096, 10000])
+def test_host_builder_matches_python_restatement(block_size):
+    keys, kpos, vals, vpos = synth.reference_bench_entries(300)
+    src, ext = synth.build_blocks(keys, kpos, vals, vpos, block_size)
+    t = MG.SsTableBuilder(block_size, fpp=-1.0)
+    for i in range(300):
+        t.add(keys[kpos[i]:kpos[i + 1]].tobytes(), vals[vpos[i]:vpos[i + 1]].tobytes())
+    t._block_build()
+    assert src.tobytes() == bytes(t.data)
+    assert ext[:-1].tolist() == [m[0] for m in t.meta]
+
+
+@pytest.mark.parametrize("config,nb", [("4k", 40), ("zipf", 40), ("64k", 3)])
+def test_synth_regions_decode_on_oracle(config, nb):
+    src, ext = synth.make_region(config, nb)
+    d = O.decode_batch(src, ext)
+    assert (d.status == O.OK).all()
+    if config == "4k":
+        assert (np.diff(ext) == 4155).all() and (d.count == 34).all()
+    if config == "64k":
+        assert (np.diff(ext) == 64789).all() and (d.count == 61).all()
+    n_gen = 34 * nb if config == "zipf" else int(d.count.sum())  # as make_region generates
+    keys, kpos, vals, vpos = synth.entries(config, n_gen)
+    kpos, vpos = kpos[:int(d.count.sum()) + 1], vpos[:int(d.count.sum()) + 1]
+    assert d.keys.tobytes() == keys[:int(kpos[-1])].tobytes()
+    assert d.vals.tobytes() == vals[:int(vpos[-1])].tobytes()
+
+
+def test_product_library_does_not_link_the_oracle():
+    so = open(_lib.LIB_PATH, "rb").read()
+    assert b"tpzo_" not in so and b"liboracle" not in so

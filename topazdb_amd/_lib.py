@@ -1,0 +1,136 @@
+"""ctypes binding of topazdb_amd/libtpz_gpu.so (the C ABI in include/tpz_gpu.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no gfx950 device is
+visible, these calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libtpz_gpu.so")
+HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
+
+# tpz_err
+SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
+# tpz_block_status
+(BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
+ BLOCK_MALFORMED, BLOCK_OVERLAP, BLOCK_TOO_LARGE) = range(8)
+MAX_BLOCK_BYTES = 86000
+MAX_BLOCK_ENTRIES = 2048
+
+
+class TpzError(RuntimeError):
+    pass
+
+
+class Batch(C.Structure):
+    _fields_ = [("d_src", C.c_void_p), ("d_ext", C.c_void_p), ("n_blocks", C.c_uint32),
+                ("src_bytes", C.c_uint64)]
+
+
+class Columns(C.Structure):
+    _fields_ = [("d_keys", C.c_void_p), ("d_vals", C.c_void_p), ("d_kend", C.c_void_p),
+                ("d_vend", C.c_void_p), ("d_count", C.c_void_p), ("d_status", C.c_void_p),
+                ("d_crc", C.c_void_p)]
+
+
+_lib = None
+
+
+def header_functions() -> list[str]:
+    """Names of every function include/tpz_gpu.h declares (non-inline)."""
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"static inline[^{]*\{[^}]*\}", "", src)
+    return re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(tpz_[a-z_0-9]+)\s*\(", src, flags=re.M)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TpzError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C "
+                           "topazdb_amd/csrc); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        L.tpz_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.tpz_ctx_create.restype = C.c_int
+        L.tpz_ctx_destroy.argtypes = [C.c_void_p]
+        L.tpz_ctx_destroy.restype = None
+        L.tpz_ctx_reserve.argtypes = [C.c_void_p, C.c_uint32]
+        L.tpz_decode_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
+                                        C.c_void_p]
+        L.tpz_decode_blocks.restype = C.c_int
+        L.tpz_format_block_error.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_char_p,
+                                             C.c_size_t]
+        L.tpz_last_error.restype = C.c_char_p
+        for f in ("key_base", "slot_base", "col_capacity", "slot_capacity"):
+            fn = getattr(L, "tpz_layout_" + f)
+            fn.argtypes = [C.c_uint64, C.c_uint64]
+            fn.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SUCCESS:
+        raise TpzError(f"{what} failed ({rc}): {lib().tpz_last_error().decode()}")
+
+
+def format_block_error(status: int, crc_expected: int = 0, crc_actual: int = 0) -> str:
+    buf = C.create_string_buffer(128)
+    lib().tpz_format_block_error(status, crc_expected, crc_actual, buf, 128)
+    return buf.value.decode()
+
+
+# layout (mirrors the static inline helpers of include/tpz_gpu.h)
+def key_base(ext_i, i):
+    return ((ext_i + 63) & ~63) + 128 * i
+
+
+def slot_base(ext_i, i):
+    return 16 * (ext_i // 96 + i)
+
+
+def col_capacity(src_bytes: int, n_blocks: int) -> int:
+    return key_base(src_bytes, n_blocks) + 64
+
+
+def slot_capacity(src_bytes: int, n_blocks: int) -> int:
+    return slot_base(src_bytes, n_blocks) + 16
+
+
+class Context:
+    """One tpz_ctx per device (tpz_ctx_create / tpz_ctx_destroy)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        h = C.c_void_p()
+        check(lib().tpz_ctx_create(device, C.byref(h)), "tpz_ctx_create")
+        self.handle = h
+
+    def reserve(self, max_blocks: int) -> None:
+        check(lib().tpz_ctx_reserve(self.handle, max_blocks), "tpz_ctx_reserve")
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().tpz_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int, cols: dict,
+                    stream: int = 0) -> None:
+        """tpz_decode_blocks on raw device pointers; cols maps field name -> device pointer."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        c = Columns(cols["keys"], cols["vals"], cols["kend"], cols["vend"], cols["count"],
+                    cols["status"], cols["crc"])
+        check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
+              "tpz_decode_blocks")

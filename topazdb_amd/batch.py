@@ -1,0 +1,144 @@
+"""Device batches and decoded columns (torch tensors are the HBM allocator only).
+
+`decode_batch` is the batched replacement for calling SsTable::read_block + Block::decode +
+BlockIterator over every block (src/table.rs:154-164, src/block.rs:46-65,
+src/block/iterator.rs:63-83): it uploads (if needed) and decodes a whole batch of encoded
+blocks on the GPU through tpz_decode_blocks.
+
+`SlottedColumns.dense()` turns the slotted device layout (include/tpz_gpu.h) into dense
+per-entry arrays in block order, vectorised with numpy; the parity tests and the table
+facade use it.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import BLOCK_OK, Context
+
+
+def _dev(device: int) -> torch.device:
+    return torch.device("cuda", device)
+
+
+class DeviceBatch:
+    """Encoded blocks resident in HBM: src bytes + n_blocks+1 extents (tpz_batch)."""
+
+    def __init__(self, src, ext, device: int = 0):
+        dev = _dev(device)
+        if isinstance(src, np.ndarray) or isinstance(src, (bytes, bytearray, memoryview)):
+            a = np.frombuffer(src, np.uint8) if not isinstance(src, np.ndarray) else src
+            src = torch.from_numpy(np.ascontiguousarray(a, np.uint8)).to(dev)
+        if isinstance(ext, np.ndarray) or isinstance(ext, (list, tuple)):
+            e = np.ascontiguousarray(np.asarray(ext, np.uint64)).view(np.int64)
+            ext_host = e.view(np.uint64)
+            ext = torch.from_numpy(e.copy()).to(dev)
+        else:
+            ext_host = ext.cpu().numpy().view(np.uint64)
+        assert src.dtype == torch.uint8 and src.is_cuda and ext.dtype == torch.int64 and ext.is_cuda
+        if src.numel() == 0:
+            src = torch.zeros(16, dtype=torch.uint8, device=dev)
+        self.src, self.ext = src, ext
+        self.ext_host = np.ascontiguousarray(ext_host, np.uint64)
+        self.n_blocks = len(self.ext_host) - 1
+        self.src_bytes = int(self.ext_host[-1]) if self.n_blocks >= 0 else 0
+        assert self.src_bytes <= src.numel()
+
+
+class SlottedColumns:
+    """Device output buffers in the slotted layout of include/tpz_gpu.h (tpz_columns)."""
+
+    def __init__(self, n_blocks: int, src_bytes: int, device: int = 0):
+        dev = _dev(device)
+        cap = _lib.col_capacity(src_bytes, n_blocks)
+        scap = _lib.slot_capacity(src_bytes, n_blocks)
+        nb = max(n_blocks, 1)
+        self.keys = torch.empty(cap, dtype=torch.uint8, device=dev)
+        self.vals = torch.empty(cap, dtype=torch.uint8, device=dev)
+        self.kend = torch.empty(scap, dtype=torch.int32, device=dev)
+        self.vend = torch.empty(scap, dtype=torch.int32, device=dev)
+        self.count = torch.empty(nb, dtype=torch.int32, device=dev)
+        self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
+        self.crc = torch.empty(nb, dtype=torch.int32, device=dev)
+        self.n_blocks = n_blocks
+
+    def ptrs(self) -> dict:
+        return {k: getattr(self, k).data_ptr() for k in
+                ("keys", "vals", "kend", "vend", "count", "status", "crc")}
+
+    def meta_host(self):
+        nb = self.n_blocks
+        return (self.status[:nb].cpu().numpy(), self.crc[:nb].cpu().numpy().view(np.uint32),
+                self.count[:nb].cpu().numpy().view(np.uint32))
+
+    def dense(self, ext_host: np.ndarray) -> "DenseDecode":
+        """Gather every OK block's entries into dense arrays (block order)."""
+        status, crc, count = self.meta_host()
+        nb = self.n_blocks
+        ext = np.asarray(ext_host[:nb], np.int64)
+        bid = np.arange(nb, dtype=np.int64)
+        n_ok = np.where(status == BLOCK_OK, count, 0).astype(np.int64)
+        ebase = np.zeros(nb + 1, np.int64)
+        np.cumsum(n_ok, out=ebase[1:])
+        total = int(ebase[-1])
+        eblk = np.repeat(bid, n_ok)
+        j = np.arange(total, dtype=np.int64) - ebase[eblk]
+        sb = 16 * (ext // 96 + bid)
+        kb = ((ext + 63) & ~63) + 128 * bid
+        slot = sb[eblk] + j
+        kend_d = self.kend.cpu().numpy().view(np.uint32)
+        vend_d = self.vend.cpu().numpy().view(np.uint32)
+        ke = kend_d[slot].astype(np.int64)
+        ve = vend_d[slot].astype(np.int64)
+        first = j == 0
+        ks = np.where(first, 0, kend_d[np.maximum(slot - 1, 0)].astype(np.int64))
+        vs = np.where(first, 0, vend_d[np.maximum(slot - 1, 0)].astype(np.int64))
+        klen, vlen = ke - ks, ve - vs
+        keys_d = self.keys.cpu().numpy()
+        vals_d = self.vals.cpu().numpy()
+        keys = _gather(keys_d, kb[eblk] + ks, klen)
+        vals = _gather(vals_d, kb[eblk] + vs, vlen)
+        return DenseDecode(status, crc, np.where(status == BLOCK_OK, count, 0).astype(np.uint32),
+                           count, klen.astype(np.uint32), vlen.astype(np.uint32), keys, vals)
+
+
+def _gather(buf: np.ndarray, starts: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    tot = int(lens.sum())
+    if tot == 0:
+        return np.zeros(0, np.uint8)
+    dpos = np.zeros(len(lens), np.int64)
+    np.cumsum(lens[:-1], out=dpos[1:])
+    idx = np.repeat(starts - dpos, lens) + np.arange(tot, dtype=np.int64)
+    return buf[idx]
+
+
+class DenseDecode:
+    """Same shape as the oracle's dense decode: per-block status/crc/count and entries."""
+
+    def __init__(self, status, crc, count, raw_count, klen, vlen, keys, vals):
+        self.status, self.crc_actual, self.count, self.raw_count = status, crc, count, raw_count
+        self.klen, self.vlen, self.keys, self.vals = klen, vlen, keys, vals
+        self.entry_base = np.zeros(len(count) + 1, np.int64)
+        np.cumsum(count, out=self.entry_base[1:])
+        self.kpos = np.zeros(len(klen) + 1, np.int64)
+        np.cumsum(klen, out=self.kpos[1:])
+        self.vpos = np.zeros(len(vlen) + 1, np.int64)
+        np.cumsum(vlen, out=self.vpos[1:])
+
+    def entries(self, b: int) -> list[tuple[bytes, bytes]]:
+        out = []
+        for e in range(self.entry_base[b], self.entry_base[b + 1]):
+            out.append((self.keys[self.kpos[e]:self.kpos[e + 1]].tobytes(),
+                        self.vals[self.vpos[e]:self.vpos[e + 1]].tobytes()))
+        return out
+
+
+def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None = None,
+                 stream: torch.cuda.Stream | None = None) -> SlottedColumns:
+    if cols is None:
+        cols = SlottedColumns(batch.n_blocks, batch.src_bytes, ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
+    ctx.decode_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes,
+                    cols.ptrs(), s.cuda_stream)
+    return cols

@@ -1,0 +1,43 @@
+// tpz_internal.h — shared between the C ABI (tpz_api.cpp) and the kernels (tpz_decode.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tpz_gpu.h"
+
+namespace tpz {
+
+// CRC-32 lookup tables uploaded once per context (see tpz_api.cpp: build_crc_tables):
+// ids 0..15 = T_0..T_15; ids 16+4(j-1)+i = T_{(16<<j)-1-i} for j = 1..6.
+constexpr int kNumCrcTables = 40;
+
+// Slotted layout (include/tpz_gpu.h), callable from device code.
+__host__ __device__ inline uint64_t key_base(uint64_t ext_i, uint64_t i) {
+  return ((ext_i + 63u) & ~(uint64_t)63u) + 128u * i;
+}
+__host__ __device__ inline uint64_t slot_base(uint64_t ext_i, uint64_t i) {
+  return 16u * (ext_i / 96u + i);
+}
+
+struct LaunchArgs {
+  const uint8_t* src;
+  const uint64_t* ext;
+  uint64_t src_bytes;
+  uint32_t n_blocks;
+  const uint32_t* crc_tables;
+  uint8_t* keys;
+  uint8_t* vals;
+  uint32_t* kend;
+  uint32_t* vend;
+  uint32_t* count;
+  uint8_t* status;
+  uint32_t* crc;
+  uint32_t* defer_list;   // workspace: n_blocks entries
+  uint32_t* defer_count;  // workspace: one u32, zeroed before the launch
+  uint32_t num_cus;
+};
+
+void launch_decode(const LaunchArgs& a, hipStream_t stream);
+
+}  // namespace tpz
