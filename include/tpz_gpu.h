@@ -52,11 +52,11 @@ typedef enum {
                                       overlap so the decoded bytes exceed the block's slot:
                                       6*n > len or key bytes > len or value bytes > len.
                                       topazdb's BlockBuilder never writes such a block.      */
-  TPZ_BLOCK_TOO_LARGE = 7          /* len > TPZ_MAX_BLOCK_BYTES or n > TPZ_MAX_BLOCK_ENTRIES */
+  TPZ_BLOCK_TOO_LARGE = 7          /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
+                                      block_size <= 64 KiB BlockBuilder emits)               */
 } tpz_block_status;
 
-#define TPZ_MAX_BLOCK_BYTES 86000u
-#define TPZ_MAX_BLOCK_ENTRIES 2048u
+#define TPZ_MAX_BLOCK_BYTES 94192u
 
 /* ---- batch input -------------------------------------------------------------------------
  * Encoded blocks back to back in one device buffer (an SST data region [0, meta_off), or the

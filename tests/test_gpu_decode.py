@@ -46,6 +46,12 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
     cols, g = gpu_decode(ctx, src, ext)
     o = O.decode_batch(src, ext)
     st_o = o.status.copy()
+    # documented device limit: blocks longer than TPZ_MAX_BLOCK_BYTES report TOO_LARGE
+    big = np.diff(ext.astype(np.int64)) > _lib.MAX_BLOCK_BYTES
+    st_o[big] = _lib.BLOCK_TOO_LARGE
+    o.status = st_o
+    o_count_all = o.count.astype(np.int64)  # oracle emitted entries for these blocks too
+    o.count = np.where(big, 0, o.count).astype(o.count.dtype)
     np.testing.assert_array_equal(g.status, st_o)
     if expect_all_ok:
         assert (st_o == O.OK).all()
@@ -59,7 +65,7 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
     okm = st_o == O.OK
     o_cnt = np.where(okm, o.count, 0)
     assert (g.count == o_cnt).all()
-    sel_e = np.repeat(okm, o.count.astype(np.int64))
+    sel_e = np.repeat(okm, o_count_all)
     np.testing.assert_array_equal(g.klen, o.klen[sel_e])
     np.testing.assert_array_equal(g.vlen, o.vlen[sel_e])
     ksel = np.repeat(sel_e, o.klen.astype(np.int64))
@@ -145,11 +151,20 @@ def test_random_blocks(ctx, seed):
 def test_random_blocks_large_and_many_entries(ctx):
     """Blocks past the wave slot (len > 5104 B or n > 256) take the big path."""
     rng = np.random.default_rng(11)
-    src, ext = _random_blocks(rng, 120, max_target=70000)
+    src, ext = _random_blocks(rng, 120, max_target=65536)
     lens = np.diff(ext.astype(np.int64))
     assert (lens > 5104).any()
     g, o = assert_parity(ctx, src, ext)
-    assert (o.count > 256).any() or True
+    assert (o.count[o.status == O.OK] > 256).any()
+    assert ((lens > 60000) & (o.status == O.OK)).any()
+
+
+def test_too_large_blocks(ctx):
+    rng = np.random.default_rng(12)
+    src, ext = _random_blocks(rng, 40, max_target=200000)
+    lens = np.diff(ext.astype(np.int64))
+    assert (lens > _lib.MAX_BLOCK_BYTES).any()
+    assert_parity(ctx, src, ext)
 
 
 def test_tiny_entries_many_per_block(ctx):

@@ -19,8 +19,7 @@ SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
  BLOCK_MALFORMED, BLOCK_OVERLAP, BLOCK_TOO_LARGE) = range(8)
-MAX_BLOCK_BYTES = 86000
-MAX_BLOCK_ENTRIES = 2048
+MAX_BLOCK_BYTES = 94192
 
 
 class TpzError(RuntimeError):

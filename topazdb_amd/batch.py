@@ -29,7 +29,8 @@ class DeviceBatch:
         dev = _dev(device)
         if isinstance(src, np.ndarray) or isinstance(src, (bytes, bytearray, memoryview)):
             a = np.frombuffer(src, np.uint8) if not isinstance(src, np.ndarray) else src
-            src = torch.from_numpy(np.ascontiguousarray(a, np.uint8)).to(dev)
+            a = np.ascontiguousarray(a, np.uint8)
+            src = torch.from_numpy(a if a.flags.writeable else a.copy()).to(dev)
         if isinstance(ext, np.ndarray) or isinstance(ext, (list, tuple)):
             e = np.ascontiguousarray(np.asarray(ext, np.uint64)).view(np.int64)
             ext_host = e.view(np.uint64)

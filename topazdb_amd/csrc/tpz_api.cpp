@@ -59,6 +59,7 @@ struct tpz_ctx {
   uint32_t num_cus = 0;
   uint32_t* d_tables = nullptr;
   uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
+  uint64_t* d_big_scratch = nullptr;
   uint32_t defer_cap = 0;
   std::mutex mu;  // guards workspace growth only
 };
@@ -93,6 +94,8 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
   std::vector<uint32_t> t = build_crc_tables();
   hipError_t e = hipMalloc(&c->d_tables, t.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_tables, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMalloc(&c->d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t));
   if (e != hipSuccess) {
     tpz_ctx_destroy(c);
     return hip_fail(e, "tpz_ctx_create");
@@ -106,6 +109,7 @@ void tpz_ctx_destroy(tpz_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->d_tables) (void)hipFree(c->d_tables);
   if (c->d_defer) (void)hipFree(c->d_defer);
+  if (c->d_big_scratch) (void)hipFree(c->d_big_scratch);
   delete c;
 }
 
@@ -154,6 +158,8 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.defer_count = c->d_defer;
   a.defer_list = c->d_defer + 1;
   a.num_cus = c->num_cus;
+  a.big_scratch = c->d_big_scratch;
+  a.big_grid = c->num_cus;
   tpz::launch_decode(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;

@@ -14,7 +14,8 @@
 //    processed out of the wave's LDS slot, so HBM reads stay in flight during the decode.
 //  * big path   — blocks that do not fit a wave slot (len > 5104 B or n > 256) are appended to
 //    a device worklist by the wave path and decoded by a second kernel, one wave per block with
-//    an 84 KiB LDS window (TPZ_MAX_BLOCK_BYTES).
+//    a 92 KiB LDS window (TPZ_MAX_BLOCK_BYTES: every block a 64 KiB-target BlockBuilder can
+//    emit) and its entry table in a per-workgroup global scratch (no entry-count limit).
 //  CRC-32: payload split into 16-byte chunks aligned to the payload END; lane l folds chunks
 //  l, l+64, ... (Horner with a shift-by-1024 operator), then a 6-level lane tree combines with
 //  shift-by-16*2^k operators. All operators are byte-sliced lookup tables in LDS (40 KiB).
@@ -49,11 +50,10 @@ static_assert(kSlotBytes % 16 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard][window 84 KiB][pad][ktab 2048 x u64][vtab 2048 x u64]
-constexpr int kBigWinBytes = 86016;
-constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 86000 (a0 + len <= window)
-constexpr u32 kBigMaxN = TPZ_MAX_BLOCK_ENTRIES;     // 2048
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + kBigMaxN * 16;
+// big path (one wave per block): [guard][window 92 KiB][pad]; entry table in global scratch
+constexpr int kBigWinBytes = 94208;
+constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
 static_assert(kBigLds <= 163840, "big path LDS");
 
@@ -183,18 +183,25 @@ struct TabSmall {
     src = t & 0xFFFFu;
   }
 };
+// Big path: per entry one u64 per column, {end, src}, in this workgroup's global scratch.
+// Written and read back by the same wave: stores are drained (s_waitcnt vmcnt(0)) before the
+// copy phase and reads use sc1 (L2-served) loads, so no stale L1 line of a previous block's
+// table can be returned.
 struct TabBig {
-  uint2* k;
-  uint2* v;
+  u64* k;
+  u64* v;
   __device__ __forceinline__ void put(u32 i, u32 kend, u32 ksrc, u32 vend, u32 vsrc) const {
-    k[i] = make_uint2(kend, ksrc);
-    v[i] = make_uint2(vend, vsrc);
+    k[i] = ((u64)ksrc << 32) | kend;
+    v[i] = ((u64)vsrc << 32) | vend;
   }
-  __device__ __forceinline__ u32 end(bool val, u32 j) const { return (val ? v[j] : k[j]).x; }
+  __device__ __forceinline__ u64 ld(bool val, u32 j) const {
+    return __hip_atomic_load(val ? v + j : k + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ u32 end(bool val, u32 j) const { return (u32)ld(val, j); }
   __device__ __forceinline__ void get(bool val, u32 j, u32& end, u32& src) const {
-    uint2 t = val ? v[j] : k[j];
-    end = t.x;
-    src = t.y;
+    u64 t = ld(val, j);
+    end = (u32)t;
+    src = (u32)(t >> 32);
   }
 };
 
@@ -313,13 +320,9 @@ __device__ __forceinline__ bool decode_block(const u32* tab, uint8_t* win, const
   if (P < 2) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }          // block.rs:54
   const u32 n = lds_be16(win, a0);
   if (P < 2 + 2 * n) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }  // :56-59
-  if (n > (BIG ? kBigMaxN : kWaveMaxN)) {
-    if (!BIG) {
-      if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
-      return true;
-    }
-    put_meta(o, b, TPZ_BLOCK_TOO_LARGE, 0, crc);
-    return false;
+  if (!BIG && n > kWaveMaxN) {
+    if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
+    return true;
   }
   const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
   const u32 dl = P - 2 - 2 * n;
@@ -353,6 +356,10 @@ __device__ __forceinline__ bool decode_block(const u32* tab, uint8_t* win, const
   }
   if (bad) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }
   if (!slots_fit || kc > len || vc > len) { put_meta(o, b, TPZ_BLOCK_OVERLAP, n, crc); return false; }
+  if (BIG) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  }
   __builtin_amdgcn_wave_barrier();
   const u64 kb = key_base(ext_b, b);
   copy_column(win, et, false, n, kc, o.keys + kb);
@@ -375,7 +382,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const uint8_t* src
   return __builtin_amdgcn_make_buffer_rsrc((void*)(src + wstart), (short)0, (int)rem, 0x00020000);
 }
 
+// A 16-byte piece that straddles the end of the source buffer comes back zeroed from the
+// range-checked buffer load; refill the in-range bytes one by one (only the batch's tail).
+__device__ __forceinline__ void fix_tail(uint4& v, const uint8_t* src, u64 piece, u64 src_bytes) {
+  if (piece + 16 > src_bytes && piece < src_bytes) {
+    u32 w[4] = {0, 0, 0, 0};
+    for (u32 k = 0; k < 16 && piece + k < src_bytes; k++) w[k >> 2] |= (u32)src[piece + k] << (8 * (k & 3));
+    v = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 struct Params {
+  u64* big_scratch;  // gridDim(big) x 2 x kBigMaxSlots u64
   const uint8_t* src;
   const u64* ext;
   u64 src_bytes;
@@ -416,6 +434,11 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #pragma unroll
     for (int r = 0; r < kWinRounds; r++)
       if ((u32)r < rounds) v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
+    if (e + 16 > p.src_bytes) {
+#pragma unroll
+      for (int r = 0; r < kWinRounds; r++)
+        if ((u32)r < rounds) fix_tail(v[r], p.src, ws + r * 1024 + lane * 16, p.src_bytes);
+    }
   };
   issue(b, s_cur, e_cur);
 
@@ -451,8 +474,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
   load_tables(tab, p.crc_tables);
   const u32 lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
-  TabBig et{reinterpret_cast<uint2*>(win + kBigWinBytes + 32),
-            reinterpret_cast<uint2*>(win + kBigWinBytes + 32 + kBigMaxN * 8)};
+  TabBig et{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots,
+            p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
   const u32 cnt = uni(*p.out.defer_count);
   for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
     const u32 b = uni(p.out.defer_list[it]);
@@ -467,8 +490,10 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       for (int r = 0; r < 4; r++)
         t[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + r * 1024 + lane * 16, 0, 0));
 #pragma unroll
-      for (int r = 0; r < 4; r++)
+      for (int r = 0; r < 4; r++) {
+        fix_tail(t[r], p.src, ws + off + r * 1024 + lane * 16, p.src_bytes);
         if (off + r * 1024 < nbytes) *reinterpret_cast<uint4*>(win + off + r * 1024 + lane * 16) = t[r];
+      }
     }
     __builtin_amdgcn_wave_barrier();
     decode_block<TabBig, true>(tab, win, et, (u32)(s & 15u), len, b, s, p.out);
@@ -483,12 +508,13 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.src_bytes = a.src_bytes;
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
+  p.big_scratch = a.big_scratch;
   p.out = Out{a.keys, a.vals, a.kend, a.vend, a.count, a.status, a.crc, a.defer_list, a.defer_count};
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
-  hipLaunchKernelGGL(decode_big_kernel, dim3(a.num_cus), dim3(kWave), 0, stream, p);
+  hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kWave), 0, stream, p);
 }
 
 }  // namespace tpz

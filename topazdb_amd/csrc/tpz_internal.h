@@ -11,6 +11,8 @@ namespace tpz {
 // CRC-32 lookup tables uploaded once per context (see tpz_api.cpp: build_crc_tables):
 // ids 0..15 = T_0..T_15; ids 16+4(j-1)+i = T_{(16<<j)-1-i} for j = 1..6.
 constexpr int kNumCrcTables = 40;
+// Big path entry-table capacity per block: slots are only written when 6n <= len.
+constexpr uint32_t kBigMaxSlots = TPZ_MAX_BLOCK_BYTES / 6 + 16;
 
 // Slotted layout (include/tpz_gpu.h), callable from device code.
 __host__ __device__ inline uint64_t key_base(uint64_t ext_i, uint64_t i) {
@@ -36,6 +38,8 @@ struct LaunchArgs {
   uint32_t* defer_list;   // workspace: n_blocks entries
   uint32_t* defer_count;  // workspace: one u32, zeroed before the launch
   uint32_t num_cus;
+  uint64_t* big_scratch;  // big_grid x 2 x kBigMaxSlots
+  uint32_t big_grid;
 };
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
