@@ -56,7 +56,7 @@ def block_counts(src: np.ndarray, ext: np.ndarray) -> np.ndarray:
 def algorithmic_bytes(ext: np.ndarray, n_ent: np.ndarray, kbytes: int, vbytes: int) -> int:
     nb = len(ext) - 1
     reads = int(ext[-1] - ext[0]) + 8 * nb           # block bytes + extent
-    writes = kbytes + vbytes + 8 * int(n_ent.sum()) + 9 * nb  # columns + kend/vend + count/status/crc
+    writes = kbytes + vbytes + 8 * int(n_ent.sum()) + 9 * nb  # columns + {kend,vend} + count/status/crc
     return reads + writes
 
 
@@ -73,8 +73,9 @@ def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev)
     np.cumsum(n_ent, out=e0[1:])
     bid = np.arange(nb, dtype=np.int64)
     ext64 = ext[:-1].astype(np.int64)
-    kb = ((ext64 + 63) & ~63) + 128 * bid
-    sb = 16 * (ext64 // 96 + bid)
+    kb = _lib.key_base(ext64, bid)
+    sb = _lib.entry_base(ext64, bid)
+    ends = cols.ends.view(-1, 2)
     kpos = kpos.astype(np.int64)
     vpos = vpos.astype(np.int64)
     step = 65536
@@ -82,8 +83,8 @@ def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev)
     dvals = torch.from_numpy(vals[:int(vpos[e0[-1]])]).to(dev)
     for lo in range(0, nb, step):
         hi = min(nb, lo + step)
-        for col, pos, dexp, dend in ((cols.keys, kpos, dkeys, cols.kend),
-                                     (cols.vals, vpos, dvals, cols.vend)):
+        for col, pos, dexp, dend in ((cols.keys, kpos, dkeys, ends[:, 0]),
+                                     (cols.vals, vpos, dvals, ends[:, 1])):
             tot = pos[e0[lo + 1:hi + 1]] - pos[e0[lo:hi]]          # bytes per block
             start_exp = pos[e0[lo:hi]]
             n = int(tot.sum())
@@ -192,7 +193,7 @@ def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
         d_ext = torch.empty(cb + 1, dtype=torch.int64, device=dev)
         cols = SlottedColumns(cb, cap, dev.index)
         h_cols = {k: torch.empty(getattr(cols, k).numel(), dtype=getattr(cols, k).dtype).pin_memory()
-                  for k in ("keys", "vals", "kend", "vend", "count", "status", "crc")}
+                  for k in ("keys", "vals", "ends", "count", "status", "crc")}
         bufs.append((d_src, d_ext, cols, h_cols))
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -208,8 +209,8 @@ def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
             ctx.decode_ptrs(d_src.data_ptr(), d_ext.data_ptr(), hi - lo, end - base,
                             cols.ptrs(), s.cuda_stream)
             kc = _lib.col_capacity(end - base, hi - lo)
-            sc = _lib.slot_capacity(end - base, hi - lo)
-            for k, n in (("keys", kc), ("vals", kc), ("kend", sc), ("vend", sc),
+            sc = 2 * _lib.entry_capacity(end - base, hi - lo)
+            for k, n in (("keys", kc), ("vals", kc), ("ends", sc),
                          ("count", hi - lo), ("status", hi - lo), ("crc", hi - lo)):
                 h_cols[k][:n].copy_(getattr(cols, k)[:n], non_blocking=True)
     torch.cuda.synchronize(dev)

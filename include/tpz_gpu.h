@@ -71,45 +71,48 @@ typedef struct {
 
 /* ---- decoded columns (the "slotted" layout) ----------------------------------------------
  * No global prefix pass: every block owns a slot derived from its input extent, so blocks
- * decode independently (and shard across GPUs) with no cross-block communication.
+ * decode independently (and shard across GPUs) with no cross-block communication. Every slot
+ * starts on a 128-byte line and is written in whole lines (HBM3E then never sees a partial-line
+ * write from two different workgroups).
  *   keys / vals : block i's key bytes are packed at keys[tpz_key_base(ext[i], i) ...
- *                 + key_bytes), same for values at vals[tpz_key_base(ext[i], i) ...]
- *   kend / vend : entry j of block i (j < count[i]) has its inclusive end offsets, relative to
- *                 the block's base, at kend[tpz_slot_base(ext[i], i) + j]:
- *                 key_j = keys[kb + (j ? kend[s+j-1] : 0) .. kb + kend[s+j]]
+ *                 + key_bytes), its value bytes at vals[tpz_key_base(ext[i], i) ...]
+ *   ends        : entry j of block i (j < count[i]) has its inclusive end offsets, relative to
+ *                 the block's base, at ends[2*(e+j)] (key) and ends[2*(e+j)+1] (value),
+ *                 e = tpz_entry_base(ext[i], i):
+ *                 key_j   = keys[kb + (j ? ends[2(e+j-1)]   : 0) .. kb + ends[2(e+j)]]
+ *                 value_j = vals[kb + (j ? ends[2(e+j-1)+1] : 0) .. kb + ends[2(e+j)+1]]
  *   count[i]    : entries in block i (n) for OK and OVERLAP, else 0
  *   status[i]   : tpz_block_status
  *   crc[i]      : CRC-32 the device computed over the payload (valid for OK, MALFORMED,
  *                 OVERLAP, CHECKSUM_MISMATCH; the stored one is the payload's trailing u32)
  * Bytes of a slot beyond the block's own data are unspecified. */
 typedef struct {
-  uint8_t* d_keys;   /* capacity tpz_col_capacity(src_bytes, n_blocks) bytes   */
-  uint8_t* d_vals;   /* same capacity                                          */
-  uint32_t* d_kend;  /* capacity tpz_slot_capacity(src_bytes, n_blocks) u32     */
-  uint32_t* d_vend;  /* same capacity                                          */
+  uint8_t* d_keys;   /* capacity tpz_col_capacity(src_bytes, n_blocks) bytes        */
+  uint8_t* d_vals;   /* same capacity                                               */
+  uint32_t* d_ends;  /* capacity 2 * tpz_entry_capacity(src_bytes, n_blocks) u32     */
   uint32_t* d_count; /* n_blocks */
   uint8_t* d_status; /* n_blocks */
   uint32_t* d_crc;   /* n_blocks */
 } tpz_columns;
 
 static inline uint64_t tpz_key_base(uint64_t ext_i, uint64_t i) {
-  return ((ext_i + 63u) & ~(uint64_t)63u) + 128u * i;
+  return ((ext_i + 127u) & ~(uint64_t)127u) + 256u * i;
 }
-static inline uint64_t tpz_slot_base(uint64_t ext_i, uint64_t i) {
+static inline uint64_t tpz_entry_base(uint64_t ext_i, uint64_t i) {
   return 16u * (ext_i / 96u + i);
 }
 static inline uint64_t tpz_col_capacity(uint64_t src_bytes, uint64_t n_blocks) {
-  return tpz_key_base(src_bytes, n_blocks) + 64u;
+  return tpz_key_base(src_bytes, n_blocks) + 128u;
 }
-static inline uint64_t tpz_slot_capacity(uint64_t src_bytes, uint64_t n_blocks) {
-  return tpz_slot_base(src_bytes, n_blocks) + 16u;
+static inline uint64_t tpz_entry_capacity(uint64_t src_bytes, uint64_t n_blocks) {
+  return tpz_entry_base(src_bytes, n_blocks) + 16u;
 }
 
 /* Exported copies of the layout helpers for FFI callers that cannot use static inline. */
 uint64_t tpz_layout_key_base(uint64_t ext_i, uint64_t i);
-uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i);
+uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i);
 uint64_t tpz_layout_col_capacity(uint64_t src_bytes, uint64_t n_blocks);
-uint64_t tpz_layout_slot_capacity(uint64_t src_bytes, uint64_t n_blocks);
+uint64_t tpz_layout_entry_capacity(uint64_t src_bytes, uint64_t n_blocks);
 
 /* ---- context ------------------------------------------------------------------------------ */
 typedef struct tpz_ctx tpz_ctx;

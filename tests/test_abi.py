@@ -32,14 +32,15 @@ def test_layout_helpers_match_python():
     for _ in range(200):
         e, i = int(rng.integers(0, 1 << 40)), int(rng.integers(0, 1 << 24))
         assert L.tpz_layout_key_base(e, i) == _lib.key_base(e, i)
-        assert L.tpz_layout_slot_base(e, i) == _lib.slot_base(e, i)
+        assert L.tpz_layout_entry_base(e, i) == _lib.entry_base(e, i)
         assert L.tpz_layout_col_capacity(e, i) == _lib.col_capacity(e, i)
-        assert L.tpz_layout_slot_capacity(e, i) == _lib.slot_capacity(e, i)
+        assert L.tpz_layout_entry_capacity(e, i) == _lib.entry_capacity(e, i)
 
 
 def test_slots_never_overlap():
-    """Worst case a block may emit under the slot contract: 16-byte chunked key/value bytes
-    up to len, and floor(len/6) entries; consecutive slots must stay disjoint."""
+    """Worst case a block may emit under the slot contract: key/value bytes up to len written
+    in whole 128-byte lines, and floor(len/6) entries written in whole lines of 16 {kend, vend}
+    pairs; consecutive slots must stay disjoint and line aligned."""
     rng = np.random.default_rng(2)
     lens = np.concatenate([rng.integers(0, 70000, 3000), rng.integers(0, 40, 3000),
                            np.full(100, 4155), np.arange(0, 200)])
@@ -50,12 +51,12 @@ def test_slots_never_overlap():
     for i in range(n):
         ln = int(lens[i])
         kb, kb1 = _lib.key_base(int(ext[i]), i), _lib.key_base(int(ext[i + 1]), i + 1)
-        assert kb % 64 == 0
-        assert kb + ((ln + 15) & ~15) <= kb1
-        sb, sb1 = _lib.slot_base(int(ext[i]), i), _lib.slot_base(int(ext[i + 1]), i + 1)
-        assert sb + ln // 6 <= sb1
+        assert kb % 128 == 0
+        assert kb + ((ln + 127) & ~127) <= kb1
+        sb, sb1 = _lib.entry_base(int(ext[i]), i), _lib.entry_base(int(ext[i + 1]), i + 1)
+        assert sb % 16 == 0 and sb + ((ln // 6 + 15) & ~15) <= sb1
     assert _lib.key_base(int(ext[-1]), n) <= _lib.col_capacity(int(ext[-1]), n)
-    assert _lib.slot_base(int(ext[-1]), n) <= _lib.slot_capacity(int(ext[-1]), n)
+    assert _lib.entry_base(int(ext[-1]), n) <= _lib.entry_capacity(int(ext[-1]), n)
 
 
 def test_error_strings_match_reference():

@@ -11,7 +11,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libtpz_gpu.so")
+# TPZ_LIB_PATH: diagnostic override (ablation builds under topazdb_amd/variants/)
+LIB_PATH = os.environ.get("TPZ_LIB_PATH") or os.path.join(HERE, "libtpz_gpu.so")
 HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 
 # tpz_err
@@ -32,9 +33,8 @@ class Batch(C.Structure):
 
 
 class Columns(C.Structure):
-    _fields_ = [("d_keys", C.c_void_p), ("d_vals", C.c_void_p), ("d_kend", C.c_void_p),
-                ("d_vend", C.c_void_p), ("d_count", C.c_void_p), ("d_status", C.c_void_p),
-                ("d_crc", C.c_void_p)]
+    _fields_ = [("d_keys", C.c_void_p), ("d_vals", C.c_void_p), ("d_ends", C.c_void_p),
+                ("d_count", C.c_void_p), ("d_status", C.c_void_p), ("d_crc", C.c_void_p)]
 
 
 _lib = None
@@ -66,7 +66,7 @@ def lib() -> C.CDLL:
         L.tpz_format_block_error.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_char_p,
                                              C.c_size_t]
         L.tpz_last_error.restype = C.c_char_p
-        for f in ("key_base", "slot_base", "col_capacity", "slot_capacity"):
+        for f in ("key_base", "entry_base", "col_capacity", "entry_capacity"):
             fn = getattr(L, "tpz_layout_" + f)
             fn.argtypes = [C.c_uint64, C.c_uint64]
             fn.restype = C.c_uint64
@@ -85,21 +85,21 @@ def format_block_error(status: int, crc_expected: int = 0, crc_actual: int = 0) 
     return buf.value.decode()
 
 
-# layout (mirrors the static inline helpers of include/tpz_gpu.h)
+# layout (mirrors the static inline helpers of include/tpz_gpu.h; works on ints and numpy int64)
 def key_base(ext_i, i):
-    return ((ext_i + 63) & ~63) + 128 * i
+    return ((ext_i + 127) & ~127) + 256 * i
 
 
-def slot_base(ext_i, i):
+def entry_base(ext_i, i):
     return 16 * (ext_i // 96 + i)
 
 
 def col_capacity(src_bytes: int, n_blocks: int) -> int:
-    return key_base(src_bytes, n_blocks) + 64
+    return key_base(src_bytes, n_blocks) + 128
 
 
-def slot_capacity(src_bytes: int, n_blocks: int) -> int:
-    return slot_base(src_bytes, n_blocks) + 16
+def entry_capacity(src_bytes: int, n_blocks: int) -> int:
+    return entry_base(src_bytes, n_blocks) + 16
 
 
 class Context:
@@ -129,7 +129,7 @@ class Context:
                     stream: int = 0) -> None:
         """tpz_decode_blocks on raw device pointers; cols maps field name -> device pointer."""
         b = Batch(d_src, d_ext, n_blocks, src_bytes)
-        c = Columns(cols["keys"], cols["vals"], cols["kend"], cols["vend"], cols["count"],
-                    cols["status"], cols["crc"])
+        c = Columns(cols["keys"], cols["vals"], cols["ends"], cols["count"], cols["status"],
+                    cols["crc"])
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")

@@ -53,12 +53,11 @@ class SlottedColumns:
     def __init__(self, n_blocks: int, src_bytes: int, device: int = 0):
         dev = _dev(device)
         cap = _lib.col_capacity(src_bytes, n_blocks)
-        scap = _lib.slot_capacity(src_bytes, n_blocks)
+        ecap = _lib.entry_capacity(src_bytes, n_blocks)
         nb = max(n_blocks, 1)
         self.keys = torch.empty(cap, dtype=torch.uint8, device=dev)
         self.vals = torch.empty(cap, dtype=torch.uint8, device=dev)
-        self.kend = torch.empty(scap, dtype=torch.int32, device=dev)
-        self.vend = torch.empty(scap, dtype=torch.int32, device=dev)
+        self.ends = torch.empty(2 * ecap, dtype=torch.int32, device=dev)  # {kend, vend} pairs
         self.count = torch.empty(nb, dtype=torch.int32, device=dev)
         self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
         self.crc = torch.empty(nb, dtype=torch.int32, device=dev)
@@ -66,7 +65,7 @@ class SlottedColumns:
 
     def ptrs(self) -> dict:
         return {k: getattr(self, k).data_ptr() for k in
-                ("keys", "vals", "kend", "vend", "count", "status", "crc")}
+                ("keys", "vals", "ends", "count", "status", "crc")}
 
     def meta_host(self):
         nb = self.n_blocks
@@ -85,11 +84,11 @@ class SlottedColumns:
         total = int(ebase[-1])
         eblk = np.repeat(bid, n_ok)
         j = np.arange(total, dtype=np.int64) - ebase[eblk]
-        sb = 16 * (ext // 96 + bid)
-        kb = ((ext + 63) & ~63) + 128 * bid
+        sb = _lib.entry_base(ext, bid)
+        kb = _lib.key_base(ext, bid)
         slot = sb[eblk] + j
-        kend_d = self.kend.cpu().numpy().view(np.uint32)
-        vend_d = self.vend.cpu().numpy().view(np.uint32)
+        ends = self.ends.cpu().numpy().view(np.uint32)
+        kend_d, vend_d = ends[0::2], ends[1::2]
         ke = kend_d[slot].astype(np.int64)
         ve = vend_d[slot].astype(np.int64)
         first = j == 0

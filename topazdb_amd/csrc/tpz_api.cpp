@@ -28,7 +28,7 @@ tpz_err hip_fail(hipError_t e, const char* what) {
 // bytes; T_{k+1}[b] = (T_k[b] >> 8) ^ T_0[T_k[b] & 0xFF]. Only the 40 tables the kernels use
 // are kept (ids documented in tpz_internal.h).
 std::vector<uint32_t> build_crc_tables() {
-  const int kmax = 1024;
+  const int kmax = 5120;
   std::vector<uint32_t> all((size_t)kmax * 256);
   for (uint32_t b = 0; b < 256; b++) {
     uint32_t c = b;
@@ -45,9 +45,9 @@ std::vector<uint32_t> build_crc_tables() {
     std::memcpy(&out[(size_t)id * 256], &all[(size_t)k * 256], 256 * 4);
   };
   for (int k = 0; k < 16; k++) put(k, k);
-  for (int j = 1; j <= 6; j++) {
-    const int n = 16 << j;
-    for (int i = 0; i < 4; i++) put(16 + 4 * (j - 1) + i, n - 1 - i);
+  for (int j = 0; j < 6; j++) {
+    const int n = tpz::kCrcShiftBytes[j];
+    for (int i = 0; i < 4; i++) put(16 + 4 * j + i, n - 1 - i);
   }
   return out;
 }
@@ -67,9 +67,9 @@ struct tpz_ctx {
 extern "C" {
 
 uint64_t tpz_layout_key_base(uint64_t ext_i, uint64_t i) { return tpz_key_base(ext_i, i); }
-uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i) { return tpz_slot_base(ext_i, i); }
+uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i) { return tpz_entry_base(ext_i, i); }
 uint64_t tpz_layout_col_capacity(uint64_t s, uint64_t n) { return tpz_col_capacity(s, n); }
-uint64_t tpz_layout_slot_capacity(uint64_t s, uint64_t n) { return tpz_slot_capacity(s, n); }
+uint64_t tpz_layout_entry_capacity(uint64_t s, uint64_t n) { return tpz_entry_capacity(s, n); }
 
 const char* tpz_last_error(void) { return g_last_error.c_str(); }
 
@@ -132,8 +132,8 @@ tpz_err tpz_ctx_reserve(tpz_ctx* c, uint32_t max_blocks) {
 tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, void* stream) {
   if (!c || !b || !o) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
-  if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_vals || !o->d_kend || !o->d_vend ||
-      !o->d_count || !o->d_status || !o->d_crc)
+  if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_vals || !o->d_ends || !o->d_count ||
+      !o->d_status || !o->d_crc)
     return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks > c->defer_cap || !c->d_defer) {
     tpz_err r = tpz_ctx_reserve(c, b->n_blocks);
@@ -150,8 +150,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.crc_tables = c->d_tables;
   a.keys = o->d_keys;
   a.vals = o->d_vals;
-  a.kend = o->d_kend;
-  a.vend = o->d_vend;
+  a.ends = o->d_ends;
   a.count = o->d_count;
   a.status = o->d_status;
   a.crc = o->d_crc;

@@ -17,11 +17,15 @@
 //    a 92 KiB LDS window (TPZ_MAX_BLOCK_BYTES: every block a 64 KiB-target BlockBuilder can
 //    emit) and its entry table in a per-workgroup global scratch (no entry-count limit).
 //  CRC-32: payload split into 16-byte chunks aligned to the payload END; lane l folds chunks
-//  l, l+64, ... (Horner with a shift-by-1024 operator), then a 6-level lane tree combines with
-//  shift-by-16*2^k operators. All operators are byte-sliced lookup tables in LDS (40 KiB).
+//  l, l+64, ... (Horner with a shift-by-1024 operator), then a lane tree (DPP row shifts, then
+//  readlane across rows) combines with shift-by-16*2^k operators. All operators are
+//  byte-sliced lookup tables in LDS (40 KiB).
 //  Decode: lanes parse 64 entries at a time (n, offsets, klen, vlen, bounds checks that mirror
-//  the reference's panics), a wave prefix sum gives packed output positions, then each lane
-//  assembles 16-byte output chunks (output-driven gather, coalesced 1 KiB dwordx4 stores).
+//  the reference's panics), a DPP wave prefix sum gives packed output positions, and each
+//  entry marks the 16-byte output chunks that start inside it in a chunk->entry map. The copy
+//  is output-driven: lane c assembles output chunk c from the (usually one) source segment(s)
+//  covering it with two ds_read_b128 + a funnel shift per segment, then one coalesced dwordx4
+//  store (1 KiB per wave instruction).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -40,24 +44,23 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
 constexpr int kGuard = 32;
 
-// wave path slot: [guard 32][window 5120][pad 32][ktab 256 x u32][vtab 256 x u32]
+// wave path slot: [guard 32][window 5120][pad 32][ktab n x u32][vtab n x u32][hist 64 x u32]
 constexpr int kWinRounds = 5;                       // 5 x 1 KiB window
 constexpr int kWinBytes = kWinRounds * 1024;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
 constexpr u32 kWaveMaxN = 256;
-constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveMaxN * 8;
+constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveMaxN * 8 + 256;
 static_assert(kSlotBytes % 16 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard][window 92 KiB][pad]; entry table in global scratch
+// big path (one wave per block): [guard][window 92 KiB][pad][hist 64 x u32];
+// entry tables in global scratch
 constexpr int kBigWinBytes = 94208;
 constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32;
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + 256;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
 static_assert(kBigLds <= 163840, "big path LDS");
-
-constexpr uint8_t kStDeferred = 0xFF;  // internal: handed to the big path
 
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -66,6 +69,14 @@ __device__ __forceinline__ u64 uni64(u64 x) {
   u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
   return ((u64)hi << 32) | lo;
 }
+__device__ __forceinline__ u32 readlane(u32 x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// DPP row op with bound_ctrl: lanes whose source is outside their row of 16 read 0.
+template <int CTRL>
+__device__ __forceinline__ u32 dpp(u32 x) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+constexpr int kRowShr = 0x110;  // row_shr:n = 0x110 + n (lane l reads l-n)
+constexpr int kRowShl = 0x100;  // row_shl:n = 0x100 + n (lane l reads l+n)
 
 // Unaligned little-endian u32 from LDS at byte offset a (>= 0) of an LDS byte array whose base
 // is 4-byte aligned: two ds_read_b32 + v_alignbyte.
@@ -80,9 +91,30 @@ __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
+// 16 bytes starting at signed LDS byte offset x (relative to base, base 16-aligned): two
+// ds_read_b128 then a per-lane funnel shift by x & 15.
+__device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
+  // Two whole ds_read_b128. The empty asm hides the loads from the selects below: otherwise
+  // hipcc turns "select of loaded dwords" into branches and sinks dword-sized reads into them.
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* p = reinterpret_cast<const u32x4*>(base + (x & ~15));
+  u32x4 va = p[0], vb = p[1];
+  asm volatile("" : "+v"(va), "+v"(vb));
+  const uint4 a = make_uint4(va.x, va.y, va.z, va.w);
+  const uint4 b = make_uint4(vb.x, vb.y, vb.z, vb.w);
+  const u32 sh = (u32)x & 15u, s = sh & 3u, q = sh >> 2;
+  const u32 w0 = q < 2 ? (q == 0 ? a.x : a.y) : (q == 2 ? a.z : a.w);
+  const u32 w1 = q < 2 ? (q == 0 ? a.y : a.z) : (q == 2 ? a.w : b.x);
+  const u32 w2 = q < 2 ? (q == 0 ? a.z : a.w) : (q == 2 ? b.x : b.y);
+  const u32 w3 = q < 2 ? (q == 0 ? a.w : b.x) : (q == 2 ? b.y : b.z);
+  const u32 w4 = q < 2 ? (q == 0 ? b.x : b.y) : (q == 2 ? b.z : b.w);
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
+                    __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
+}
+
 // ------------------------------------------------------------------ CRC-32 (table driven)
 // tab = kNumCrcTables x 256 u32 in LDS. T_k[b] = R0(b || 0^k): raw CRC (init 0, no xorout).
-// ids 0..15: T_0..T_15 (slice-by-16); ids 16+4(j-1)+i (j=1..6): T_{n-1-i}, n = 16<<j.
+// ids 0..15: T_0..T_15 (slice-by-16); ids 16+4j+i: T_{n_j-1-i}, n_j = kCrcShiftBytes[j].
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
 
 // R0 of one 16-byte chunk (little-endian dwords w0..w3): XOR_i T_{15-i}[c_i].
@@ -98,130 +130,115 @@ __device__ __forceinline__ u32 slice16(const u32* tab, u32 w0, u32 w1, u32 w2, u
   return c;
 }
 
-// shift_n(A) = R_A(0^n) = XOR_i T_{n-1-i}[byte_i(A)], n = 16 << J.
+// shift_n(A) = R_A(0^n) = XOR_i T_{n-1-i}[byte_i(A)], n = kCrcShiftBytes[J].
 template <int J>
 __device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
-  constexpr int b0 = J == 0 ? 15 : 16 + 4 * (J - 1);
-  constexpr int d = J == 0 ? -1 : 1;
-  return tlook(tab, b0, a & 0xFF) ^ tlook(tab, b0 + d, (a >> 8) & 0xFF) ^
-         tlook(tab, b0 + 2 * d, (a >> 16) & 0xFF) ^ tlook(tab, b0 + 3 * d, a >> 24);
+  constexpr int b0 = 16 + 4 * J;
+  return tlook(tab, b0, a & 0xFF) ^ tlook(tab, b0 + 1, (a >> 8) & 0xFF) ^
+         tlook(tab, b0 + 2, (a >> 16) & 0xFF) ^ tlook(tab, b0 + 3, a >> 24);
 }
 
-// 16 bytes starting at signed LDS byte offset x (relative to win); e = x & 15 is wave-uniform.
-__device__ __forceinline__ void lds_chunk16(const uint8_t* win, int x, u32 e, u32& o0, u32& o1,
-                                            u32& o2, u32& o3) {
-  const uint4* p = reinterpret_cast<const uint4*>(win + (x & ~15));
-  uint4 a = p[0], b = p[1];
-  u32 s = e & 3u, q = e >> 2;
-  u32 w0, w1, w2, w3, w4;
-  if (q == 0) { w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; }
-  else if (q == 1) { w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; }
-  else if (q == 2) { w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; }
-  else { w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; }
-  o0 = __builtin_amdgcn_alignbyte(w1, w0, s);
-  o1 = __builtin_amdgcn_alignbyte(w2, w1, s);
-  o2 = __builtin_amdgcn_alignbyte(w3, w2, s);
-  o3 = __builtin_amdgcn_alignbyte(w4, w3, s);
-}
-
-// keep the bytes of dword at payload position pos (4 bytes) that are >= 0
+// keep the bytes of the dword at payload position pos (4 bytes) that are at positions >= 0
 __device__ __forceinline__ u32 mask_front(u32 w, int pos) {
-  if (pos >= 0) return w;
-  if (pos <= -4) return 0u;
-  return w & (~0u << (8 * (-pos)));
+  const int sh = min(max(-pos, 0), 4) * 8;
+  return sh >= 32 ? 0u : (w & (~0u << sh));
 }
 
 // CRC-32 of the payload at LDS offset pb (relative to win), length P >= 4, whose first four
 // bytes have already been complemented (init 0xFFFFFFFF folded into the message).
-// Returns ~R0(payload') in every lane.
+// The payload is cut into 80-byte runs aligned to its END (leading zero padding leaves a raw CRC
+// unchanged); lane l folds run l (counted from the end) with five chained slice-by-16 steps,
+// super-rounds of 64 runs (5120 B) are chained with a shift-by-5120 operator, and the lanes are
+// combined by a tree of shift-by-80*2^k operators. Returns ~R0(payload') (wave-uniform).
 __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int pb, u32 P) {
   const u32 lane = lane_id();
-  const u32 G = (P + 15) >> 4;          // chunks, end-aligned
-  const u32 R = (G + 63) >> 6;          // rounds of 64 chunks
-  const u32 e = (u32)(pb + (int)P) & 15u;
+  const u32 S = (P + 5119) / 5120;      // super-rounds, end-aligned
   u32 A = 0;
-  for (u32 r = R; r-- > 0;) {
-    const u32 g = lane + 64u * r;
+  for (u32 r = S; r-- > 0;) {
+    const int seg = (int)P - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
     u32 c = 0;
-    if (g < G) {
-      const int start = (int)P - 16 * (int)(g + 1);
-      u32 w0, w1, w2, w3;
-      lds_chunk16(win, pb + start, e, w0, w1, w2, w3);
-      w0 = mask_front(w0, start);
-      w1 = mask_front(w1, start + 4);
-      w2 = mask_front(w2, start + 8);
-      w3 = mask_front(w3, start + 12);
-      c = slice16(tab, w0, w1, w2, w3);
+    if (seg + kCrcLaneBytes > 0) {
+#pragma unroll
+      for (int t = 0; t < kCrcLaneBytes / 16; t++) {
+        const int start = seg + 16 * t;
+        const uint4 w = lds_window16(win, pb + max(start, -16));
+        c = slice16(tab, mask_front(w.x, start) ^ c, mask_front(w.y, start + 4),
+                    mask_front(w.z, start + 8), mask_front(w.w, start + 12));
+      }
     }
-    A = (r + 1 == R) ? c : (crc_shift<6>(tab, A) ^ c);
+    A = (r + 1 == S) ? c : (crc_shift<5>(tab, A) ^ c);
   }
-  // lane tree: result = XOR_l shift_{16 l}(A_l)
+  // lane tree inside each row of 16 lanes: lane l+d covers bytes further from the end
   u32 y;
-  y = __shfl_down(A, 1);  if ((lane & 1u) == 0) A ^= crc_shift<0>(tab, y);
-  y = __shfl_down(A, 2);  if ((lane & 3u) == 0) A ^= crc_shift<1>(tab, y);
-  y = __shfl_down(A, 4);  if ((lane & 7u) == 0) A ^= crc_shift<2>(tab, y);
-  y = __shfl_down(A, 8);  if ((lane & 15u) == 0) A ^= crc_shift<3>(tab, y);
-  y = __shfl_down(A, 16); if ((lane & 31u) == 0) A ^= crc_shift<4>(tab, y);
-  y = __shfl_down(A, 32); if ((lane & 63u) == 0) A ^= crc_shift<5>(tab, y);
-  return ~uni(A);
+  y = dpp<kRowShl + 1>(A); if ((lane & 1u) == 0) A ^= crc_shift<0>(tab, y);
+  y = dpp<kRowShl + 2>(A); if ((lane & 3u) == 0) A ^= crc_shift<1>(tab, y);
+  y = dpp<kRowShl + 4>(A); if ((lane & 7u) == 0) A ^= crc_shift<2>(tab, y);
+  y = dpp<kRowShl + 8>(A); if ((lane & 15u) == 0) A ^= crc_shift<3>(tab, y);
+  // rows of 16 lanes = 1280 B: R0 ^ shift1280(R1 ^ shift1280(R2 ^ shift1280(R3)))
+  u32 t = readlane(A, 48);
+  t = readlane(A, 32) ^ crc_shift<4>(tab, t);
+  t = readlane(A, 16) ^ crc_shift<4>(tab, uni(t));
+  t = readlane(A, 0) ^ crc_shift<4>(tab, uni(t));
+  return ~uni(t);
 }
 
 // ------------------------------------------------------------------ entry tables
-// Wave path: per entry one u32 per column, (end << 16) | src, both < 65536 (block <= 5104 B).
-// Big path: per entry one uint2 per column, {end, src}.
-struct TabSmall {
-  u32* k;
-  u32* v;
-  __device__ __forceinline__ void put(u32 i, u32 kend, u32 ksrc, u32 vend, u32 vsrc) const {
-    k[i] = (kend << 16) | ksrc;
-    v[i] = (vend << 16) | vsrc;
+// Per column, the NON-EMPTY entries in order (compacted): end = inclusive end offset of the
+// entry's bytes in the column, delta = (LDS offset of its first byte) - (its start offset in
+// the column), so byte x of the column inside that entry sits at LDS offset x + delta.
+// Wave path: one u32 per entry, (end << 16) | (u16)delta (block <= 5104 B).
+struct ColSmall {
+  u32* t;
+  __device__ __forceinline__ void put(u32 k, u32 end, int delta) const {
+    t[k] = (end << 16) | ((u32)delta & 0xFFFFu);
   }
-  __device__ __forceinline__ u32 end(bool val, u32 j) const { return (val ? v[j] : k[j]) >> 16; }
-  __device__ __forceinline__ void get(bool val, u32 j, u32& end, u32& src) const {
-    u32 t = val ? v[j] : k[j];
-    end = t >> 16;
-    src = t & 0xFFFFu;
+  __device__ __forceinline__ u32 end(u32 k) const { return t[k] >> 16; }
+  __device__ __forceinline__ void get(u32 k, u32& end, int& delta) const {
+    const u32 v = t[k];
+    end = v >> 16;
+    delta = (int)(short)(v & 0xFFFFu);
   }
 };
-// Big path: per entry one u64 per column, {end, src}, in this workgroup's global scratch.
-// Written and read back by the same wave: stores are drained (s_waitcnt vmcnt(0)) before the
-// copy phase and reads use sc1 (L2-served) loads, so no stale L1 line of a previous block's
-// table can be returned.
-struct TabBig {
-  u64* k;
-  u64* v;
-  __device__ __forceinline__ void put(u32 i, u32 kend, u32 ksrc, u32 vend, u32 vsrc) const {
-    k[i] = ((u64)ksrc << 32) | kend;
-    v[i] = ((u64)vsrc << 32) | vend;
+// Big path: one u64 per entry, {end, delta}, in this workgroup's global scratch. Written and
+// read back by the same wave: stores are drained (s_waitcnt vmcnt(0)) before the copy phase and
+// reads use sc1 (L2-served) loads, so no stale L1 line of a previous block can be returned.
+struct ColBig {
+  u64* t;
+  __device__ __forceinline__ void put(u32 k, u32 end, int delta) const {
+    t[k] = ((u64)(u32)delta << 32) | end;
   }
-  __device__ __forceinline__ u64 ld(bool val, u32 j) const {
-    return __hip_atomic_load(val ? v + j : k + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __device__ __forceinline__ u64 ld(u32 k) const {
+    return __hip_atomic_load(t + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __device__ __forceinline__ u32 end(bool val, u32 j) const { return (u32)ld(val, j); }
-  __device__ __forceinline__ void get(bool val, u32 j, u32& end, u32& src) const {
-    u64 t = ld(val, j);
-    end = (u32)t;
-    src = (u32)(t >> 32);
+  __device__ __forceinline__ u32 end(u32 k) const { return (u32)ld(k); }
+  __device__ __forceinline__ void get(u32 k, u32& end, int& delta) const {
+    const u64 v = ld(k);
+    end = (u32)v;
+    delta = (int)(u32)(v >> 32);
   }
 };
 
-// wave-inclusive prefix sum over 64 lanes
+// Wave-inclusive prefix sum over 64 lanes: DPP row scans, then row carries via readlane.
 __device__ __forceinline__ u32 wave_scan_incl(u32 x) {
   const u32 lane = lane_id();
-#pragma unroll
-  for (u32 d = 1; d < 64; d <<= 1) {
-    u32 t = __shfl_up(x, d);
-    if (lane >= d) x += t;
-  }
-  return x;
+  x += dpp<kRowShr + 1>(x);
+  x += dpp<kRowShr + 2>(x);
+  x += dpp<kRowShr + 4>(x);
+  x += dpp<kRowShr + 8>(x);
+  const u32 r0 = readlane(x, 15), r1 = readlane(x, 31), r2 = readlane(x, 47);
+  const u32 row = lane >> 4;
+  return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+__device__ __forceinline__ u32 lanes_below(u64 mask) {
+  return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
 }
 
 // ------------------------------------------------------------------ per-block decode
 struct Out {
   uint8_t* keys;
   uint8_t* vals;
-  u32* kend;
-  u32* vend;
+  u32* ends;
   u32* count;
   uint8_t* status;
   u32* crc;
@@ -237,74 +254,150 @@ __device__ __forceinline__ void put_meta(const Out& o, u32 b, u32 st, u32 n, u32
   }
 }
 
-// Output-driven copy of one column: lane handles 16-byte chunks c = lane, lane+64, ...
-// Byte x of the column comes from segment j = first entry with end_j > x, at LDS offset
-// src_j + (x - start_j) (relative to win). Empty segments (tombstone values) are skipped by
-// the end_j > x search.
-template <class Tab>
-__device__ __forceinline__ void copy_column(const uint8_t* win, const Tab& tab, bool val, u32 n,
-                                            u32 tot, uint8_t* dst) {
+// Bytes [lo, hi) of the 4-byte word d (lo, hi in 0..16, relative to the chunk start).
+__device__ __forceinline__ u32 byte_mask(int lo, int hi, int d) {
+  const int a = max(lo - 4 * d, 0), b = min(hi - 4 * d, 4);
+  if (a >= b) return 0u;
+  const u32 top = b >= 4 ? ~0u : ((1u << (8 * b)) - 1u);
+  return top & (~0u << (8 * a));
+}
+
+// 64-bit OR over the wave (DPP row scans, then the four row results via readlane).
+__device__ __forceinline__ u64 wave_or64(u64 m) {
+  u32 lo = (u32)m, hi = (u32)(m >> 32);
+  lo |= dpp<kRowShr + 1>(lo); hi |= dpp<kRowShr + 1>(hi);
+  lo |= dpp<kRowShr + 2>(lo); hi |= dpp<kRowShr + 2>(hi);
+  lo |= dpp<kRowShr + 4>(lo); hi |= dpp<kRowShr + 4>(hi);
+  lo |= dpp<kRowShr + 8>(lo); hi |= dpp<kRowShr + 8>(hi);
+  lo = readlane(lo, 15) | readlane(lo, 31) | readlane(lo, 47) | readlane(lo, 63);
+  hi = readlane(hi, 15) | readlane(hi, 31) | readlane(hi, 47) | readlane(hi, 63);
+  return ((u64)hi << 32) | lo;
+}
+
+// Bytes [m, 16) of a chunk (m in 0..16): per-dword masks of the tail part.
+__device__ __forceinline__ u32 tail_mask(int m, int d) {
+  const int a = min(max(m - 4 * d, 0), 4);
+  return a >= 4 ? 0u : (~0u << (8 * a));
+}
+
+// Output-driven copy of one column (nk non-empty entries, tot bytes): the wave takes 64 output
+// chunks of 16 B at a time, lane l chunk c = t0 + l, so every store is a coalesced 1 KiB.
+// Chunk -> entry without a search: entry m of the window ends in lane tl_m's chunk range
+// (tl = ceil(end/16) - t0); when no two entries share a tl, OR-ing 1 << tl over the wave and a
+// popcount below each lane gives the number of entries that end before the lane's chunk, i.e.
+// the entry holding its first byte (a scalar walk over the window's entries otherwise).
+// The chunk is then assembled from that entry and, if it crosses an entry end, the next one
+// (two funnel-shifted LDS reads and a byte select); chunks spanning 3+ entries (entries shorter
+// than 16 B) take a loop.
+template <class Col>
+__device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, u32 nk, u32 tot,
+                                            uint8_t* dst) {
   const u32 lane = lane_id();
   const u32 nchunks = (tot + 15) >> 4;
-  u32 top = 1;
-  while (top * 2 <= n) top *= 2;
-  for (u32 c0 = 0; c0 < nchunks; c0 += 64) {
-    const u32 c = c0 + lane;
-    if (c >= nchunks) break;
-    const u32 x0 = c * 16;
-    // j = #entries with end <= x0 (upper bound), fixed-step binary search
-    u32 j = 0;
-    for (u32 step = top; step; step >>= 1)
-      if (j + step <= n && tab.end(val, j + step - 1) <= x0) j += step;
-    u32 end, src, st;
-    tab.get(val, j, end, src);
-    st = j ? tab.end(val, j - 1) : 0;
-    u32 w[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      const u32 x = x0 + 4 * d;
-      u32 word = 0;
-      if (x < tot) {
-        while (end <= x && j + 1 < n) { st = end; j++; tab.get(val, j, end, src); }
-        if (x + 4 <= end) {
-          word = lds_u32(win, src + (x - st));
-        } else {
-#pragma unroll
-          for (u32 bb = 0; bb < 4; bb++) {
-            const u32 xb = x + bb;
-            if (xb < tot) {
-              while (end <= xb && j + 1 < n) { st = end; j++; tab.get(val, j, end, src); }
-              word |= (u32)win[src + (xb - st)] << (8 * bb);
-            }
-          }
+  const u32 npad = (nchunks + 7) & ~7u;  // the slot is written in whole 128-byte lines
+#ifdef TPZ_ABL_MEMONLY
+  for (u32 c = lane; c < npad; c += 64) *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(c, 0, 0, 0);
+  return;
+#endif
+  u32 base = 0;  // entries ending at or before the window's first chunk start
+  for (u32 t0 = 0; t0 < npad; t0 += 64) {
+    const u32 c = t0 + lane;
+    u32 j = base;
+    if (t0 < nchunks) {
+      // entries base.. : the ones with tl < 64 end before some chunk start of this window
+      const u32 k = base + lane;
+      const u32 tl = k < nk ? min(((col.end(k) + 15) >> 4) - t0, 64u) : 64u;
+      const u64 inw = __ballot(tl < 64);
+      const u32 cnt = __builtin_popcountll(inw);
+      const u64 bits = wave_or64(tl < 64 ? (1ull << tl) : 0ull);
+      if (__builtin_popcountll(bits) == cnt && cnt < 64) {
+        const u64 le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        j = base + __builtin_popcountll(bits & le);
+        base += cnt;
+      } else {
+        // two entries end in one chunk, or >= 64 entries in the window: walk them
+        u32 m = base;
+        while (true) {
+          const u32 kk = m + lane;
+          const u32 t = kk < nk ? min(((col.end(kk) + 15) >> 4) - t0, 64u) : 64u;
+          const u32 n_here = __builtin_popcountll(__ballot(t < 64));
+          for (u32 q = 0; q < n_here; q++) j += readlane(t, q) <= lane ? 1u : 0u;
+          m += n_here;
+          if (n_here < 64) break;
+        }
+        base = m;
+      }
+    }
+    if (c < nchunks) {
+      const u32 x0 = c * 16;
+      u32 end0, end1 = 0;
+      int d0, d1 = 0;
+      col.get(j, end0, d0);
+      const bool more = j + 1 < nk;
+      if (more) col.get(j + 1, end1, d1);
+      uint4 acc = lds_window16(win, (int)x0 + d0);
+      const bool cross = end0 < x0 + 16 && more;
+      if (__ballot(cross)) {
+        const uint4 w = lds_window16(win, (int)x0 + d1);
+        const int m = cross ? (int)(end0 - x0) : 16;
+        acc.x = (acc.x & ~tail_mask(m, 0)) | (w.x & tail_mask(m, 0));
+        acc.y = (acc.y & ~tail_mask(m, 1)) | (w.y & tail_mask(m, 1));
+        acc.z = (acc.z & ~tail_mask(m, 2)) | (w.z & tail_mask(m, 2));
+        acc.w = (acc.w & ~tail_mask(m, 3)) | (w.w & tail_mask(m, 3));
+        // chunks spanning three or more entries
+        u32 k = j + 1, end = end1;
+        while (cross && end < x0 + 16 && k + 1 < nk) {
+          const int lo = (int)(end - x0);
+          k++;
+          int delta;
+          col.get(k, end, delta);
+          const int hi = min((int)(end - x0), 16);
+          const uint4 v = lds_window16(win, (int)x0 + delta);
+          acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
+          acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
+          acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
+          acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
         }
       }
-      w[d] = word;
+#ifdef TPZ_ABL_NOSTORE
+      asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+#else
+      *reinterpret_cast<uint4*>(dst + x0) = acc;
+#endif
+    } else if (c < npad) {
+      *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(0, 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(dst + x0) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b.
-// Returns true when the block was handed to the big path instead.
-template <class Tab, bool BIG>
-__device__ __forceinline__ bool decode_block(const u32* tab, uint8_t* win, const Tab& et, u32 a0,
-                                             u32 len, u32 b, u64 ext_b, const Out& o) {
+template <class Col, bool BIG>
+__device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
+                                             const Col& vcol, u32* hist, u32 a0, u32 len, u32 b,
+                                             u64 ext_b, const Out& o) {
   const u32 lane = lane_id();
-  if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return false; }           // compress.rs:96
-  const u32 tag = win[a0 + len - 1];                                                 // compress.rs:99
-  if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return false; } // :44-53,102
-  if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return false; }
-  if (len - 1 < 4) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, 0); return false; }     // block.rs:49
+#ifdef TPZ_ABL_LOADONLY
+  put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
+  return;
+#endif
+  if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
+  const u32 tag = win[a0 + len - 1];                                           // compress.rs:99
+  if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
+  if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
+  if (len - 1 < 4) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, 0); return; }     // block.rs:49
   const u32 P = len - 5;
   const int pb = (int)a0;
-  const u32 stored = bswap32(lds_u32(win, a0 + P));                                  // block.rs:51
+  const u32 stored = bswap32(lds_u32(win, a0 + P));                            // block.rs:51
   u32 crc;
   if (P >= 4) {
     // fold init 0xFFFFFFFF into the first four payload bytes, compute, restore
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
     __builtin_amdgcn_wave_barrier();
+#if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
+    crc = stored;
+#else
     crc = wave_crc(tab, win, pb, P);
+#endif
     __builtin_amdgcn_wave_barrier();
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
     __builtin_amdgcn_wave_barrier();
@@ -316,20 +409,24 @@ __device__ __forceinline__ bool decode_block(const u32* tab, uint8_t* win, const
     }
     crc = ~c;
   }
-  if (crc != stored) { put_meta(o, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc); return false; }
-  if (P < 2) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }          // block.rs:54
+  if (crc != stored) { put_meta(o, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc); return; }
+  if (P < 2) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }          // block.rs:54
   const u32 n = lds_be16(win, a0);
-  if (P < 2 + 2 * n) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }  // :56-59
+#ifdef TPZ_ABL_NOPARSE
+  put_meta(o, b, TPZ_BLOCK_OK, n, crc);
+  return;
+#endif
+  if (P < 2 + 2 * n) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }  // :56-59
   if (!BIG && n > kWaveMaxN) {
     if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
-    return true;
+    return;
   }
   const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
   const u32 dl = P - 2 - 2 * n;
   const bool slots_fit = 6u * n <= len;
-  u32* kend_g = o.kend + slot_base(ext_b, b);
-  u32* vend_g = o.vend + slot_base(ext_b, b);
-  u32 kc = 0, vc = 0;
+  uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
+  const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
+  u32 kc = 0, vc = 0, knz = 0, vnz = 0;
   bool bad = false;
   for (u32 g0 = 0; g0 < n; g0 += 64) {
     const u32 i = g0 + lane;
@@ -337,35 +434,39 @@ __device__ __forceinline__ bool decode_block(const u32* tab, uint8_t* win, const
     u32 off = 0, kl = 0, vl = 0;
     bool ok = true;
     if (act) {
-      off = lds_be16(win, a0 + 2 + 2 * i);                                          // iterator.rs:74
+      off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
       ok = off + 2 <= dl;
-      if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }            // :77-81
+      if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }        // :77-81
       if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
       if (!ok) kl = vl = 0;
     }
     bad |= __ballot(act && !ok) != 0;
     const u32 ki = wave_scan_incl(kl) + kc;
     const u32 vi = wave_scan_incl(vl) + vc;
+    const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+    if (slots_fit && i < n_pad) ends_g[i] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
     if (act && slots_fit) {
-      et.put(i, ki, db + off + 2, vi, db + off + 4 + kl);
-      kend_g[i] = ki;
-      vend_g[i] = vi;
+      if (kl) kcol.put(knz + lanes_below(kmask), ki, (int)(db + off + 2) - (int)(ki - kl));
+      if (vl) vcol.put(vnz + lanes_below(vmask), vi, (int)(db + off + 4 + kl) - (int)(vi - vl));
     }
-    kc = __shfl(ki, 63);
-    vc = __shfl(vi, 63);
+    knz += __builtin_popcountll(kmask);
+    vnz += __builtin_popcountll(vmask);
+    kc = readlane(ki, 63);
+    vc = readlane(vi, 63);
   }
-  if (bad) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return false; }
-  if (!slots_fit || kc > len || vc > len) { put_meta(o, b, TPZ_BLOCK_OVERLAP, n, crc); return false; }
+  if (bad) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }
+  if (!slots_fit || kc > len || vc > len) { put_meta(o, b, TPZ_BLOCK_OVERLAP, n, crc); return; }
   if (BIG) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   }
   __builtin_amdgcn_wave_barrier();
   const u64 kb = key_base(ext_b, b);
-  copy_column(win, et, false, n, kc, o.keys + kb);
-  copy_column(win, et, true, n, vc, o.vals + kb);
+#ifndef TPZ_ABL_NOCOPY
+  copy_column(win, kcol, knz, kc, o.keys + kb);
+  copy_column(win, vcol, vnz, vc, o.vals + kb);
+#endif
   put_meta(o, b, TPZ_BLOCK_OK, n, crc);
-  return false;
 }
 
 __device__ __forceinline__ void load_tables(u32* tab, const u32* gtab) {
@@ -412,8 +513,10 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 lane = lane_id();
   uint8_t* slot = lds + kTableBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
-  TabSmall et{reinterpret_cast<u32*>(win + kWinBytes + 32),
-              reinterpret_cast<u32*>(win + kWinBytes + 32 + kWaveMaxN * 4)};
+  uint8_t* etab = win + kWinBytes + 32;
+  const ColSmall kcol{reinterpret_cast<u32*>(etab)};
+  const ColSmall vcol{reinterpret_cast<u32*>(etab + kWaveMaxN * 4)};
+  u32* hist = reinterpret_cast<u32*>(etab + kWaveMaxN * 8);
 
   const u32 nw = gridDim.x * kWavesPerWG;
   u32 b = blockIdx.x * kWavesPerWG + wid;
@@ -457,7 +560,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     if (fits) {
-      decode_block<TabSmall, false>(tab, win, et, (u32)(s & 15u), len64, bcur, s, p.out);
+      decode_block<ColSmall, false>(tab, win, kcol, vcol, hist, (u32)(s & 15u), len64, bcur, s, p.out);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
@@ -474,8 +577,9 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
   load_tables(tab, p.crc_tables);
   const u32 lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
-  TabBig et{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots,
-            p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
+  u32* hist = reinterpret_cast<u32*>(win + kBigWinBytes + 32);
+  const ColBig kcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
+  const ColBig vcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
   const u32 cnt = uni(*p.out.defer_count);
   for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
     const u32 b = uni(p.out.defer_list[it]);
@@ -496,7 +600,7 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<TabBig, true>(tab, win, et, (u32)(s & 15u), len, b, s, p.out);
+    decode_block<ColBig, true>(tab, win, kcol, vcol, hist, (u32)(s & 15u), len, b, s, p.out);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -509,7 +613,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
   p.big_scratch = a.big_scratch;
-  p.out = Out{a.keys, a.vals, a.kend, a.vend, a.count, a.status, a.crc, a.defer_list, a.defer_count};
+  p.out = Out{a.keys, a.vals, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count};
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;

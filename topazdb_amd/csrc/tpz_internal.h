@@ -9,16 +9,19 @@
 namespace tpz {
 
 // CRC-32 lookup tables uploaded once per context (see tpz_api.cpp: build_crc_tables):
-// ids 0..15 = T_0..T_15; ids 16+4(j-1)+i = T_{(16<<j)-1-i} for j = 1..6.
+// ids 0..15 = T_0..T_15 (slice-by-16); ids 16+4j+i = T_{n_j-1-i}: the shift-by-n_j operator,
+// n_j = kCrcShiftBytes[j] (lane run 80 B, tree levels x2, row step 1280 B, super-round 5120 B).
 constexpr int kNumCrcTables = 40;
+constexpr int kCrcLaneBytes = 80;
+constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 5120};
 // Big path entry-table capacity per block: slots are only written when 6n <= len.
 constexpr uint32_t kBigMaxSlots = TPZ_MAX_BLOCK_BYTES / 6 + 16;
 
 // Slotted layout (include/tpz_gpu.h), callable from device code.
 __host__ __device__ inline uint64_t key_base(uint64_t ext_i, uint64_t i) {
-  return ((ext_i + 63u) & ~(uint64_t)63u) + 128u * i;
+  return ((ext_i + 127u) & ~(uint64_t)127u) + 256u * i;
 }
-__host__ __device__ inline uint64_t slot_base(uint64_t ext_i, uint64_t i) {
+__host__ __device__ inline uint64_t entry_base(uint64_t ext_i, uint64_t i) {
   return 16u * (ext_i / 96u + i);
 }
 
@@ -30,8 +33,7 @@ struct LaunchArgs {
   const uint32_t* crc_tables;
   uint8_t* keys;
   uint8_t* vals;
-  uint32_t* kend;
-  uint32_t* vend;
+  uint32_t* ends;
   uint32_t* count;
   uint8_t* status;
   uint32_t* crc;
