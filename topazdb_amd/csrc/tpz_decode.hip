@@ -42,23 +42,23 @@ constexpr int kWave = 64;
 constexpr int kWavesPerWG = 16;
 constexpr int kWGThreads = kWave * kWavesPerWG;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
-constexpr int kGuard = 32;
+constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
-// wave path slot: [guard 32][window 5120][pad 32][ktab n x u32][vtab n x u32][hist 64 x u32]
+// wave path slot: [guard 96][window 5120][pad 32][ktab n x u32][vtab n x u32]
 constexpr int kWinRounds = 5;                       // 5 x 1 KiB window
 constexpr int kWinBytes = kWinRounds * 1024;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
 constexpr u32 kWaveMaxN = 256;
-constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveMaxN * 8 + 256;
+constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveMaxN * 8;
 static_assert(kSlotBytes % 16 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard][window 92 KiB][pad][hist 64 x u32];
+// big path (one wave per block): [guard 96][window 92 KiB][pad];
 // entry tables in global scratch
 constexpr int kBigWinBytes = 94208;
 constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + 256;
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
 static_assert(kBigLds <= 163840, "big path LDS");
 
@@ -138,10 +138,13 @@ __device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
          tlook(tab, b0 + 2, (a >> 16) & 0xFF) ^ tlook(tab, b0 + 3, a >> 24);
 }
 
-// keep the bytes of the dword at payload position pos (4 bytes) that are at positions >= 0
-__device__ __forceinline__ u32 mask_front(u32 w, int pos) {
-  const int sh = min(max(-pos, 0), 4) * 8;
-  return sh >= 32 ? 0u : (w & (~0u << sh));
+// Zero the first k bytes of a 16-byte piece (k in 0..15).
+__device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
+  const u64 lo = (u64)v.y << 32 | v.x, hi = (u64)v.w << 32 | v.z;
+  const u64 mlo = k >= 8 ? 0ull : (~0ull << (8 * k));
+  const u64 mhi = k <= 8 ? ~0ull : (~0ull << (8 * (k - 8)));
+  const u64 a = lo & mlo, b = hi & mhi;
+  return make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
 }
 
 // CRC-32 of the payload at LDS offset pb (relative to win), length P >= 4, whose first four
@@ -160,10 +163,10 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
     if (seg + kCrcLaneBytes > 0) {
 #pragma unroll
       for (int t = 0; t < kCrcLaneBytes / 16; t++) {
-        const int start = seg + 16 * t;
-        const uint4 w = lds_window16(win, pb + max(start, -16));
-        c = slice16(tab, mask_front(w.x, start) ^ c, mask_front(w.y, start + 4),
-                    mask_front(w.z, start + 8), mask_front(w.w, start + 12));
+        // bytes before the payload read as zero: the zeroed guard, and the window's leading
+        // bytes (another block's tail) are zeroed when the window is staged
+        const uint4 w = lds_window16(win, pb + seg + 16 * t);
+        c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
       }
     }
     A = (r + 1 == S) ? c : (crc_shift<5>(tab, A) ^ c);
@@ -274,10 +277,14 @@ __device__ __forceinline__ u64 wave_or64(u64 m) {
   return ((u64)hi << 32) | lo;
 }
 
-// Bytes [m, 16) of a chunk (m in 0..16): per-dword masks of the tail part.
-__device__ __forceinline__ u32 tail_mask(int m, int d) {
-  const int a = min(max(m - 4 * d, 0), 4);
-  return a >= 4 ? 0u : (~0u << (8 * a));
+// acc = bytes [0, m) of a, bytes [m, 16) of w (m in 0..16).
+__device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
+  const u64 mlo = m >= 8 ? 0ull : (~0ull << (8 * m));          // bytes taken from w, low half
+  const u64 mhi = m <= 8 ? ~0ull : (m >= 16 ? 0ull : (~0ull << (8 * (m - 8))));
+  const u64 alo = (u64)a.y << 32 | a.x, ahi = (u64)a.w << 32 | a.z;
+  const u64 wlo = (u64)w.y << 32 | w.x, whi = (u64)w.w << 32 | w.z;
+  const u64 lo = (alo & ~mlo) | (wlo & mlo), hi = (ahi & ~mhi) | (whi & mhi);
+  return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
 }
 
 // Output-driven copy of one column (nk non-empty entries, tot bytes): the wave takes 64 output
@@ -330,20 +337,16 @@ __device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, 
     }
     if (c < nchunks) {
       const u32 x0 = c * 16;
-      u32 end0, end1 = 0;
-      int d0, d1 = 0;
-      col.get(j, end0, d0);
+      u32 end0, end1;
+      int d0, d1;
       const bool more = j + 1 < nk;
-      if (more) col.get(j + 1, end1, d1);
+      col.get(j, end0, d0);
+      col.get(more ? j + 1 : j, end1, d1);
       uint4 acc = lds_window16(win, (int)x0 + d0);
       const bool cross = end0 < x0 + 16 && more;
       if (__ballot(cross)) {
         const uint4 w = lds_window16(win, (int)x0 + d1);
-        const int m = cross ? (int)(end0 - x0) : 16;
-        acc.x = (acc.x & ~tail_mask(m, 0)) | (w.x & tail_mask(m, 0));
-        acc.y = (acc.y & ~tail_mask(m, 1)) | (w.y & tail_mask(m, 1));
-        acc.z = (acc.z & ~tail_mask(m, 2)) | (w.z & tail_mask(m, 2));
-        acc.w = (acc.w & ~tail_mask(m, 3)) | (w.w & tail_mask(m, 3));
+        acc = merge_at(acc, w, cross ? (int)(end0 - x0) : 16);
         // chunks spanning three or more entries
         u32 k = j + 1, end = end1;
         while (cross && end < x0 + 16 && k + 1 < nk) {
@@ -373,7 +376,7 @@ __device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, 
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b.
 template <class Col, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
-                                             const Col& vcol, u32* hist, u32 a0, u32 len, u32 b,
+                                             const Col& vcol, u32 a0, u32 len, u32 b,
                                              u64 ext_b, const Out& o) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
@@ -516,8 +519,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   uint8_t* etab = win + kWinBytes + 32;
   const ColSmall kcol{reinterpret_cast<u32*>(etab)};
   const ColSmall vcol{reinterpret_cast<u32*>(etab + kWaveMaxN * 4)};
-  u32* hist = reinterpret_cast<u32*>(etab + kWaveMaxN * 8);
 
+  if (lane < kGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   const u32 nw = gridDim.x * kWavesPerWG;
   u32 b = blockIdx.x * kWavesPerWG + wid;
 
@@ -551,6 +554,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     const bool fits = (e - s) <= kWaveMaxLen;
     if (fits) {
       const u32 rounds = (u32)((e - (s & ~15ull)) + 1023) >> 10;
+      v[0] = zero_head(v[0], lane == 0 ? (u32)(s & 15u) : 0u);  // the previous block's tail
 #pragma unroll
       for (int r = 0; r < kWinRounds; r++)
         if ((u32)r < rounds) *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
@@ -560,7 +564,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     if (fits) {
-      decode_block<ColSmall, false>(tab, win, kcol, vcol, hist, (u32)(s & 15u), len64, bcur, s, p.out);
+      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
   load_tables(tab, p.crc_tables);
   const u32 lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
-  u32* hist = reinterpret_cast<u32*>(win + kBigWinBytes + 32);
+  if (lane < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[lane] = make_uint4(0, 0, 0, 0);
   const ColBig kcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
   const ColBig vcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
   const u32 cnt = uni(*p.out.defer_count);
@@ -596,11 +600,12 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         fix_tail(t[r], p.src, ws + off + r * 1024 + lane * 16, p.src_bytes);
+        if (r == 0 && off == 0) t[0] = zero_head(t[0], lane == 0 ? (u32)(s & 15u) : 0u);
         if (off + r * 1024 < nbytes) *reinterpret_cast<uint4*>(win + off + r * 1024 + lane * 16) = t[r];
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, true>(tab, win, kcol, vcol, hist, (u32)(s & 15u), len, b, s, p.out);
+    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out);
     __builtin_amdgcn_wave_barrier();
   }
 }
