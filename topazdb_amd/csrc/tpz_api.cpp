@@ -26,7 +26,7 @@ tpz_err hip_fail(hipError_t e, const char* what) {
 
 // T_k[b] = raw CRC-32 (reflected 0xEDB88320, init 0, no xorout) of byte b followed by k zero
 // bytes; T_{k+1}[b] = (T_k[b] >> 8) ^ T_0[T_k[b] & 0xFF]. Only the 40 tables the kernels use
-// are kept (ids documented in tpz_internal.h).
+// are kept, plus the inverse of T_0's top byte (ids documented in tpz_internal.h).
 std::vector<uint32_t> build_crc_tables() {
   const int kmax = 5120;
   std::vector<uint32_t> all((size_t)kmax * 256);
@@ -49,6 +49,7 @@ std::vector<uint32_t> build_crc_tables() {
     const int n = tpz::kCrcShiftBytes[j];
     for (int i = 0; i < 4; i++) put(16 + 4 * j + i, n - 1 - i);
   }
+  for (uint32_t b = 0; b < 256; b++) out[(size_t)tpz::kCrcInvTable * 256 + (all[b] >> 24)] = b;
   return out;
 }
 

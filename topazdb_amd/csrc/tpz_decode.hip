@@ -94,9 +94,15 @@ __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 // 16 bytes starting at signed LDS byte offset x (relative to base, base 16-aligned): two
 // ds_read_b128 then a per-lane funnel shift by x & 15.
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+#ifndef TPZ_ABL_FUNNEL
+  // gfx950 LDS serves a ds_read_b128 at any byte address (unaligned DS access mode).
+  typedef u32x4 u32x4_u __attribute__((aligned(1)));
+  const u32x4 v = *reinterpret_cast<const u32x4_u*>(base + x);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#endif
   // Two whole ds_read_b128. The empty asm hides the loads from the selects below: otherwise
   // hipcc turns "select of loaded dwords" into branches and sinks dword-sized reads into them.
-  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* p = reinterpret_cast<const u32x4*>(base + (x & ~15));
   u32x4 va = p[0], vb = p[1];
   asm volatile("" : "+v"(va), "+v"(vb));
@@ -117,25 +123,44 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
 // ids 0..15: T_0..T_15 (slice-by-16); ids 16+4j+i: T_{n_j-1-i}, n_j = kCrcShiftBytes[j].
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
 
+// a ^ b ^ c in one v_bitop3_b32.
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
 // R0 of one 16-byte chunk (little-endian dwords w0..w3): XOR_i T_{15-i}[c_i].
 __device__ __forceinline__ u32 slice16(const u32* tab, u32 w0, u32 w1, u32 w2, u32 w3) {
-  u32 c = tlook(tab, 15, w0 & 0xFF) ^ tlook(tab, 14, (w0 >> 8) & 0xFF) ^
-          tlook(tab, 13, (w0 >> 16) & 0xFF) ^ tlook(tab, 12, w0 >> 24);
-  c ^= tlook(tab, 11, w1 & 0xFF) ^ tlook(tab, 10, (w1 >> 8) & 0xFF) ^
-       tlook(tab, 9, (w1 >> 16) & 0xFF) ^ tlook(tab, 8, w1 >> 24);
-  c ^= tlook(tab, 7, w2 & 0xFF) ^ tlook(tab, 6, (w2 >> 8) & 0xFF) ^
-       tlook(tab, 5, (w2 >> 16) & 0xFF) ^ tlook(tab, 4, w2 >> 24);
-  c ^= tlook(tab, 3, w3 & 0xFF) ^ tlook(tab, 2, (w3 >> 8) & 0xFF) ^
-       tlook(tab, 1, (w3 >> 16) & 0xFF) ^ tlook(tab, 0, w3 >> 24);
-  return c;
+  u32 c = xor3(tlook(tab, 15, w0 & 0xFF), tlook(tab, 14, (w0 >> 8) & 0xFF), tlook(tab, 13, (w0 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 12, w0 >> 24), tlook(tab, 11, w1 & 0xFF));
+  c = xor3(c, tlook(tab, 10, (w1 >> 8) & 0xFF), tlook(tab, 9, (w1 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 8, w1 >> 24), tlook(tab, 7, w2 & 0xFF));
+  c = xor3(c, tlook(tab, 6, (w2 >> 8) & 0xFF), tlook(tab, 5, (w2 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 4, w2 >> 24), tlook(tab, 3, w3 & 0xFF));
+  c = xor3(c, tlook(tab, 2, (w3 >> 8) & 0xFF), tlook(tab, 1, (w3 >> 16) & 0xFF));
+  return c ^ tlook(tab, 0, w3 >> 24);
+}
+
+// shift_k(A) = R_A(0^k) for a wave-uniform k in 0..15, from the slice tables T_0..T_15.
+__device__ __forceinline__ u32 crc_shift_small(const u32* tab, u32 a, u32 k) {
+  u32 r = k >= 4 ? 0u : (a >> (8 * k));
+  for (u32 i = 0; i < 4 && i < k; i++) r ^= tlook(tab, (int)(k - 1 - i), (a >> (8 * i)) & 0xFF);
+  return r;
+}
+
+// Inverse of shift_k: un-feed k zero bytes (crc' = (crc >> 8) ^ T_0[crc & 0xFF] is invertible
+// because the top byte of T_0[b] determines b). Only used to report a mismatching CRC.
+__device__ __forceinline__ u32 crc_unshift_small(const u32* tab, u32 r, u32 k) {
+  for (u32 i = 0; i < k; i++) {
+    const u32 b = tlook(tab, kCrcInvTable, r >> 24);
+    r = ((r ^ tlook(tab, 0, b)) << 8) | b;
+  }
+  return r;
 }
 
 // shift_n(A) = R_A(0^n) = XOR_i T_{n-1-i}[byte_i(A)], n = kCrcShiftBytes[J].
 template <int J>
 __device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
   constexpr int b0 = 16 + 4 * J;
-  return tlook(tab, b0, a & 0xFF) ^ tlook(tab, b0 + 1, (a >> 8) & 0xFF) ^
-         tlook(tab, b0 + 2, (a >> 16) & 0xFF) ^ tlook(tab, b0 + 3, a >> 24);
+  return xor3(tlook(tab, b0, a & 0xFF), tlook(tab, b0 + 1, (a >> 8) & 0xFF),
+              tlook(tab, b0 + 2, (a >> 16) & 0xFF)) ^ tlook(tab, b0 + 3, a >> 24);
 }
 
 // Zero the first k bytes of a 16-byte piece (k in 0..15).
@@ -147,25 +172,28 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
   return make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
 }
 
-// CRC-32 of the payload at LDS offset pb (relative to win), length P >= 4, whose first four
-// bytes have already been complemented (init 0xFFFFFFFF folded into the message).
-// The payload is cut into 80-byte runs aligned to its END (leading zero padding leaves a raw CRC
-// unchanged); lane l folds run l (counted from the end) with five chained slice-by-16 steps,
+// Raw CRC R0 of the LDS bytes [pb, pb + Pa), where pb + Pa is 16-byte aligned: the payload
+// (first four bytes already complemented: init 0xFFFFFFFF folded into the message) followed by
+// the zero bytes that pad it to the 16-byte boundary (the caller compares in that shifted domain).
+// The range is cut into 80-byte runs aligned to its END (leading zero padding leaves a raw CRC
+// unchanged), so every LDS read is an aligned ds_read_b128 (80-byte lane stride: conflict-free
+// per 16 lanes); lane l folds run l (counted from the end) with five chained slice-by-16 steps,
 // super-rounds of 64 runs (5120 B) are chained with a shift-by-5120 operator, and the lanes are
-// combined by a tree of shift-by-80*2^k operators. Returns ~R0(payload') (wave-uniform).
-__device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int pb, u32 P) {
+// combined by a tree of shift-by-80*2^k operators. Returns R0 (wave-uniform).
+__device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
   const u32 lane = lane_id();
-  const u32 S = (P + 5119) / 5120;      // super-rounds, end-aligned
+  const u32 S = (Pa + 5119) / 5120;      // super-rounds, end-aligned
   u32 A = 0;
   for (u32 r = S; r-- > 0;) {
-    const int seg = (int)P - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
+    const int seg = (int)Pa - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
     u32 c = 0;
     if (seg + kCrcLaneBytes > 0) {
 #pragma unroll
       for (int t = 0; t < kCrcLaneBytes / 16; t++) {
         // bytes before the payload read as zero: the zeroed guard, and the window's leading
         // bytes (another block's tail) are zeroed when the window is staged
-        const uint4 w = lds_window16(win, pb + seg + 16 * t);
+        const u32x4 w = *reinterpret_cast<const u32x4*>(win + pb + seg + 16 * t);
         c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
       }
     }
@@ -182,7 +210,7 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
   t = readlane(A, 32) ^ crc_shift<4>(tab, t);
   t = readlane(A, 16) ^ crc_shift<4>(tab, uni(t));
   t = readlane(A, 0) ^ crc_shift<4>(tab, uni(t));
-  return ~uni(t);
+  return uni(t);
 }
 
 // ------------------------------------------------------------------ entry tables
@@ -296,8 +324,20 @@ __device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
 // The chunk is then assembled from that entry and, if it crosses an entry end, the next one
 // (two funnel-shifted LDS reads and a byte select); chunks spanning 3+ entries (entries shorter
 // than 16 B) take a loop.
-template <class Col>
-__device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, u32 nk, u32 tot,
+// Source of the copy: the LDS window, or (GL) the same bytes re-read through the block's buffer
+// resource (L2/MALL-resident: the window was fetched from HBM one block earlier).
+template <bool GL>
+struct Src16 {
+  const uint8_t* win;
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ uint4 operator()(int x) const {
+    if (GL) return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)x, 0, 0));
+    return lds_window16(win, x);
+  }
+};
+
+template <class Col, class S>
+__device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk, u32 tot,
                                             uint8_t* dst) {
   const u32 lane = lane_id();
   const u32 nchunks = (tot + 15) >> 4;
@@ -342,10 +382,10 @@ __device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, 
       const bool more = j + 1 < nk;
       col.get(j, end0, d0);
       col.get(more ? j + 1 : j, end1, d1);
-      uint4 acc = lds_window16(win, (int)x0 + d0);
+      uint4 acc = src((int)x0 + d0);
       const bool cross = end0 < x0 + 16 && more;
       if (__ballot(cross)) {
-        const uint4 w = lds_window16(win, (int)x0 + d1);
+        const uint4 w = src((int)x0 + d1);
         acc = merge_at(acc, w, cross ? (int)(end0 - x0) : 16);
         // chunks spanning three or more entries
         u32 k = j + 1, end = end1;
@@ -355,7 +395,7 @@ __device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, 
           int delta;
           col.get(k, end, delta);
           const int hi = min((int)(end - x0), 16);
-          const uint4 v = lds_window16(win, (int)x0 + delta);
+          const uint4 v = src((int)x0 + delta);
           acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
           acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
           acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
@@ -377,7 +417,8 @@ __device__ __forceinline__ void copy_column(const uint8_t* win, const Col& col, 
 template <class Col, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
                                              const Col& vcol, u32 a0, u32 len, u32 b,
-                                             u64 ext_b, const Out& o) {
+                                             u64 ext_b, const Out& o, __amdgpu_buffer_rsrc_t rs,
+                                             bool gl) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
@@ -393,13 +434,19 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   const u32 stored = bswap32(lds_u32(win, a0 + P));                            // block.rs:51
   u32 crc;
   if (P >= 4) {
-    // fold init 0xFFFFFFFF into the first four payload bytes, compute, restore
+    // fold init 0xFFFFFFFF into the first four payload bytes; zero the k bytes from the payload
+    // end to the next 16-byte boundary (stored CRC and tag are already in registers). Then
+    // R = R0(payload' || 0^k) = shift_k(R0(payload')), which equals shift_k(~stored) iff the CRC
+    // matches.
+    const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
+    if (lane < k) win[a0 + P + lane] = 0;
     __builtin_amdgcn_wave_barrier();
 #if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
     crc = stored;
 #else
-    crc = wave_crc(tab, win, pb, P);
+    const u32 R = wave_crc(tab, win, pb, P + k);
+    crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
 #endif
     __builtin_amdgcn_wave_barrier();
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
@@ -466,8 +513,18 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   __builtin_amdgcn_wave_barrier();
   const u64 kb = key_base(ext_b, b);
 #ifndef TPZ_ABL_NOCOPY
-  copy_column(win, kcol, knz, kc, o.keys + kb);
-  copy_column(win, vcol, vnz, vc, o.vals + kb);
+#ifdef TPZ_ABL_GCOPY
+  if (gl) {
+    const Src16<true> sg{win, rs};
+    copy_column(sg, kcol, knz, kc, o.keys + kb);
+    copy_column(sg, vcol, vnz, vc, o.vals + kb);
+  } else
+#endif
+  {
+    const Src16<false> sl{win, rs};
+    copy_column(sl, kcol, knz, kc, o.keys + kb);
+    copy_column(sl, vcol, vnz, vc, o.vals + kb);
+  }
 #endif
   put_meta(o, b, TPZ_BLOCK_OK, n, crc);
 }
@@ -564,7 +621,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     if (fits) {
-      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out);
+      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out,
+                                    window_rsrc(p.src, p.src_bytes, s & ~15ull), e + 16 <= p.src_bytes);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
@@ -605,7 +663,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out);
+    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out, rs,
+                               e + 16 <= p.src_bytes);
     __builtin_amdgcn_wave_barrier();
   }
 }
