@@ -218,6 +218,44 @@ def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
     return float(ext[-1] - ext[0]) / dt / GIB
 
 
+DEFAULT_BLOCKS = {"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}
+
+
+def shard_seed(config: str, rank: int) -> int:
+    """Rank r's shard of an N x nb-block data set: its own generator seed (round-robin shards
+    with no overlap and no exchange)."""
+    return synth.CONFIGS[config]["seed"] + 7919 * rank
+
+
+def make_shard(config: str, nb: int, rank: int):
+    """This rank's nb blocks: (src, ext, gen, entries per block, key bytes, value bytes)."""
+    cfg = synth.CONFIGS[config]
+    if cfg["klen"] is None:
+        n_gen = 34 * nb
+    else:
+        n_gen = (cfg["block_size"] - 2) // (4 + cfg["klen"] + cfg["vlen"]) * nb
+    gen = synth.entries(config, n_gen, shard_seed(config, rank))
+    src, ext = synth.build_blocks(*gen, cfg["block_size"])
+    ext = ext[:nb + 1].copy()
+    src = src[:int(ext[-1])]
+    n_ent = block_counts(src, ext)
+    etot = int(n_ent.sum())
+    return src, ext, gen, n_ent, int(gen[1][etot]), int(gen[3][etot])
+
+
+def max_over_ranks(dist, vals, device) -> list[float]:
+    """MAX over ranks of the per-rank timings (the only collective; not on the data path)."""
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def job_rate(in_bytes_per_rank: float, world: int, steps: int, wall_max: float) -> float:
+    """Whole-job GiB/s: every rank's input bytes over the slowest rank's time."""
+    return in_bytes_per_rank * world * steps / wall_max / GIB
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,29 +279,16 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    nb = args.blocks or ({"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}[args.config])
+    nb = args.blocks or DEFAULT_BLOCKS[args.config]
     t0 = time.time()
-    # round-robin shard r of an N x nb data set: each rank generates its own blocks
-    seed = synth.CONFIGS[args.config]["seed"] + 7919 * rank
-    n_gen = (34 * nb) if synth.CONFIGS[args.config]["klen"] is None else None
-    if n_gen is None:
-        cfg = synth.CONFIGS[args.config]
-        n_gen = (cfg["block_size"] - 2) // (4 + cfg["klen"] + cfg["vlen"]) * nb
-    gen = synth.entries(args.config, n_gen, seed)
-    src, ext = synth.build_blocks(*gen, synth.CONFIGS[args.config]["block_size"])
-    ext = ext[:nb + 1].copy()
-    src = src[:int(ext[-1])]
-    n_ent = block_counts(src, ext)
-    kpos, vpos = gen[1], gen[3]
-    etot = int(n_ent.sum())
-    kbytes, vbytes = int(kpos[etot]), int(vpos[etot])
+    src, ext, gen, n_ent, kbytes, vbytes = make_shard(args.config, nb, rank)
     log(rank, f"generated {nb} blocks ({src.nbytes / GIB:.2f} GiB) in {time.time() - t0:.1f} s")
 
     ctx = _lib.Context(local)
-    ctx.reserve(nb)
     batch = DeviceBatch(src, ext, local)
     cols = SlottedColumns(nb, batch.src_bytes, local)
     stream = torch.cuda.current_stream(dev)
+    ctx.reserve(nb, stream.cuda_stream)
 
     for _ in range(args.warmup):
         decode_batch(ctx, batch, cols, stream)
@@ -283,13 +308,9 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t_start
     ev_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([wall, ev_ms], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, ev_ms_max = float(t[0]), float(t[1])
+    wall_max, ev_ms_max = max_over_ranks(dist, [wall, ev_ms], dev)
     in_bytes = float(ext[-1] - ext[0])
-    total_in = in_bytes * world
-    value = total_in * args.steps / wall_max / GIB
+    value = job_rate(in_bytes, world, args.steps, wall_max)
     alg = algorithmic_bytes(ext, n_ent, kbytes, vbytes)
     achieved = alg / (ev_ms_max * 1e-3) / 1e9
 

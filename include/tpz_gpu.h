@@ -15,8 +15,9 @@
  * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
  * device; h_* are host pointers. `stream` is a hipStream_t passed as void* (NULL = default).
  * Every call is asynchronous on `stream` unless it says otherwise; the library never frees
- * caller memory and holds no global mutable state (one context per device, many host threads
- * may share it if each uses its own stream).
+ * caller memory and holds no global mutable state (one context per device; many host threads
+ * may share it, and decodes on different streams run concurrently: every stream gets its own
+ * device workspace).
  */
 #ifndef TPZ_GPU_H
 #define TPZ_GPU_H
@@ -122,9 +123,10 @@ typedef struct tpz_ctx tpz_ctx;
 tpz_err tpz_ctx_create(int device, tpz_ctx** out);
 void tpz_ctx_destroy(tpz_ctx* ctx);
 
-/* Pre-sizes the context's device workspace for batches of up to max_blocks blocks so that
- * tpz_decode_blocks never allocates (needed before capturing it in a hipGraph). */
-tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks);
+/* Pre-sizes the device workspace `stream` uses for batches of up to max_blocks blocks, so that
+ * tpz_decode_blocks on that stream never allocates (needed before capturing it in a hipGraph).
+ * Each stream gets its own workspace, so decodes on different streams may run concurrently. */
+tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
 
 /* ---- the hot path ------------------------------------------------------------------------ */
 /* Checksum-verify and decode every block of `batch` into `out`. Asynchronous on `stream`;

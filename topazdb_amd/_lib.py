@@ -59,7 +59,8 @@ def lib() -> C.CDLL:
         L.tpz_ctx_create.restype = C.c_int
         L.tpz_ctx_destroy.argtypes = [C.c_void_p]
         L.tpz_ctx_destroy.restype = None
-        L.tpz_ctx_reserve.argtypes = [C.c_void_p, C.c_uint32]
+        L.tpz_ctx_reserve.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.tpz_ctx_reserve.restype = C.c_int
         L.tpz_decode_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
                                         C.c_void_p]
         L.tpz_decode_blocks.restype = C.c_int
@@ -111,8 +112,9 @@ class Context:
         check(lib().tpz_ctx_create(device, C.byref(h)), "tpz_ctx_create")
         self.handle = h
 
-    def reserve(self, max_blocks: int) -> None:
-        check(lib().tpz_ctx_reserve(self.handle, max_blocks), "tpz_ctx_reserve")
+    def reserve(self, max_blocks: int, stream: int = 0) -> None:
+        check(lib().tpz_ctx_reserve(self.handle, max_blocks, C.c_void_p(stream)),
+              "tpz_ctx_reserve")
 
     def close(self) -> None:
         if getattr(self, "handle", None):

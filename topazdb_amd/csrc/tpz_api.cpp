@@ -5,6 +5,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "tpz_internal.h"
@@ -55,15 +56,52 @@ std::vector<uint32_t> build_crc_tables() {
 
 }  // namespace
 
+// Device workspace of one stream: the big-path worklist (counter + list) and the big path's
+// per-workgroup entry tables. Decodes on different streams run concurrently, so each stream
+// has its own; decodes on one stream are ordered by the stream.
+struct tpz_workspace {
+  uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
+  uint32_t defer_cap = 0;
+  uint64_t* d_big_scratch = nullptr;
+};
+
 struct tpz_ctx {
   int device = 0;
   uint32_t num_cus = 0;
   uint32_t* d_tables = nullptr;
-  uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
-  uint64_t* d_big_scratch = nullptr;
-  uint32_t defer_cap = 0;
-  std::mutex mu;  // guards workspace growth only
+  std::mutex mu;  // guards the workspace map
+  std::unordered_map<void*, tpz_workspace> ws;
 };
+
+namespace {
+
+void free_workspace(tpz_workspace& w) {
+  if (w.d_defer) (void)hipFree(w.d_defer);
+  if (w.d_big_scratch) (void)hipFree(w.d_big_scratch);
+  w = tpz_workspace{};
+}
+
+// The stream's workspace, grown to max_blocks. Caller holds c->mu.
+tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspace** out) {
+  tpz_workspace& w = c->ws[stream];
+  if (!w.d_big_scratch)
+    TPZ_HIP(hipMalloc(&w.d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t)));
+  if (!w.d_defer || w.defer_cap < max_blocks) {
+    uint32_t* d = nullptr;
+    TPZ_HIP(hipMalloc(&d, ((size_t)max_blocks + 1) * 4));
+    if (w.d_defer) {
+      // an earlier decode on this stream may still be reading the old list
+      (void)hipStreamSynchronize((hipStream_t)stream);
+      (void)hipFree(w.d_defer);
+    }
+    w.d_defer = d;
+    w.defer_cap = max_blocks;
+  }
+  *out = &w;
+  return TPZ_SUCCESS;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -95,8 +133,6 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
   std::vector<uint32_t> t = build_crc_tables();
   hipError_t e = hipMalloc(&c->d_tables, t.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(c->d_tables, t.data(), t.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipMalloc(&c->d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t));
   if (e != hipSuccess) {
     tpz_ctx_destroy(c);
     return hip_fail(e, "tpz_ctx_create");
@@ -108,26 +144,18 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
 void tpz_ctx_destroy(tpz_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();  // decodes still in flight use the workspaces
   if (c->d_tables) (void)hipFree(c->d_tables);
-  if (c->d_defer) (void)hipFree(c->d_defer);
-  if (c->d_big_scratch) (void)hipFree(c->d_big_scratch);
+  for (auto& kv : c->ws) free_workspace(kv.second);
   delete c;
 }
 
-tpz_err tpz_ctx_reserve(tpz_ctx* c, uint32_t max_blocks) {
+tpz_err tpz_ctx_reserve(tpz_ctx* c, uint32_t max_blocks, void* stream) {
   if (!c) return TPZ_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (max_blocks <= c->defer_cap && c->d_defer) return TPZ_SUCCESS;
   TPZ_HIP(hipSetDevice(c->device));
-  uint32_t* d = nullptr;
-  TPZ_HIP(hipMalloc(&d, ((size_t)max_blocks + 1) * 4));
-  if (c->d_defer) {
-    (void)hipDeviceSynchronize();  // an in-flight decode may still use the old list
-    (void)hipFree(c->d_defer);
-  }
-  c->d_defer = d;
-  c->defer_cap = max_blocks;
-  return TPZ_SUCCESS;
+  std::lock_guard<std::mutex> g(c->mu);
+  tpz_workspace* w = nullptr;
+  return get_workspace(c, stream, max_blocks, &w);
 }
 
 tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, void* stream) {
@@ -136,13 +164,15 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_vals || !o->d_ends || !o->d_count ||
       !o->d_status || !o->d_crc)
     return TPZ_ERR_INVALID_ARG;
-  if (b->n_blocks > c->defer_cap || !c->d_defer) {
-    tpz_err r = tpz_ctx_reserve(c, b->n_blocks);
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz_workspace* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = get_workspace(c, stream, b->n_blocks, &w);
     if (r != TPZ_SUCCESS) return r;
   }
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipSetDevice(c->device));
-  TPZ_HIP(hipMemsetAsync(c->d_defer, 0, 4, s));
+  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 4, s));
   tpz::LaunchArgs a{};
   a.src = b->d_src;
   a.ext = b->d_ext;
@@ -155,10 +185,10 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.count = o->d_count;
   a.status = o->d_status;
   a.crc = o->d_crc;
-  a.defer_count = c->d_defer;
-  a.defer_list = c->d_defer + 1;
+  a.defer_count = w->d_defer;
+  a.defer_list = w->d_defer + 1;
   a.num_cus = c->num_cus;
-  a.big_scratch = c->d_big_scratch;
+  a.big_scratch = w->d_big_scratch;
   a.big_grid = c->num_cus;
   tpz::launch_decode(a, s);
   TPZ_HIP(hipGetLastError());

@@ -350,7 +350,11 @@ __device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk
   for (u32 t0 = 0; t0 < npad; t0 += 64) {
     const u32 c = t0 + lane;
     u32 j = base;
+#ifdef TPZ_ABL_NOMAP
+    if (false) {
+#else
     if (t0 < nchunks) {
+#endif
       // entries base.. : the ones with tl < 64 end before some chunk start of this window
       const u32 k = base + lane;
       const u32 tl = k < nk ? min(((col.end(k) + 15) >> 4) - t0, 64u) : 64u;
@@ -384,7 +388,11 @@ __device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk
       col.get(more ? j + 1 : j, end1, d1);
       uint4 acc = src((int)x0 + d0);
       const bool cross = end0 < x0 + 16 && more;
+#ifdef TPZ_ABL_NOCROSS
+      if (false) {
+#else
       if (__ballot(cross)) {
+#endif
         const uint4 w = src((int)x0 + d1);
         acc = merge_at(acc, w, cross ? (int)(end0 - x0) : 16);
         // chunks spanning three or more entries
