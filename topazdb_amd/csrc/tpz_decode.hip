@@ -39,7 +39,13 @@ typedef uint64_t u64;
 
 // ------------------------------------------------------------------ LDS geometry
 constexpr int kWave = 64;
+#ifdef TPZ_ABL_W8
+constexpr int kWavesPerWG = 8;
+#elif defined(TPZ_ABL_W12)
+constexpr int kWavesPerWG = 12;
+#else
 constexpr int kWavesPerWG = 16;
+#endif
 constexpr int kWGThreads = kWave * kWavesPerWG;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
@@ -91,18 +97,19 @@ __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
-// 16 bytes starting at signed LDS byte offset x (relative to base, base 16-aligned): two
-// ds_read_b128 then a per-lane funnel shift by x & 15.
+// 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: three
+// 8-byte-aligned ds_read_b64 (24 B), a one-bit dword select and v_alignbyte (9 VALU). A
+// ds_read_b128 off 16-byte alignment would be replayed at 64 LDS cycles (TPZ_ABL_UNALIGNED).
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-#ifndef TPZ_ABL_FUNNEL
-  // gfx950 LDS serves a ds_read_b128 at any byte address (unaligned DS access mode).
+  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+#if defined(TPZ_ABL_UNALIGNED)
   typedef u32x4 u32x4_u __attribute__((aligned(1)));
   const u32x4 v = *reinterpret_cast<const u32x4_u*>(base + x);
   return make_uint4(v.x, v.y, v.z, v.w);
-#endif
-  // Two whole ds_read_b128. The empty asm hides the loads from the selects below: otherwise
-  // hipcc turns "select of loaded dwords" into branches and sinks dword-sized reads into them.
+#elif defined(TPZ_ABL_FUNNEL)
+  // two aligned ds_read_b128 + a two-bit dword select. The empty asm hides the loads from the
+  // selects: otherwise hipcc turns "select of loaded dwords" into branches around dword reads.
   const u32x4* p = reinterpret_cast<const u32x4*>(base + (x & ~15));
   u32x4 va = p[0], vb = p[1];
   asm volatile("" : "+v"(va), "+v"(vb));
@@ -116,6 +123,17 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
   const u32 w4 = q < 2 ? (q == 0 ? b.x : b.y) : (q == 2 ? b.z : b.w);
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
                     __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
+#else
+  const u32x2* p = reinterpret_cast<const u32x2*>(base + (x & ~7));
+  u32x2 a = p[0], b = p[1], c = p[2];
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+  const u32 s = (u32)x & 3u;
+  const bool h = ((u32)x & 4u) != 0;
+  const u32 s0 = h ? a.y : a.x, s1 = h ? b.x : a.y, s2 = h ? b.y : b.x, s3 = h ? c.x : b.y,
+            s4 = h ? c.y : c.x;
+  return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, s), __builtin_amdgcn_alignbyte(s2, s1, s),
+                    __builtin_amdgcn_alignbyte(s3, s2, s), __builtin_amdgcn_alignbyte(s4, s3, s));
+#endif
 }
 
 // ------------------------------------------------------------------ CRC-32 (table driven)
@@ -177,9 +195,11 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
 // the zero bytes that pad it to the 16-byte boundary (the caller compares in that shifted domain).
 // The range is cut into 80-byte runs aligned to its END (leading zero padding leaves a raw CRC
 // unchanged), so every LDS read is an aligned ds_read_b128 (80-byte lane stride: conflict-free
-// per 16 lanes); lane l folds run l (counted from the end) with five chained slice-by-16 steps,
-// super-rounds of 64 runs (5120 B) are chained with a shift-by-5120 operator, and the lanes are
-// combined by a tree of shift-by-80*2^k operators. Returns R0 (wave-uniform).
+// per 16 lanes); lane l folds run l (counted from the end) with five chained slice-by-16 steps;
+// super-rounds of 64 runs (5120 B, long blocks only) are chained with two shift-by-2560 steps.
+// Run l then sits 80*l bytes before the end: every lane applies shift-by-80*2^k for the set bits
+// k of l (six levels, the same instruction stream in all lanes), and the lanes' values are
+// XOR-ed together with DPP and readlane. Returns R0 (wave-uniform).
 __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
   const u32 lane = lane_id();
@@ -197,20 +217,21 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
         c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
       }
     }
-    A = (r + 1 == S) ? c : (crc_shift<5>(tab, A) ^ c);
+    A = (r + 1 == S) ? c : (crc_shift<5>(tab, crc_shift<5>(tab, A)) ^ c);
   }
-  // lane tree inside each row of 16 lanes: lane l+d covers bytes further from the end
-  u32 y;
-  y = dpp<kRowShl + 1>(A); if ((lane & 1u) == 0) A ^= crc_shift<0>(tab, y);
-  y = dpp<kRowShl + 2>(A); if ((lane & 3u) == 0) A ^= crc_shift<1>(tab, y);
-  y = dpp<kRowShl + 4>(A); if ((lane & 7u) == 0) A ^= crc_shift<2>(tab, y);
-  y = dpp<kRowShl + 8>(A); if ((lane & 15u) == 0) A ^= crc_shift<3>(tab, y);
-  // rows of 16 lanes = 1280 B: R0 ^ shift1280(R1 ^ shift1280(R2 ^ shift1280(R3)))
-  u32 t = readlane(A, 48);
-  t = readlane(A, 32) ^ crc_shift<4>(tab, t);
-  t = readlane(A, 16) ^ crc_shift<4>(tab, uni(t));
-  t = readlane(A, 0) ^ crc_shift<4>(tab, uni(t));
-  return uni(t);
+  // lane l: shift by 80 * l
+  A = (lane & 1u) ? crc_shift<0>(tab, A) : A;
+  A = (lane & 2u) ? crc_shift<1>(tab, A) : A;
+  A = (lane & 4u) ? crc_shift<2>(tab, A) : A;
+  A = (lane & 8u) ? crc_shift<3>(tab, A) : A;
+  A = (lane & 16u) ? crc_shift<4>(tab, A) : A;
+  A = (lane & 32u) ? crc_shift<5>(tab, A) : A;
+  // XOR over the wave
+  A ^= dpp<kRowShr + 1>(A);
+  A ^= dpp<kRowShr + 2>(A);
+  A ^= dpp<kRowShr + 4>(A);
+  A ^= dpp<kRowShr + 8>(A);
+  return readlane(A, 15) ^ readlane(A, 31) ^ readlane(A, 47) ^ readlane(A, 63);
 }
 
 // ------------------------------------------------------------------ entry tables
@@ -324,16 +345,10 @@ __device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
 // The chunk is then assembled from that entry and, if it crosses an entry end, the next one
 // (two funnel-shifted LDS reads and a byte select); chunks spanning 3+ entries (entries shorter
 // than 16 B) take a loop.
-// Source of the copy: the LDS window, or (GL) the same bytes re-read through the block's buffer
-// resource (L2/MALL-resident: the window was fetched from HBM one block earlier).
-template <bool GL>
+// Source of the copy: the staged LDS window.
 struct Src16 {
   const uint8_t* win;
-  __amdgpu_buffer_rsrc_t rs;
-  __device__ __forceinline__ uint4 operator()(int x) const {
-    if (GL) return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)x, 0, 0));
-    return lds_window16(win, x);
-  }
+  __device__ __forceinline__ uint4 operator()(int x) const { return lds_window16(win, x); }
 };
 
 template <class Col, class S>
@@ -350,11 +365,7 @@ __device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk
   for (u32 t0 = 0; t0 < npad; t0 += 64) {
     const u32 c = t0 + lane;
     u32 j = base;
-#ifdef TPZ_ABL_NOMAP
-    if (false) {
-#else
     if (t0 < nchunks) {
-#endif
       // entries base.. : the ones with tl < 64 end before some chunk start of this window
       const u32 k = base + lane;
       const u32 tl = k < nk ? min(((col.end(k) + 15) >> 4) - t0, 64u) : 64u;
@@ -388,11 +399,7 @@ __device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk
       col.get(more ? j + 1 : j, end1, d1);
       uint4 acc = src((int)x0 + d0);
       const bool cross = end0 < x0 + 16 && more;
-#ifdef TPZ_ABL_NOCROSS
-      if (false) {
-#else
       if (__ballot(cross)) {
-#endif
         const uint4 w = src((int)x0 + d1);
         acc = merge_at(acc, w, cross ? (int)(end0 - x0) : 16);
         // chunks spanning three or more entries
@@ -425,21 +432,23 @@ __device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk
 template <class Col, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
                                              const Col& vcol, u32 a0, u32 len, u32 b,
-                                             u64 ext_b, const Out& o, __amdgpu_buffer_rsrc_t rs,
-                                             bool gl) {
+                                             u64 ext_b, const Out& o) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
   return;
 #endif
+  // the header reads are issued together (one LDS round trip); the checks keep the reference's
+  // order
+  const u32 tag = win[(int)(a0 + len) - 1];                                    // compress.rs:99
+  const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));      // block.rs:51
+  const u32 n = lds_be16(win, a0);                                             // block.rs:54
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
-  const u32 tag = win[a0 + len - 1];                                           // compress.rs:99
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
   if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
   if (len - 1 < 4) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, 0); return; }     // block.rs:49
   const u32 P = len - 5;
   const int pb = (int)a0;
-  const u32 stored = bswap32(lds_u32(win, a0 + P));                            // block.rs:51
   u32 crc;
   if (P >= 4) {
     // fold init 0xFFFFFFFF into the first four payload bytes; zero the k bytes from the payload
@@ -469,7 +478,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   }
   if (crc != stored) { put_meta(o, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc); return; }
   if (P < 2) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }          // block.rs:54
-  const u32 n = lds_be16(win, a0);
 #ifdef TPZ_ABL_NOPARSE
   put_meta(o, b, TPZ_BLOCK_OK, n, crc);
   return;
@@ -521,18 +529,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   __builtin_amdgcn_wave_barrier();
   const u64 kb = key_base(ext_b, b);
 #ifndef TPZ_ABL_NOCOPY
-#ifdef TPZ_ABL_GCOPY
-  if (gl) {
-    const Src16<true> sg{win, rs};
-    copy_column(sg, kcol, knz, kc, o.keys + kb);
-    copy_column(sg, vcol, vnz, vc, o.vals + kb);
-  } else
-#endif
-  {
-    const Src16<false> sl{win, rs};
-    copy_column(sl, kcol, knz, kc, o.keys + kb);
-    copy_column(sl, vcol, vnz, vc, o.vals + kb);
-  }
+  copy_column(Src16{win}, kcol, knz, kc, o.keys + kb);
+  copy_column(Src16{win}, vcol, vnz, vc, o.vals + kb);
 #endif
   put_meta(o, b, TPZ_BLOCK_OK, n, crc);
 }
@@ -552,12 +550,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rsrc(const uint8_t* src
 }
 
 // A 16-byte piece that straddles the end of the source buffer comes back zeroed from the
-// range-checked buffer load; refill the in-range bytes one by one (only the batch's tail).
+// range-checked buffer load; refill its in-range bytes (only the batch's last blocks). Branch-free
+// per lane: clamped byte loads and selects.
 __device__ __forceinline__ void fix_tail(uint4& v, const uint8_t* src, u64 piece, u64 src_bytes) {
-  if (piece + 16 > src_bytes && piece < src_bytes) {
+  const bool straddle = piece + 16 > src_bytes && piece < src_bytes;
+  if (__ballot(straddle)) {
     u32 w[4] = {0, 0, 0, 0};
-    for (u32 k = 0; k < 16 && piece + k < src_bytes; k++) w[k >> 2] |= (u32)src[piece + k] << (8 * (k & 3));
-    v = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (u32 k = 0; k < 16; k++) {
+      const u64 a = piece + k;
+      const u32 byte = src[a < src_bytes ? a : src_bytes - 1];
+      w[k >> 2] |= (a < src_bytes ? byte : 0u) << (8 * (k & 3));
+    }
+    v.x = straddle ? w[0] : v.x;
+    v.y = straddle ? w[1] : v.y;
+    v.z = straddle ? w[2] : v.z;
+    v.w = straddle ? w[3] : v.w;
   }
 }
 
@@ -629,8 +637,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     if (fits) {
-      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out,
-                                    window_rsrc(p.src, p.src_bytes, s & ~15ull), e + 16 <= p.src_bytes);
+      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
@@ -671,8 +678,7 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out, rs,
-                               e + 16 <= p.src_bytes);
+    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out);
     __builtin_amdgcn_wave_barrier();
   }
 }

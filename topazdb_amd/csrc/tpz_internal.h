@@ -10,12 +10,13 @@ namespace tpz {
 
 // CRC-32 lookup tables uploaded once per context (see tpz_api.cpp: build_crc_tables):
 // ids 0..15 = T_0..T_15 (slice-by-16); ids 16+4j+i = T_{n_j-1-i}: the shift-by-n_j operator,
-// n_j = kCrcShiftBytes[j] (lane run 80 B, tree levels x2, row step 1280 B, super-round 5120 B);
+// n_j = kCrcShiftBytes[j] = 80 * 2^j (the lane-position shifts of the CRC combine; 2 x 2560 B
+// chains the 5120-B super-rounds of long blocks);
 // id 40 = kCrcInvTable: inv[t] = the byte b whose T_0[b] has top byte t (one zero byte un-shifted).
 constexpr int kNumCrcTables = 41;
 constexpr int kCrcInvTable = 40;
 constexpr int kCrcLaneBytes = 80;
-constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 5120};
+constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
 // Big path entry-table capacity per block: slots are only written when 6n <= len.
 constexpr uint32_t kBigMaxSlots = TPZ_MAX_BLOCK_BYTES / 6 + 16;
 
