@@ -50,22 +50,28 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
-// wave path slot: [guard 96][window 5120][pad 32][ktab n x u32][vtab n x u32]
-constexpr int kWinRounds = 5;                       // 5 x 1 KiB window
-constexpr int kWinBytes = kWinRounds * 1024;
+// wave path slot: [guard 96][window 4352][pad 32][ktab 256 x u32][vtab 256 x u32]
+//                 [kmap 288 x u8][vmap 288 x u8]
+// The window holds any block of a block_size <= 4 KiB builder (<= 4101 B; topazdb's default,
+// src/opt.rs:39); longer blocks take the big path.
+constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads, the 5th partial
+constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
-constexpr u32 kWaveMaxN = 256;
-constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveMaxN * 8;
-static_assert(kSlotBytes % 16 == 0, "slot alignment");
+constexpr u32 kWaveMaxN = 255;                      // map entries hold (compact index + 1) as u8
+constexpr int kWaveMapLen = 288;                    // >= kWinBytes / 16 + 1 chunk map slots
+constexpr int kSlotBytes = kGuard + kWinBytes + 32 + 256 * 8 + 2 * kWaveMapLen;
+static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 16 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard 96][window 92 KiB][pad];
+// big path (one wave per block): [guard 96][window 92 KiB][pad 32][kmap u16][vmap u16];
 // entry tables in global scratch
 constexpr int kBigWinBytes = 94208;
 constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32;
+constexpr int kBigMapLen = 5904;                    // >= kBigWinBytes / 16 + 1
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + 2 * kBigMapLen * 2;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
+static_assert((kBigMapLen * 2) % 16 == 0, "big map alignment");
 static_assert(kBigLds <= 163840, "big path LDS");
 
 // ------------------------------------------------------------------ small helpers
@@ -97,13 +103,13 @@ __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
-// 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: three
-// 8-byte-aligned ds_read_b64 (24 B), a one-bit dword select and v_alignbyte (9 VALU). A
-// ds_read_b128 off 16-byte alignment would be replayed at 64 LDS cycles (TPZ_ABL_UNALIGNED).
+// 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: one
+// ds_read_b128 at the byte address (gfx950 replays it: 64 LDS cycles, no VALU). Variants: three
+// 8-byte-aligned ds_read_b64 + a one-bit dword select + alignbyte (TPZ_ABL_F64, 9 VALU), two
+// aligned ds_read_b128 + a two-bit select (TPZ_ABL_FUNNEL, 16 VALU).
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
-#if defined(TPZ_ABL_UNALIGNED)
+#if !defined(TPZ_ABL_F64) && !defined(TPZ_ABL_FUNNEL)
   typedef u32x4 u32x4_u __attribute__((aligned(1)));
   const u32x4 v = *reinterpret_cast<const u32x4_u*>(base + x);
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -123,7 +129,8 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
   const u32 w4 = q < 2 ? (q == 0 ? b.x : b.y) : (q == 2 ? b.z : b.w);
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
                     __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
-#else
+#else  // TPZ_ABL_F64
+  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
   const u32x2* p = reinterpret_cast<const u32x2*>(base + (x & ~7));
   u32x2 a = p[0], b = p[1], c = p[2];
   asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
@@ -250,6 +257,15 @@ struct ColSmall {
     end = v >> 16;
     delta = (int)(short)(v & 0xFFFFu);
   }
+  // entries k and k + 1 in one ds_read2_b32 (k + 1 may be one past the last entry: the table has
+  // room for it and the caller ignores it)
+  __device__ __forceinline__ void get2(u32 k, u32& e0, int& d0, u32& e1, int& d1) const {
+    const u32 a = t[k], b = t[k + 1];
+    e0 = a >> 16;
+    d0 = (int)(short)(a & 0xFFFFu);
+    e1 = b >> 16;
+    d1 = (int)(short)(b & 0xFFFFu);
+  }
 };
 // Big path: one u64 per entry, {end, delta}, in this workgroup's global scratch. Written and
 // read back by the same wave: stores are drained (s_waitcnt vmcnt(0)) before the copy phase and
@@ -268,18 +284,32 @@ struct ColBig {
     end = (u32)v;
     delta = (int)(u32)(v >> 32);
   }
+  __device__ __forceinline__ void get2(u32 k, u32& e0, int& d0, u32& e1, int& d1) const {
+    get(k, e0, d0);
+    get(k + 1, e1, d1);
+  }
 };
 
-// Wave-inclusive prefix sum over 64 lanes: DPP row scans, then row carries via readlane.
+// Wave-inclusive prefix sum / max over 64 lanes: DPP row shifts, then row_bcast:15 / :31
+// (GFX9 DPP) carry each row's last lane into the following rows. Six DPP ops, no readlane.
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;
 __device__ __forceinline__ u32 wave_scan_incl(u32 x) {
-  const u32 lane = lane_id();
   x += dpp<kRowShr + 1>(x);
   x += dpp<kRowShr + 2>(x);
   x += dpp<kRowShr + 4>(x);
   x += dpp<kRowShr + 8>(x);
-  const u32 r0 = readlane(x, 15), r1 = readlane(x, 31), r2 = readlane(x, 47);
-  const u32 row = lane >> 4;
-  return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast15, 0xA, 0xF, false);
+  x += (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast31, 0xC, 0xF, false);
+  return x;
+}
+__device__ __forceinline__ u32 wave_scan_max(u32 x) {
+  x = max(x, dpp<kRowShr + 1>(x));
+  x = max(x, dpp<kRowShr + 2>(x));
+  x = max(x, dpp<kRowShr + 4>(x));
+  x = max(x, dpp<kRowShr + 8>(x));
+  x = max(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast15, 0xA, 0xF, false));
+  x = max(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast31, 0xC, 0xF, false));
+  return x;
 }
 
 __device__ __forceinline__ u32 lanes_below(u64 mask) {
@@ -314,18 +344,6 @@ __device__ __forceinline__ u32 byte_mask(int lo, int hi, int d) {
   return top & (~0u << (8 * a));
 }
 
-// 64-bit OR over the wave (DPP row scans, then the four row results via readlane).
-__device__ __forceinline__ u64 wave_or64(u64 m) {
-  u32 lo = (u32)m, hi = (u32)(m >> 32);
-  lo |= dpp<kRowShr + 1>(lo); hi |= dpp<kRowShr + 1>(hi);
-  lo |= dpp<kRowShr + 2>(lo); hi |= dpp<kRowShr + 2>(hi);
-  lo |= dpp<kRowShr + 4>(lo); hi |= dpp<kRowShr + 4>(hi);
-  lo |= dpp<kRowShr + 8>(lo); hi |= dpp<kRowShr + 8>(hi);
-  lo = readlane(lo, 15) | readlane(lo, 31) | readlane(lo, 47) | readlane(lo, 63);
-  hi = readlane(hi, 15) | readlane(hi, 31) | readlane(hi, 47) | readlane(hi, 63);
-  return ((u64)hi << 32) | lo;
-}
-
 // acc = bytes [0, m) of a, bytes [m, 16) of w (m in 0..16).
 __device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
   const u64 mlo = m >= 8 ? 0ull : (~0ull << (8 * m));          // bytes taken from w, low half
@@ -336,103 +354,118 @@ __device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
   return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
 }
 
-// Output-driven copy of one column (nk non-empty entries, tot bytes): the wave takes 64 output
-// chunks of 16 B at a time, lane l chunk c = t0 + l, so every store is a coalesced 1 KiB.
-// Chunk -> entry without a search: entry m of the window ends in lane tl_m's chunk range
-// (tl = ceil(end/16) - t0); when no two entries share a tl, OR-ing 1 << tl over the wave and a
-// popcount below each lane gives the number of entries that end before the lane's chunk, i.e.
-// the entry holding its first byte (a scalar walk over the window's entries otherwise).
-// The chunk is then assembled from that entry and, if it crosses an entry end, the next one
-// (two funnel-shifted LDS reads and a byte select); chunks spanning 3+ entries (entries shorter
-// than 16 B) take a loop.
+// One output column of a block: its entry table, its chunk map (LDS: map[t] = 1 + the compact
+// index of an entry whose end lies in (16(t-1), 16t], written by the parse), entry count,
+// byte count and destination slot.
+template <class Col, class MapT>
+struct ColOut {
+  Col col;
+  const MapT* map;
+  u32 nk, tot;
+  uint8_t* dst;
+  __device__ __forceinline__ u32 nchunks() const { return (tot + 15) >> 4; }
+  __device__ __forceinline__ u32 npad() const { return (nchunks() + 7) & ~7u; }  // whole 128-B lines
+};
+
 // Source of the copy: the staged LDS window.
 struct Src16 {
   const uint8_t* win;
   __device__ __forceinline__ uint4 operator()(int x) const { return lds_window16(win, x); }
 };
 
-template <class Col, class S>
-__device__ __forceinline__ void copy_column(const S& src, const Col& col, u32 nk, u32 tot,
-                                            uint8_t* dst) {
+// Output-driven copy of both columns: the wave takes 64 output chunks of 16 B per window (lane l
+// chunk c = t0 + l), so every store is a coalesced 1 KiB; key windows first, then value windows.
+//   1. chunk -> entry: the parse scattered (1 + compact index) of every entry into the chunk map
+//      at t = ceil(end / 16), the first chunk starting at or after the entry's end, so a wave
+//      prefix max of map[c] (carried across the column's windows) is the number of entries that
+//      end at or before the chunk start = the entry j holding its first byte. (Two entries ending
+//      in one chunk race for one map byte; a lane that got the smaller index walks forward.)
+//   2. entries j and j + 1 from the entry table.
+//   3. the chunk's bytes from LDS at x0 + delta_j; a chunk crossing entry j's end takes entry
+//      j+1's bytes after it (exec-masked second read + 64-bit mask select); chunks spanning 3+
+//      entries (entries shorter than 16 B) take a loop.
+//   4. store; pad chunks up to the 128-byte line are zeroed.
+template <class Col, class MapT, class S>
+__device__ __forceinline__ void copy_columns(const S& src, const ColOut<Col, MapT>& K,
+                                             const ColOut<Col, MapT>& V, u32 map_len) {
   const u32 lane = lane_id();
-  const u32 nchunks = (tot + 15) >> 4;
-  const u32 npad = (nchunks + 7) & ~7u;  // the slot is written in whole 128-byte lines
+  const u32 nwk = (K.npad() + 63) >> 6;
+  const u32 nw = nwk + ((V.npad() + 63) >> 6);
 #ifdef TPZ_ABL_MEMONLY
-  for (u32 c = lane; c < npad; c += 64) *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(c, 0, 0, 0);
+  for (u32 c = lane; c < K.npad(); c += 64) *reinterpret_cast<uint4*>(K.dst + c * 16) = make_uint4(c, 0, 0, 0);
+  for (u32 c = lane; c < V.npad(); c += 64) *reinterpret_cast<uint4*>(V.dst + c * 16) = make_uint4(c, 0, 0, 0);
   return;
 #endif
-  u32 base = 0;  // entries ending at or before the window's first chunk start
-  for (u32 t0 = 0; t0 < npad; t0 += 64) {
-    const u32 c = t0 + lane;
-    u32 j = base;
-    if (t0 < nchunks) {
-      // entries base.. : the ones with tl < 64 end before some chunk start of this window
-      const u32 k = base + lane;
-      const u32 tl = k < nk ? min(((col.end(k) + 15) >> 4) - t0, 64u) : 64u;
-      const u64 inw = __ballot(tl < 64);
-      const u32 cnt = __builtin_popcountll(inw);
-      const u64 bits = wave_or64(tl < 64 ? (1ull << tl) : 0ull);
-      if (__builtin_popcountll(bits) == cnt && cnt < 64) {
-        const u64 le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-        j = base + __builtin_popcountll(bits & le);
-        base += cnt;
-      } else {
-        // two entries end in one chunk, or >= 64 entries in the window: walk them
-        u32 m = base;
-        while (true) {
-          const u32 kk = m + lane;
-          const u32 t = kk < nk ? min(((col.end(kk) + 15) >> 4) - t0, 64u) : 64u;
-          const u32 n_here = __builtin_popcountll(__ballot(t < 64));
-          for (u32 q = 0; q < n_here; q++) j += readlane(t, q) <= lane ? 1u : 0u;
-          m += n_here;
-          if (n_here < 64) break;
-        }
-        base = m;
+  u32 carry = 0;
+  for (u32 w = 0; w < nw; w++) {
+    const bool isk = w < nwk;
+    if (w == nwk) carry = 0;                          // first value window
+    const Col col = isk ? K.col : V.col;
+    const MapT* map = isk ? K.map : V.map;
+    const u32 nk = isk ? K.nk : V.nk, nch = isk ? K.nchunks() : V.nchunks();
+    const u32 npad = isk ? K.npad() : V.npad();
+    uint8_t* dst = isk ? K.dst : V.dst;
+    const u32 last = nk ? nk - 1 : 0u;
+    const u32 c = 64 * (isk ? w : w - nwk) + lane;
+    const u32 x0 = 16 * c;
+    const bool act = c < nch;
+    // 1. chunk -> entry: prefix max of the map, carried across the column's windows
+    u32 j = map[min(c, map_len - 1)];
+    j = max(wave_scan_max(act ? j : 0u), carry);
+    carry = readlane(j, 63);
+    // 2. entries j and j + 1 (one ds_read2_b32)
+    u32 e0, e1;
+    int d0, d1;
+    col.get2(min(j, last), e0, d0, e1, d1);
+    // 3. the chunk's bytes; a chunk crossing entry j's end also reads entry j+1's bytes
+    //    (exec-masked). Reads are issued before the rare-case checks so they overlap.
+    uint4 acc = src(act ? (int)x0 + d0 : 0);
+    bool cross = act && j + 1 < nk && e0 < x0 + 16;
+    uint4 nx = make_uint4(0, 0, 0, 0);
+    if (cross) nx = src((int)x0 + d1);
+    if (__ballot(act && e0 <= x0)) {
+      // a lost map race (two entries ended in one chunk): walk forward to the holding entry
+      while (act && e0 <= x0) {
+        j++;
+        col.get2(min(j, last), e0, d0, e1, d1);
+      }
+      acc = src(act ? (int)x0 + d0 : 0);
+      cross = act && j + 1 < nk && e0 < x0 + 16;
+      if (cross) nx = src((int)x0 + d1);
+    }
+    if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
+    // chunks spanning three or more entries (entries shorter than 16 B)
+    if (__ballot(cross && e1 < x0 + 16 && j + 2 < nk)) {
+      u32 k = j + 1, end = e1;
+      while (cross && end < x0 + 16 && k + 1 < nk) {
+        const int lo = (int)(end - x0);
+        k++;
+        int delta;
+        col.get(k, end, delta);
+        const int hi = min((int)(end - x0), 16);
+        const uint4 v = src((int)x0 + delta);
+        acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
+        acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
+        acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
+        acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
       }
     }
-    if (c < nchunks) {
-      const u32 x0 = c * 16;
-      u32 end0, end1;
-      int d0, d1;
-      const bool more = j + 1 < nk;
-      col.get(j, end0, d0);
-      col.get(more ? j + 1 : j, end1, d1);
-      uint4 acc = src((int)x0 + d0);
-      const bool cross = end0 < x0 + 16 && more;
-      if (__ballot(cross)) {
-        const uint4 w = src((int)x0 + d1);
-        acc = merge_at(acc, w, cross ? (int)(end0 - x0) : 16);
-        // chunks spanning three or more entries
-        u32 k = j + 1, end = end1;
-        while (cross && end < x0 + 16 && k + 1 < nk) {
-          const int lo = (int)(end - x0);
-          k++;
-          int delta;
-          col.get(k, end, delta);
-          const int hi = min((int)(end - x0), 16);
-          const uint4 v = src((int)x0 + delta);
-          acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
-          acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
-          acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
-          acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
-        }
-      }
+    // 4. store (pad chunks up to the 128-byte line are zeroed)
+    const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
 #ifdef TPZ_ABL_NOSTORE
-      asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
 #else
-      *reinterpret_cast<uint4*>(dst + x0) = acc;
+    if (c < npad) *reinterpret_cast<uint4*>(dst + x0) = v;
 #endif
-    } else if (c < npad) {
-      *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(0, 0, 0, 0);
-    }
   }
 }
 
-// Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b.
-template <class Col, bool BIG>
+// Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. kmap / vmap are
+// the column chunk maps (kMapLen entries each, LDS, contiguous: vmap = kmap + kMapLen).
+template <class Col, class MapT, int kMapLen, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
-                                             const Col& vcol, u32 a0, u32 len, u32 b,
-                                             u64 ext_b, const Out& o) {
+                                             const Col& vcol, MapT* kmap, MapT* vmap, u32 a0,
+                                             u32 len, u32 b, u64 ext_b, const Out& o) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
@@ -449,12 +482,99 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   if (len - 1 < 4) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, 0); return; }     // block.rs:49
   const u32 P = len - 5;
   const int pb = (int)a0;
+  // The parse and the copy run BEFORE the CRC (its result only selects the status): the copy's
+  // HBM stores then drain while the CRC computes, instead of stalling the next block's
+  // s_waitcnt on the prefetch loads (loads and stores share vmcnt on gfx950). A block whose CRC
+  // turns out wrong reports CHECKSUM_MISMATCH with count 0; its slot holds unspecified bytes.
+  u32 st = TPZ_BLOCK_OK, cnt = n;
+  if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
+    st = TPZ_BLOCK_MALFORMED;
+    cnt = 0;
+  } else if (!BIG && n > kWaveMaxN) {
+    if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
+    return;
+  } else {
+#ifndef TPZ_ABL_NOPARSE
+    const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
+    const u32 dl = P - 2 - 2 * n;
+    const bool slots_fit = 6u * n <= len;
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
+    const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
+    {
+      // clear the chunk maps up to the largest chunk index this block can produce
+      constexpr u32 per = 16 / sizeof(MapT);
+      const u32 nz = min((u32)kMapLen, ((len >> 4) + 2 + per - 1) / per * per);
+      for (u32 i = lane; i < nz / per; i += 64) {
+        reinterpret_cast<uint4*>(kmap)[i] = make_uint4(0, 0, 0, 0);
+        reinterpret_cast<uint4*>(vmap)[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    u32 kc = 0, vc = 0, knz = 0, vnz = 0;
+    bool bad = false;
+    for (u32 g0 = 0; g0 < n; g0 += 64) {
+      const u32 i = g0 + lane;
+      const bool act = i < n;
+      u32 off = 0, kl = 0, vl = 0;
+      bool ok = true;
+      if (act) {
+        off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
+        ok = off + 2 <= dl;
+        if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }        // :77-81
+        if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
+        if (!ok) kl = vl = 0;
+      }
+      bad |= __ballot(act && !ok) != 0;
+      const u32 ki = wave_scan_incl(kl) + kc;
+      const u32 vi = wave_scan_incl(vl) + vc;
+      const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+      if (slots_fit && i < n_pad) ends_g[i] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
+      if (act && slots_fit) {
+        // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
+        // after the entry's end (entries whose end overflows the map only occur in OVERLAP blocks)
+        if (kl) {
+          const u32 m = knz + lanes_below(kmask);
+          kcol.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
+          if (((ki + 15) >> 4) < (u32)kMapLen) kmap[(ki + 15) >> 4] = (MapT)(m + 1);
+        }
+        if (vl) {
+          const u32 m = vnz + lanes_below(vmask);
+          vcol.put(m, vi, (int)(db + off + 4 + kl) - (int)(vi - vl));
+          if (((vi + 15) >> 4) < (u32)kMapLen) vmap[(vi + 15) >> 4] = (MapT)(m + 1);
+        }
+      }
+      knz += __builtin_popcountll(kmask);
+      vnz += __builtin_popcountll(vmask);
+      kc = readlane(ki, 63);
+      vc = readlane(vi, 63);
+    }
+
+    if (bad) {
+      st = TPZ_BLOCK_MALFORMED;
+      cnt = 0;
+    } else if (!slots_fit || kc > len || vc > len) {
+      st = TPZ_BLOCK_OVERLAP;
+    } else {
+      if (BIG) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      }
+      __builtin_amdgcn_wave_barrier();
+      const u64 kb = key_base(ext_b, b);
+#ifndef TPZ_ABL_NOCOPY
+      const ColOut<Col, MapT> K{kcol, kmap, knz, kc, o.keys + kb};
+      const ColOut<Col, MapT> V{vcol, vmap, vnz, vc, o.vals + kb};
+      copy_columns(Src16{win}, K, V, (u32)kMapLen);
+#endif
+    }
+#endif
+  }
+  __builtin_amdgcn_wave_barrier();
   u32 crc;
   if (P >= 4) {
     // fold init 0xFFFFFFFF into the first four payload bytes; zero the k bytes from the payload
     // end to the next 16-byte boundary (stored CRC and tag are already in registers). Then
     // R = R0(payload' || 0^k) = shift_k(R0(payload')), which equals shift_k(~stored) iff the CRC
-    // matches.
+    // matches. (The window is not used after this, so nothing is restored.)
     const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
     if (lane < k) win[a0 + P + lane] = 0;
@@ -465,9 +585,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     const u32 R = wave_crc(tab, win, pb, P + k);
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
 #endif
-    __builtin_amdgcn_wave_barrier();
-    if (lane < 4) win[a0 + lane] ^= 0xFFu;
-    __builtin_amdgcn_wave_barrier();
   } else {
     u32 c = 0xFFFFFFFFu;
     for (u32 i = 0; i < P; i++) {
@@ -476,63 +593,11 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     }
     crc = ~c;
   }
-  if (crc != stored) { put_meta(o, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc); return; }
-  if (P < 2) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }          // block.rs:54
-#ifdef TPZ_ABL_NOPARSE
-  put_meta(o, b, TPZ_BLOCK_OK, n, crc);
-  return;
-#endif
-  if (P < 2 + 2 * n) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }  // :56-59
-  if (!BIG && n > kWaveMaxN) {
-    if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
-    return;
+  if (crc != stored) {                                                         // checksum.rs:17
+    st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+    cnt = 0;
   }
-  const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
-  const u32 dl = P - 2 - 2 * n;
-  const bool slots_fit = 6u * n <= len;
-  uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
-  const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
-  u32 kc = 0, vc = 0, knz = 0, vnz = 0;
-  bool bad = false;
-  for (u32 g0 = 0; g0 < n; g0 += 64) {
-    const u32 i = g0 + lane;
-    const bool act = i < n;
-    u32 off = 0, kl = 0, vl = 0;
-    bool ok = true;
-    if (act) {
-      off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
-      ok = off + 2 <= dl;
-      if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }        // :77-81
-      if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
-      if (!ok) kl = vl = 0;
-    }
-    bad |= __ballot(act && !ok) != 0;
-    const u32 ki = wave_scan_incl(kl) + kc;
-    const u32 vi = wave_scan_incl(vl) + vc;
-    const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
-    if (slots_fit && i < n_pad) ends_g[i] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
-    if (act && slots_fit) {
-      if (kl) kcol.put(knz + lanes_below(kmask), ki, (int)(db + off + 2) - (int)(ki - kl));
-      if (vl) vcol.put(vnz + lanes_below(vmask), vi, (int)(db + off + 4 + kl) - (int)(vi - vl));
-    }
-    knz += __builtin_popcountll(kmask);
-    vnz += __builtin_popcountll(vmask);
-    kc = readlane(ki, 63);
-    vc = readlane(vi, 63);
-  }
-  if (bad) { put_meta(o, b, TPZ_BLOCK_MALFORMED, 0, crc); return; }
-  if (!slots_fit || kc > len || vc > len) { put_meta(o, b, TPZ_BLOCK_OVERLAP, n, crc); return; }
-  if (BIG) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  }
-  __builtin_amdgcn_wave_barrier();
-  const u64 kb = key_base(ext_b, b);
-#ifndef TPZ_ABL_NOCOPY
-  copy_column(Src16{win}, kcol, knz, kc, o.keys + kb);
-  copy_column(Src16{win}, vcol, vnz, vc, o.vals + kb);
-#endif
-  put_meta(o, b, TPZ_BLOCK_OK, n, crc);
+  put_meta(o, b, st, cnt, crc);
 }
 
 __device__ __forceinline__ void load_tables(u32* tab, const u32* gtab) {
@@ -591,7 +656,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
   const ColSmall kcol{reinterpret_cast<u32*>(etab)};
-  const ColSmall vcol{reinterpret_cast<u32*>(etab + kWaveMaxN * 4)};
+  const ColSmall vcol{reinterpret_cast<u32*>(etab + 256 * 4)};
+  uint8_t* kmap = etab + 256 * 8;
+  uint8_t* vmap = kmap + kWaveMapLen;
 
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   const u32 nw = gridDim.x * kWavesPerWG;
@@ -630,14 +697,16 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       v[0] = zero_head(v[0], lane == 0 ? (u32)(s & 15u) : 0u);  // the previous block's tail
 #pragma unroll
       for (int r = 0; r < kWinRounds; r++)
-        if ((u32)r < rounds) *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
+        if ((u32)r < rounds && r * 1024 + lane * 16 < (u32)kWinBytes)
+          *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
     }
     const u32 bcur = b;
     b += nw;
     issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     if (fits) {
-      decode_block<ColSmall, false>(tab, win, kcol, vcol, (u32)(s & 15u), len64, bcur, s, p.out);
+      decode_block<ColSmall, uint8_t, kWaveMapLen, false>(tab, win, kcol, vcol, kmap, vmap,
+                                                          (u32)(s & 15u), len64, bcur, s, p.out);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
@@ -657,6 +726,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[lane] = make_uint4(0, 0, 0, 0);
   const ColBig kcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
   const ColBig vcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
+  uint16_t* kmap = reinterpret_cast<uint16_t*>(win + kBigWinBytes + 32);
+  uint16_t* vmap = kmap + kBigMapLen;
   const u32 cnt = uni(*p.out.defer_count);
   for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
     const u32 b = uni(p.out.defer_list[it]);
@@ -678,7 +749,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, true>(tab, win, kcol, vcol, (u32)(s & 15u), len, b, s, p.out);
+    decode_block<ColBig, uint16_t, kBigMapLen, true>(tab, win, kcol, vcol, kmap, vmap,
+                                                     (u32)(s & 15u), len, b, s, p.out);
     __builtin_amdgcn_wave_barrier();
   }
 }
