@@ -73,18 +73,18 @@ def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev)
     np.cumsum(n_ent, out=e0[1:])
     bid = np.arange(nb, dtype=np.int64)
     ext64 = ext[:-1].astype(np.int64)
-    kb = _lib.key_base(ext64, bid)
+    kb = _lib.slot_base(ext64, bid)
     sb = _lib.entry_base(ext64, bid)
     ends = cols.ends.view(-1, 2)
     kpos = kpos.astype(np.int64)
     vpos = vpos.astype(np.int64)
+    vb = kb + _lib.value_start(kpos[e0[1:]] - kpos[e0[:-1]])  # values start after the keys
     step = 65536
     dkeys = torch.from_numpy(keys[:int(kpos[e0[-1]])]).to(dev)
     dvals = torch.from_numpy(vals[:int(vpos[e0[-1]])]).to(dev)
     for lo in range(0, nb, step):
         hi = min(nb, lo + step)
-        for col, pos, dexp, dend in ((cols.keys, kpos, dkeys, ends[:, 0]),
-                                     (cols.vals, vpos, dvals, ends[:, 1])):
+        for base, pos, dexp, dend in ((kb, kpos, dkeys, ends[:, 0]), (vb, vpos, dvals, ends[:, 1])):
             tot = pos[e0[lo + 1:hi + 1]] - pos[e0[lo:hi]]          # bytes per block
             start_exp = pos[e0[lo:hi]]
             n = int(tot.sum())
@@ -92,7 +92,7 @@ def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev)
                 t_tot = torch.from_numpy(tot).to(dev)
                 rel = torch.arange(n, device=dev) - torch.repeat_interleave(
                     torch.cumsum(t_tot, 0) - t_tot, t_tot)
-                got = col[torch.repeat_interleave(torch.from_numpy(kb[lo:hi]).to(dev), t_tot) + rel]
+                got = cols.data[torch.repeat_interleave(torch.from_numpy(base[lo:hi]).to(dev), t_tot) + rel]
                 exp = dexp[torch.repeat_interleave(torch.from_numpy(start_exp).to(dev), t_tot) + rel]
                 assert torch.equal(got, exp), "column bytes differ"
             ne = n_ent[lo:hi]
@@ -193,7 +193,7 @@ def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
         d_ext = torch.empty(cb + 1, dtype=torch.int64, device=dev)
         cols = SlottedColumns(cb, cap, dev.index)
         h_cols = {k: torch.empty(getattr(cols, k).numel(), dtype=getattr(cols, k).dtype).pin_memory()
-                  for k in ("keys", "vals", "ends", "count", "status", "crc")}
+                  for k in _lib.COLUMN_FIELDS}
         bufs.append((d_src, d_ext, cols, h_cols))
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -208,14 +208,45 @@ def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
             d_ext[:hi - lo + 1].copy_(e, non_blocking=True)
             ctx.decode_ptrs(d_src.data_ptr(), d_ext.data_ptr(), hi - lo, end - base,
                             cols.ptrs(), s.cuda_stream)
-            kc = _lib.col_capacity(end - base, hi - lo)
+            dc = _lib.data_capacity(end - base, hi - lo)
             sc = 2 * _lib.entry_capacity(end - base, hi - lo)
-            for k, n in (("keys", kc), ("vals", kc), ("ends", sc),
-                         ("count", hi - lo), ("status", hi - lo), ("crc", hi - lo)):
+            for k, n in (("data", dc), ("ends", sc), ("count", hi - lo), ("status", hi - lo),
+                         ("crc", hi - lo)):
                 h_cols[k][:n].copy_(getattr(cols, k)[:n], non_blocking=True)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return float(ext[-1] - ext[0]) / dt / GIB
+
+
+def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10) -> dict:
+    """FileObject::open's whole-file CRC (tpz_crc32_ranges, src/table/file_object.rs:57-78) over
+    the resident shard cut into 64 MiB "files" (TABLE_CAPACITY, src/table/builder.rs:27).
+    Algorithmic bytes = the file bytes, read once. Not the metric; DESIGN.md §4."""
+    n = batch.src_bytes
+    fsz = 64 << 20
+    ext = list(range(0, n, fsz)) + [n]
+    d_ext = torch.tensor(ext, dtype=torch.int64, device=dev)
+    crc = torch.empty(len(ext) - 1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run():
+        ctx.crc32_ptrs(batch.src.data_ptr(), d_ext.data_ptr(), len(ext) - 1, n, crc.data_ptr(),
+                       stream.cuda_stream)
+    run()
+    torch.cuda.synchronize(dev)
+    got = crc.cpu().numpy().view(np.uint32)
+    for i in (0, len(ext) - 2):  # spot check against zlib (the CRC oracle)
+        assert got[i] == zlib.crc32(src[ext[i]:ext[i + 1]].tobytes()), "file CRC mismatch"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    gbs = n / (ms * 1e-3) / 1e9
+    return {"files": len(ext) - 1, "bytes": n, "ms": round(ms, 4), "gb_s": round(gbs, 1),
+            "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 DEFAULT_BLOCKS = {"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}
@@ -266,6 +297,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-file-crc", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -325,6 +357,13 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"e2e measurement failed: {ex}")
 
+    fcrc = None
+    if rank == 0 and not args.no_file_crc:
+        try:
+            fcrc = file_crc_rate(ctx, batch, src, dev)
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"file CRC measurement failed: {ex}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
@@ -363,6 +402,7 @@ def main():
                          "kernel_ms": round(ev_ms_max, 4)},
             "cpu_baseline": cpu,
             "e2e_h2d_d2h_gib_s": e2e,
+            "file_crc": fcrc,
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -10,6 +10,9 @@
  *                           tag dispatch (src/block/compress.rs:95-113) -> checksum::
  *                           verify_checksum (src/checksum.rs:12-21) -> every
  *                           BlockIterator::seek_to materialised (src/block/iterator.rs:63-83)
+ *   tpz_crc32_ranges        checksum::calculate_checksum (src/checksum.rs:6-10) over many ranges
+ *   tpz_verify_files        FileObject::open's whole-file CRC (src/table/file_object.rs:57-78),
+ *                           batched over SST file images (SsTable::open, src/table.rs:91-112)
  *   tpz_format_block_error  the reference's error strings (checksum.rs:18-21, compress.rs:97,102)
  *
  * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
@@ -51,7 +54,8 @@ typedef enum {
                                       range (iterator.rs:74-82)                              */
   TPZ_BLOCK_OVERLAP = 6,           /* CRC-valid and decodable by the reference, but entries
                                       overlap so the decoded bytes exceed the block's slot:
-                                      6*n > len or key bytes > len or value bytes > len.
+                                      6*n > len or value_start(K) + V > len + 2 (K, V = the
+                                      block's key and value bytes).
                                       topazdb's BlockBuilder never writes such a block.      */
   TPZ_BLOCK_TOO_LARGE = 7          /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
                                       block_size <= 64 KiB BlockBuilder emits)               */
@@ -75,44 +79,52 @@ typedef struct {
  * decode independently (and shard across GPUs) with no cross-block communication. Every slot
  * starts on a 128-byte line and is written in whole lines (HBM3E then never sees a partial-line
  * write from two different workgroups).
- *   keys / vals : block i's key bytes are packed at keys[tpz_key_base(ext[i], i) ...
- *                 + key_bytes), its value bytes at vals[tpz_key_base(ext[i], i) ...]
- *   ends        : entry j of block i (j < count[i]) has its inclusive end offsets, relative to
- *                 the block's base, at ends[2*(e+j)] (key) and ends[2*(e+j)+1] (value),
- *                 e = tpz_entry_base(ext[i], i):
- *                 key_j   = keys[kb + (j ? ends[2(e+j-1)]   : 0) .. kb + ends[2(e+j)]]
- *                 value_j = vals[kb + (j ? ends[2(e+j-1)+1] : 0) .. kb + ends[2(e+j)+1]]
- *   count[i]    : entries in block i (n) for OK and OVERLAP, else 0
- *   status[i]   : tpz_block_status
- *   crc[i]      : CRC-32 the device computed over the payload (valid for OK, MALFORMED,
- *                 OVERLAP, CHECKSUM_MISMATCH; the stored one is the payload's trailing u32)
- * Bytes of a slot beyond the block's own data are unspecified. */
+ *   data  : block i's slot starts at s = tpz_slot_base(ext[i], i). It holds the block's key
+ *           bytes (every entry's key, in entry order) at data[s .. s + K), K = the block's key
+ *           bytes, then its value bytes from data[s + tpz_value_start(K)] on (K rounded up to
+ *           16; the bytes in between are unspecified). One stream per block: the copy writes it
+ *           with whole-wave stores, and a consumer moves one contiguous range per block.
+ *   ends  : entry j of block i (j < count[i]) has its exclusive end offsets at ends[2*(e+j)]
+ *           (key, relative to s) and ends[2*(e+j)+1] (value, relative to s + vs),
+ *           e = tpz_entry_base(ext[i], i), K = ends[2*(e+count[i]-1)] (0 when count is 0),
+ *           vs = tpz_value_start(K):
+ *             key_j   = data[s +      (j ? ends[2(e+j-1)]   : 0) .. s +      ends[2(e+j)]]
+ *             value_j = data[s + vs + (j ? ends[2(e+j-1)+1] : 0) .. s + vs + ends[2(e+j)+1]]
+ *   count[i]  : entries in block i (n) for OK and OVERLAP, else 0
+ *   status[i] : tpz_block_status
+ *   crc[i]    : CRC-32 the device computed over the payload (valid for OK, MALFORMED,
+ *               OVERLAP, CHECKSUM_MISMATCH; the stored one is the payload's trailing u32)
+ * Bytes of a slot beyond the block's own data are unspecified. A slot spans at most
+ * len + 129 bytes (len = the block's encoded length), which never reaches the next slot. */
 typedef struct {
-  uint8_t* d_keys;   /* capacity tpz_col_capacity(src_bytes, n_blocks) bytes        */
-  uint8_t* d_vals;   /* same capacity                                               */
-  uint32_t* d_ends;  /* capacity 2 * tpz_entry_capacity(src_bytes, n_blocks) u32     */
+  uint8_t* d_data;   /* capacity tpz_data_capacity(src_bytes, n_blocks) bytes        */
+  uint32_t* d_ends;  /* capacity 2 * tpz_entry_capacity(src_bytes, n_blocks) u32      */
   uint32_t* d_count; /* n_blocks */
   uint8_t* d_status; /* n_blocks */
   uint32_t* d_crc;   /* n_blocks */
 } tpz_columns;
 
-static inline uint64_t tpz_key_base(uint64_t ext_i, uint64_t i) {
+static inline uint64_t tpz_slot_base(uint64_t ext_i, uint64_t i) {
   return ((ext_i + 127u) & ~(uint64_t)127u) + 256u * i;
+}
+static inline uint64_t tpz_value_start(uint64_t key_bytes) {
+  return (key_bytes + 15u) & ~(uint64_t)15u;
 }
 static inline uint64_t tpz_entry_base(uint64_t ext_i, uint64_t i) {
   return 16u * (ext_i / 96u + i);
 }
-static inline uint64_t tpz_col_capacity(uint64_t src_bytes, uint64_t n_blocks) {
-  return tpz_key_base(src_bytes, n_blocks) + 128u;
+static inline uint64_t tpz_data_capacity(uint64_t src_bytes, uint64_t n_blocks) {
+  return tpz_slot_base(src_bytes, n_blocks) + 128u;
 }
 static inline uint64_t tpz_entry_capacity(uint64_t src_bytes, uint64_t n_blocks) {
   return tpz_entry_base(src_bytes, n_blocks) + 16u;
 }
 
 /* Exported copies of the layout helpers for FFI callers that cannot use static inline. */
-uint64_t tpz_layout_key_base(uint64_t ext_i, uint64_t i);
+uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i);
+uint64_t tpz_layout_value_start(uint64_t key_bytes);
 uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i);
-uint64_t tpz_layout_col_capacity(uint64_t src_bytes, uint64_t n_blocks);
+uint64_t tpz_layout_data_capacity(uint64_t src_bytes, uint64_t n_blocks);
 uint64_t tpz_layout_entry_capacity(uint64_t src_bytes, uint64_t n_blocks);
 
 /* ---- context ------------------------------------------------------------------------------ */
@@ -134,6 +146,23 @@ tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
  * block: that is data, not an API failure). */
 tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* out,
                           void* stream);
+
+/* ---- whole-range CRC-32 ------------------------------------------------------------------
+ * Ranges use the batch type: range i is d_src[d_ext[i] .. d_ext[i+1]) (d_ext non-decreasing,
+ * n_blocks = number of ranges, src_bytes = d_ext[n]). Each range may be up to 2^35 bytes.
+ *
+ * checksum::calculate_checksum (src/checksum.rs:6-10) of every range: d_crc[i] = CRC-32/ISO-HDLC
+ * of range i. Asynchronous on `stream`. */
+tpz_err tpz_crc32_ranges(tpz_ctx* ctx, const tpz_batch* ranges, uint32_t* d_crc, void* stream);
+
+/* FileObject::open's whole-file check (src/table/file_object.rs:57-78) for SST file images in
+ * HBM: range i is a whole file; its CRC-32 over all but the last 4 bytes goes to d_crc[i] and
+ * is compared with the big-endian u32 in those 4 bytes. d_status[i] = TPZ_BLOCK_OK,
+ * TPZ_BLOCK_CHECKSUM_MISMATCH ("checksum: expected E, actual A", checksum.rs:18-21, with
+ * A = d_crc[i]) or TPZ_BLOCK_MALFORMED (file shorter than 4 bytes: the reference's
+ * `buf[size - CHECKSUM_SIZE..]` panics). Asynchronous on `stream`. */
+tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
+                         uint8_t* d_status, void* stream);
 
 /* ---- host write side (inputs for benches and the table facade) ---------------------------
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule

@@ -165,7 +165,8 @@ static int entry_at(const blockview* v, uint32_t i, const uint8_t** k, uint32_t*
 
 /* Decode a block and validate every entry the way an iteration over all indices would.
  * Sets TPZO_MALFORMED on any panicking entry, TPZO_OVERLAP when the decoded bytes cannot fit
- * the device slot contract (include/tpz_gpu.h: 6*n, key bytes and value bytes each <= len). */
+ * the device slot contract (include/tpz_gpu.h: 6*n <= len and value_start(K) + V <= len + 2,
+ * K/V = key/value bytes, value_start = K rounded up to 16). */
 static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt, uint64_t* vt) {
   block_decode(b, len, v);
   *kt = *vt = 0;
@@ -177,7 +178,7 @@ static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt,
     *kt += kl;
     *vt += vl;
   }
-  if (6ull * v->n > len || *kt > len || *vt > len) v->status = TPZO_OVERLAP;
+  if (6ull * v->n > len || ((*kt + 15) & ~15ull) + *vt > len + 2) v->status = TPZO_OVERLAP;
 }
 
 void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,

@@ -39,7 +39,7 @@ def main():
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
     means = {}
     disp = 0
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         m, n = pmc_means(os.path.join(src, sub), "decode_wave_kernel")
         means.update(m)
         disp = max(disp, n)

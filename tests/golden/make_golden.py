@@ -223,10 +223,10 @@ def decode_block(blk: bytes) -> dict:
         r["entries"] = ents
         ktot = sum(len(k) for k, _ in ents)
         vtot = sum(len(v) for _, v in ents)
-        # Device slot contract (include/tpz_gpu.h): decoded bytes of one block must fit the
-        # block's own extent. Only blocks whose offsets overlap can break it; topazdb's writer
+        # Device slot contract (include/tpz_gpu.h): the block's decoded stream (keys, values
+        # from the next 16-byte boundary) must fit its slot (len + 2 bytes). Only blocks whose offsets overlap can break it; topazdb's writer
         # never emits them, the reference iterator decodes them, the device reports OVERLAP.
-        if n * 6 > len(blk) or ktot > len(blk) or vtot > len(blk):
+        if n * 6 > len(blk) or (ktot + 15) // 16 * 16 + vtot > len(blk) + 2:
             r["status"] = ST_OVERLAP
     return r
 

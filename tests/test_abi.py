@@ -31,16 +31,17 @@ def test_layout_helpers_match_python():
     rng = np.random.default_rng(1)
     for _ in range(200):
         e, i = int(rng.integers(0, 1 << 40)), int(rng.integers(0, 1 << 24))
-        assert L.tpz_layout_key_base(e, i) == _lib.key_base(e, i)
+        assert L.tpz_layout_slot_base(e, i) == _lib.slot_base(e, i)
         assert L.tpz_layout_entry_base(e, i) == _lib.entry_base(e, i)
-        assert L.tpz_layout_col_capacity(e, i) == _lib.col_capacity(e, i)
+        assert L.tpz_layout_data_capacity(e, i) == _lib.data_capacity(e, i)
         assert L.tpz_layout_entry_capacity(e, i) == _lib.entry_capacity(e, i)
+        assert L.tpz_layout_value_start(e) == _lib.value_start(e) == (e + 15) // 16 * 16
 
 
 def test_slots_never_overlap():
-    """Worst case a block may emit under the slot contract: key/value bytes up to len written
-    in whole 128-byte lines, and floor(len/6) entries written in whole lines of 16 {kend, vend}
-    pairs; consecutive slots must stay disjoint and line aligned."""
+    """Worst case a block may emit under the slot contract: a stream of value_start(K) + V <=
+    len + 2 bytes written in whole 128-byte lines, and floor(len/6) entries written in whole
+    lines of 16 {kend, vend} pairs; consecutive slots must stay disjoint and line aligned."""
     rng = np.random.default_rng(2)
     lens = np.concatenate([rng.integers(0, 70000, 3000), rng.integers(0, 40, 3000),
                            np.full(100, 4155), np.arange(0, 200)])
@@ -50,12 +51,15 @@ def test_slots_never_overlap():
     n = len(lens)
     for i in range(n):
         ln = int(lens[i])
-        kb, kb1 = _lib.key_base(int(ext[i]), i), _lib.key_base(int(ext[i + 1]), i + 1)
+        kb, kb1 = _lib.slot_base(int(ext[i]), i), _lib.slot_base(int(ext[i + 1]), i + 1)
         assert kb % 128 == 0
-        assert kb + ((ln + 127) & ~127) <= kb1
+        assert kb + ((ln + 2 + 127) & ~127) <= kb1
         sb, sb1 = _lib.entry_base(int(ext[i]), i), _lib.entry_base(int(ext[i + 1]), i + 1)
         assert sb % 16 == 0 and sb + ((ln // 6 + 15) & ~15) <= sb1
-    assert _lib.key_base(int(ext[-1]), n) <= _lib.col_capacity(int(ext[-1]), n)
+    assert _lib.slot_base(int(ext[-1]), n) <= _lib.data_capacity(int(ext[-1]), n)
+    last = int(lens[-1])
+    assert (_lib.slot_base(int(ext[-2]), n - 1) + ((last + 2 + 127) & ~127)
+            <= _lib.data_capacity(int(ext[-1]), n))
     assert _lib.entry_base(int(ext[-1]), n) <= _lib.entry_capacity(int(ext[-1]), n)
 
 

@@ -33,8 +33,10 @@ class Batch(C.Structure):
 
 
 class Columns(C.Structure):
-    _fields_ = [("d_keys", C.c_void_p), ("d_vals", C.c_void_p), ("d_ends", C.c_void_p),
-                ("d_count", C.c_void_p), ("d_status", C.c_void_p), ("d_crc", C.c_void_p)]
+    _fields_ = [("d_data", C.c_void_p), ("d_ends", C.c_void_p), ("d_count", C.c_void_p),
+                ("d_status", C.c_void_p), ("d_crc", C.c_void_p)]
+
+COLUMN_FIELDS = ("data", "ends", "count", "status", "crc")
 
 
 _lib = None
@@ -64,13 +66,21 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
                                         C.c_void_p]
         L.tpz_decode_blocks.restype = C.c_int
+        for f in ("tpz_crc32_ranges",):
+            getattr(L, f).argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
+            getattr(L, f).restype = C.c_int
+        L.tpz_verify_files.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
+                                       C.c_void_p]
+        L.tpz_verify_files.restype = C.c_int
         L.tpz_format_block_error.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_char_p,
                                              C.c_size_t]
         L.tpz_last_error.restype = C.c_char_p
-        for f in ("key_base", "entry_base", "col_capacity", "entry_capacity"):
+        for f in ("slot_base", "entry_base", "data_capacity", "entry_capacity"):
             fn = getattr(L, "tpz_layout_" + f)
             fn.argtypes = [C.c_uint64, C.c_uint64]
             fn.restype = C.c_uint64
+        L.tpz_layout_value_start.argtypes = [C.c_uint64]
+        L.tpz_layout_value_start.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -87,16 +97,20 @@ def format_block_error(status: int, crc_expected: int = 0, crc_actual: int = 0) 
 
 
 # layout (mirrors the static inline helpers of include/tpz_gpu.h; works on ints and numpy int64)
-def key_base(ext_i, i):
+def slot_base(ext_i, i):
     return ((ext_i + 127) & ~127) + 256 * i
+
+
+def value_start(key_bytes):
+    return (key_bytes + 15) & ~15
 
 
 def entry_base(ext_i, i):
     return 16 * (ext_i // 96 + i)
 
 
-def col_capacity(src_bytes: int, n_blocks: int) -> int:
-    return key_base(src_bytes, n_blocks) + 128
+def data_capacity(src_bytes: int, n_blocks: int) -> int:
+    return slot_base(src_bytes, n_blocks) + 128
 
 
 def entry_capacity(src_bytes: int, n_blocks: int) -> int:
@@ -131,7 +145,21 @@ class Context:
                     stream: int = 0) -> None:
         """tpz_decode_blocks on raw device pointers; cols maps field name -> device pointer."""
         b = Batch(d_src, d_ext, n_blocks, src_bytes)
-        c = Columns(cols["keys"], cols["vals"], cols["ends"], cols["count"], cols["status"],
-                    cols["crc"])
+        c = Columns(*[cols[f] for f in COLUMN_FIELDS])
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")
+
+    def crc32_ptrs(self, d_src: int, d_ext: int, n_ranges: int, src_bytes: int, d_crc: int,
+                   stream: int = 0) -> None:
+        """tpz_crc32_ranges: CRC-32 of every range [ext[i], ext[i+1]) (checksum.rs:6-10)."""
+        b = Batch(d_src, d_ext, n_ranges, src_bytes)
+        check(lib().tpz_crc32_ranges(self.handle, C.byref(b), C.c_void_p(d_crc),
+                                     C.c_void_p(stream)), "tpz_crc32_ranges")
+
+    def verify_files_ptrs(self, d_src: int, d_ext: int, n_files: int, src_bytes: int,
+                          d_crc: int, d_status: int, stream: int = 0) -> None:
+        """tpz_verify_files: FileObject::open's whole-file CRC check (file_object.rs:57-78)."""
+        b = Batch(d_src, d_ext, n_files, src_bytes)
+        check(lib().tpz_verify_files(self.handle, C.byref(b), C.c_void_p(d_crc),
+                                     C.c_void_p(d_status), C.c_void_p(stream)),
+              "tpz_verify_files")

@@ -52,11 +52,10 @@ class SlottedColumns:
 
     def __init__(self, n_blocks: int, src_bytes: int, device: int = 0):
         dev = _dev(device)
-        cap = _lib.col_capacity(src_bytes, n_blocks)
+        cap = _lib.data_capacity(src_bytes, n_blocks)
         ecap = _lib.entry_capacity(src_bytes, n_blocks)
         nb = max(n_blocks, 1)
-        self.keys = torch.empty(cap, dtype=torch.uint8, device=dev)
-        self.vals = torch.empty(cap, dtype=torch.uint8, device=dev)
+        self.data = torch.empty(cap, dtype=torch.uint8, device=dev)   # keys | gap | values
         self.ends = torch.empty(2 * ecap, dtype=torch.int32, device=dev)  # {kend, vend} pairs
         self.count = torch.empty(nb, dtype=torch.int32, device=dev)
         self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -64,8 +63,7 @@ class SlottedColumns:
         self.n_blocks = n_blocks
 
     def ptrs(self) -> dict:
-        return {k: getattr(self, k).data_ptr() for k in
-                ("keys", "vals", "ends", "count", "status", "crc")}
+        return {k: getattr(self, k).data_ptr() for k in _lib.COLUMN_FIELDS}
 
     def meta_host(self):
         nb = self.n_blocks
@@ -85,20 +83,22 @@ class SlottedColumns:
         eblk = np.repeat(bid, n_ok)
         j = np.arange(total, dtype=np.int64) - ebase[eblk]
         sb = _lib.entry_base(ext, bid)
-        kb = _lib.key_base(ext, bid)
+        base = _lib.slot_base(ext, bid)
         slot = sb[eblk] + j
         ends = self.ends.cpu().numpy().view(np.uint32)
         kend_d, vend_d = ends[0::2], ends[1::2]
+        # the block's key bytes = kend of its last entry; its values start 16-aligned after them
+        ktot = np.where(n_ok > 0, kend_d[sb + np.maximum(n_ok - 1, 0)].astype(np.int64), 0)
+        vbase = base + _lib.value_start(ktot)
         ke = kend_d[slot].astype(np.int64)
         ve = vend_d[slot].astype(np.int64)
         first = j == 0
         ks = np.where(first, 0, kend_d[np.maximum(slot - 1, 0)].astype(np.int64))
         vs = np.where(first, 0, vend_d[np.maximum(slot - 1, 0)].astype(np.int64))
         klen, vlen = ke - ks, ve - vs
-        keys_d = self.keys.cpu().numpy()
-        vals_d = self.vals.cpu().numpy()
-        keys = _gather(keys_d, kb[eblk] + ks, klen)
-        vals = _gather(vals_d, kb[eblk] + vs, vlen)
+        data = self.data.cpu().numpy()
+        keys = _gather(data, base[eblk] + ks, klen)
+        vals = _gather(data, vbase[eblk] + vs, vlen)
         return DenseDecode(status, crc, np.where(status == BLOCK_OK, count, 0).astype(np.uint32),
                            count, klen.astype(np.uint32), vlen.astype(np.uint32), keys, vals)
 
@@ -142,3 +142,26 @@ def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None =
     ctx.decode_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes,
                     cols.ptrs(), s.cuda_stream)
     return cols
+
+
+def crc32_ranges(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None
+                 ) -> torch.Tensor:
+    """checksum::calculate_checksum (src/checksum.rs:6-10) of every range of `batch` on the GPU
+    (tpz_crc32_ranges); returns the device u32 CRCs (as int32)."""
+    crc = torch.empty(max(batch.n_blocks, 1), dtype=torch.int32, device=_dev(ctx.device))
+    s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
+    ctx.crc32_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes,
+                   crc.data_ptr(), s.cuda_stream)
+    return crc
+
+
+def verify_files(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None):
+    """FileObject::open's whole-file check (src/table/file_object.rs:57-78) for every file image
+    of `batch` (tpz_verify_files); returns device (crc, status) tensors."""
+    dev = _dev(ctx.device)
+    crc = torch.empty(max(batch.n_blocks, 1), dtype=torch.int32, device=dev)
+    st = torch.empty(max(batch.n_blocks, 1), dtype=torch.uint8, device=dev)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    ctx.verify_files_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
+                          batch.src_bytes, crc.data_ptr(), st.data_ptr(), s.cuda_stream)
+    return crc, st

@@ -54,21 +54,81 @@ std::vector<uint32_t> build_crc_tables() {
   return out;
 }
 
+// GF(2) polynomials modulo the reflected CRC-32 polynomial, bit 31 = x^0 (zlib's crc32.c
+// multmodp / x2nmodp, restated): a * b mod P, for a != 0.
+uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+// x^(8n) mod P: the operator "append n zero bytes" (Z_n(a) = multmodp(x8n(n), a)).
+uint32_t x8n(uint64_t n) {
+  uint32_t x2k[64];
+  x2k[0] = 1u << 30;  // x^1
+  for (int k = 1; k < 64; k++) x2k[k] = multmodp(x2k[k - 1], x2k[k - 1]);  // x^(2^k)
+  uint32_t p = 1u << 31;  // x^0
+  for (int k = 3; n; n >>= 1, k++)
+    if (n & 1) p = multmodp(x2k[k], p);
+  return p;
+}
+
+// Range-CRC tables (tpz_crc.hip): ids 0..15 = T_0..T_15; ids 16 + 4j + i = T_{n-1-i},
+// n = 16 * 2^j; T_k[b] = Z_k(T_0[b]).
+std::vector<uint32_t> build_range_tables() {
+  uint32_t t0[256];
+  for (uint32_t b = 0; b < 256; b++) {
+    uint32_t c = b;
+    for (int i = 0; i < 8; i++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    t0[b] = c;
+  }
+  std::vector<uint32_t> out((size_t)tpz::kRangeTables * 256);
+  auto put = [&](int id, uint64_t k) {
+    const uint32_t z = x8n(k);
+    for (uint32_t b = 0; b < 256; b++) out[(size_t)id * 256 + b] = t0[b] ? multmodp(z, t0[b]) : 0u;
+  };
+  for (int k = 0; k < 16; k++) put(k, (uint64_t)k);
+  for (int j = 0; j < tpz::kRangeShiftOps; j++) {
+    const uint64_t n = 16ull << j;
+    for (int i = 0; i < 4; i++) put(16 + 4 * j + i, n - 1 - (uint64_t)i);
+  }
+  return out;
+}
+
+// The slice-by-4 tables T_0..T_3 replicated 32 times: word (t*256 + b)*32 + r = T_t[b].
+std::vector<uint32_t> build_rep_tables(const std::vector<uint32_t>& range) {
+  std::vector<uint32_t> out((size_t)tpz::kCrcRepWords);
+  for (int t = 0; t < 4; t++)
+    for (int b = 0; b < 256; b++)
+      for (int r = 0; r < 32; r++) out[((size_t)t * 256 + b) * 32 + r] = range[(size_t)t * 256 + b];
+  return out;
+}
+
 }  // namespace
 
-// Device workspace of one stream: the big-path worklist (counter + list) and the big path's
-// per-workgroup entry tables. Decodes on different streams run concurrently, so each stream
-// has its own; decodes on one stream are ordered by the stream.
+// Device workspace of one stream: the big-path worklist (counter + list), the big path's
+// per-workgroup entry tables and the range-CRC accumulators. Decodes on different streams run
+// concurrently, so each stream has its own; calls on one stream are ordered by the stream.
 struct tpz_workspace {
   uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
   uint32_t defer_cap = 0;
   uint64_t* d_big_scratch = nullptr;
+  uint32_t* d_acc = nullptr;    // 2 x acc_cap: per-range accumulators of tpz_crc32_ranges
+  uint32_t acc_cap = 0;
 };
 
 struct tpz_ctx {
   int device = 0;
   uint32_t num_cus = 0;
-  uint32_t* d_tables = nullptr;
+  uint32_t* d_tables = nullptr;        // block-decode CRC tables
+  uint32_t* d_range_tables = nullptr;  // range-CRC tables
+  uint32_t* d_rep_tables = nullptr;    // replicated slice-by-4 tables
   std::mutex mu;  // guards the workspace map
   std::unordered_map<void*, tpz_workspace> ws;
 };
@@ -78,7 +138,25 @@ namespace {
 void free_workspace(tpz_workspace& w) {
   if (w.d_defer) (void)hipFree(w.d_defer);
   if (w.d_big_scratch) (void)hipFree(w.d_big_scratch);
+  if (w.d_acc) (void)hipFree(w.d_acc);
   w = tpz_workspace{};
+}
+
+// The stream's range-CRC accumulators, grown to n ranges. Caller holds c->mu.
+tpz_err get_acc(tpz_ctx* c, void* stream, uint32_t n, uint32_t** out) {
+  tpz_workspace& w = c->ws[stream];
+  if (!w.d_acc || w.acc_cap < n) {
+    uint32_t* d = nullptr;
+    TPZ_HIP(hipMalloc(&d, (size_t)2 * n * 4));
+    if (w.d_acc) {
+      (void)hipStreamSynchronize((hipStream_t)stream);
+      (void)hipFree(w.d_acc);
+    }
+    w.d_acc = d;
+    w.acc_cap = n;
+  }
+  *out = w.d_acc;
+  return TPZ_SUCCESS;
 }
 
 // The stream's workspace, grown to max_blocks. Caller holds c->mu.
@@ -105,9 +183,10 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
 
 extern "C" {
 
-uint64_t tpz_layout_key_base(uint64_t ext_i, uint64_t i) { return tpz_key_base(ext_i, i); }
+uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i) { return tpz_slot_base(ext_i, i); }
+uint64_t tpz_layout_value_start(uint64_t key_bytes) { return tpz_value_start(key_bytes); }
 uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i) { return tpz_entry_base(ext_i, i); }
-uint64_t tpz_layout_col_capacity(uint64_t s, uint64_t n) { return tpz_col_capacity(s, n); }
+uint64_t tpz_layout_data_capacity(uint64_t s, uint64_t n) { return tpz_data_capacity(s, n); }
 uint64_t tpz_layout_entry_capacity(uint64_t s, uint64_t n) { return tpz_entry_capacity(s, n); }
 
 const char* tpz_last_error(void) { return g_last_error.c_str(); }
@@ -130,9 +209,15 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
   tpz_ctx* c = new tpz_ctx();
   c->device = device;
   c->num_cus = (uint32_t)prop.multiProcessorCount;
-  std::vector<uint32_t> t = build_crc_tables();
-  hipError_t e = hipMalloc(&c->d_tables, t.size() * 4);
-  if (e == hipSuccess) e = hipMemcpy(c->d_tables, t.data(), t.size() * 4, hipMemcpyHostToDevice);
+  const std::vector<uint32_t> t = build_crc_tables();
+  const std::vector<uint32_t> rt = build_range_tables();
+  const std::vector<uint32_t> rep = build_rep_tables(rt);
+  hipError_t e = hipSuccess;
+  for (auto [dst, v] : {std::make_pair(&c->d_tables, &t), std::make_pair(&c->d_range_tables, &rt),
+                        std::make_pair(&c->d_rep_tables, &rep)}) {
+    if (e == hipSuccess) e = hipMalloc(dst, v->size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(*dst, v->data(), v->size() * 4, hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     tpz_ctx_destroy(c);
     return hip_fail(e, "tpz_ctx_create");
@@ -146,6 +231,8 @@ void tpz_ctx_destroy(tpz_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();  // decodes still in flight use the workspaces
   if (c->d_tables) (void)hipFree(c->d_tables);
+  if (c->d_range_tables) (void)hipFree(c->d_range_tables);
+  if (c->d_rep_tables) (void)hipFree(c->d_rep_tables);
   for (auto& kv : c->ws) free_workspace(kv.second);
   delete c;
 }
@@ -161,8 +248,8 @@ tpz_err tpz_ctx_reserve(tpz_ctx* c, uint32_t max_blocks, void* stream) {
 tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, void* stream) {
   if (!c || !b || !o) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
-  if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_vals || !o->d_ends || !o->d_count ||
-      !o->d_status || !o->d_crc)
+  if (!b->d_src || !b->d_ext || !o->d_data || !o->d_ends || !o->d_count || !o->d_status ||
+      !o->d_crc)
     return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz_workspace* w = nullptr;
@@ -179,8 +266,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.src_bytes = b->src_bytes;
   a.n_blocks = b->n_blocks;
   a.crc_tables = c->d_tables;
-  a.keys = o->d_keys;
-  a.vals = o->d_vals;
+  a.data = o->d_data;
   a.ends = o->d_ends;
   a.count = o->d_count;
   a.status = o->d_status;
@@ -193,6 +279,48 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   tpz::launch_decode(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
+}
+
+static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint32_t* d_crc,
+                          uint8_t* d_status, void* stream) {
+  if (!c || !r || !d_crc) return TPZ_ERR_INVALID_ARG;
+  if (r->n_blocks == 0) return TPZ_SUCCESS;
+  if (!r->d_src || !r->d_ext) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  uint32_t* acc = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err e = get_acc(c, stream, r->n_blocks, &acc);
+    if (e != TPZ_SUCCESS) return e;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TPZ_HIP(hipMemsetAsync(acc, 0, (size_t)2 * r->n_blocks * 4, s));
+  tpz::CrcLaunch a{};
+  a.src = r->d_src;
+  a.ext = r->d_ext;
+  a.src_bytes = r->src_bytes;
+  a.n_ranges = r->n_blocks;
+  a.trailer = trailer;
+  a.tables = c->d_range_tables;
+  a.rep = c->d_rep_tables;
+  a.acc = acc;
+  a.acc_last = acc + r->n_blocks;
+  a.crc = d_crc;
+  a.status = d_status;
+  a.num_cus = c->num_cus;
+  tpz::launch_crc_ranges(a, s);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_crc32_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t* d_crc, void* stream) {
+  return crc_ranges(c, r, 0, d_crc, nullptr, stream);
+}
+
+tpz_err tpz_verify_files(tpz_ctx* c, const tpz_batch* f, uint32_t* d_crc, uint8_t* d_status,
+                         void* stream) {
+  if (!d_status) return TPZ_ERR_INVALID_ARG;
+  return crc_ranges(c, f, 4, d_crc, d_status, stream);
 }
 
 int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actual, char* buf,

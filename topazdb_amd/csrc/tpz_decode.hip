@@ -21,11 +21,12 @@
 //  readlane across rows) combines with shift-by-16*2^k operators. All operators are
 //  byte-sliced lookup tables in LDS (40 KiB).
 //  Decode: lanes parse 64 entries at a time (n, offsets, klen, vlen, bounds checks that mirror
-//  the reference's panics), a DPP wave prefix sum gives packed output positions, and each
-//  entry marks the 16-byte output chunks that start inside it in a chunk->entry map. The copy
-//  is output-driven: lane c assembles output chunk c from the (usually one) source segment(s)
-//  covering it with two ds_read_b128 + a funnel shift per segment, then one coalesced dwordx4
-//  store (1 KiB per wave instruction).
+//  the reference's panics), DPP wave prefix sums give packed output positions in the block's
+//  output stream (key bytes, then value bytes from the next 16-byte boundary), and every
+//  non-empty key and value goes into one entry table plus a chunk->entry map. The copy is
+//  output-driven over that single stream: lane c assembles output chunk c from the (usually
+//  one) source segment(s) covering it, then one coalesced dwordx4 store (1 KiB per wave
+//  instruction).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,28 +51,28 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
-// wave path slot: [guard 96][window 4352][pad 32][ktab 256 x u32][vtab 256 x u32]
-//                 [kmap 288 x u8][vmap 288 x u8]
+// wave path slot: [guard 96][window 4352][pad 32][entry table 512 x u32][map 288 x u16]
 // The window holds any block of a block_size <= 4 KiB builder (<= 4101 B; topazdb's default,
 // src/opt.rs:39); longer blocks take the big path.
 constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads, the 5th partial
 constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
-constexpr u32 kWaveMaxN = 255;                      // map entries hold (compact index + 1) as u8
-constexpr int kWaveMapLen = 288;                    // >= kWinBytes / 16 + 1 chunk map slots
-constexpr int kSlotBytes = kGuard + kWinBytes + 32 + 256 * 8 + 2 * kWaveMapLen;
-static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 16 == 0, "slot alignment");
+constexpr u32 kWaveMaxN = 255;                      // the table holds 2n + 1 <= 511 entries
+constexpr int kWaveMapLen = 288;                    // >= (kWaveMaxLen + 2) / 16 + 3 map slots
+constexpr int kSlotBytes = kGuard + kWinBytes + 32 + 512 * 4 + 2 * kWaveMapLen;
+static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 8 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard 96][window 92 KiB][pad 32][kmap u16][vmap u16];
-// entry tables in global scratch
+// big path (one wave per block): [guard 96][window 92 KiB][pad 32][map u16]; the entry table
+// is in global scratch
 constexpr int kBigWinBytes = 94208;
 constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
-constexpr int kBigMapLen = 5904;                    // >= kBigWinBytes / 16 + 1
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + 2 * kBigMapLen * 2;
+constexpr int kBigMapLen = 5904;                    // >= (kBigMaxLen + 2) / 16 + 3
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
-static_assert((kBigMapLen * 2) % 16 == 0, "big map alignment");
+static_assert(kBigMapLen % 8 == 0 && (kWaveMaxLen + 2) / 16 + 3 <= (u32)kWaveMapLen &&
+              (kBigMaxLen + 2) / 16 + 3 <= (u32)kBigMapLen, "map sizes");
 static_assert(kBigLds <= 163840, "big path LDS");
 
 // ------------------------------------------------------------------ small helpers
@@ -242,10 +243,11 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
 }
 
 // ------------------------------------------------------------------ entry tables
-// Per column, the NON-EMPTY entries in order (compacted): end = inclusive end offset of the
-// entry's bytes in the column, delta = (LDS offset of its first byte) - (its start offset in
-// the column), so byte x of the column inside that entry sits at LDS offset x + delta.
-// Wave path: one u32 per entry, (end << 16) | (u16)delta (block <= 5104 B).
+// The NON-EMPTY keys in order, then the non-empty values in order (one table for the block's
+// output stream): end = exclusive end offset of the segment's bytes in the stream, delta = (LDS
+// offset of its first byte) - (its start offset in the stream), so byte x of the stream inside
+// that segment sits at LDS offset x + delta.
+// Wave path: one u32 per segment, (end << 16) | (u16)delta (block <= 4336 B).
 struct ColSmall {
   u32* t;
   __device__ __forceinline__ void put(u32 k, u32 end, int delta) const {
@@ -316,10 +318,41 @@ __device__ __forceinline__ u32 lanes_below(u64 mask) {
   return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
 }
 
+// ------------------------------------------------------------------ diagnostic stamps
+// TPZ_ABL_STAMPS (a timing-only diagnostic build, never shipped): per-wave cycle sums per phase,
+// read with s_memtime (cdna_hip_programming.md §7 "In-kernel stamps"), stored once per wave in
+// a buffer of their own (g_stamps). Phases: 0 wait for the prefetched block + stage it into
+// LDS, 1 issue the next block's loads, 2 header + parse, 3 copy, 4 CRC, 5 status write + loop.
+#ifdef TPZ_ABL_STAMPS
+constexpr int kStampWaves = 256 * kWavesPerWG;
+__device__ u64 g_stamps[kStampWaves * 8];
+struct Stamps {
+  u64 t[6] = {0, 0, 0, 0, 0, 0};
+  u64 last = 0;
+};
+__device__ __forceinline__ u64 stamp_now() {
+  u64 t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define TPZ_STAMP(S, k)               \
+  do {                                \
+    const u64 now_ = stamp_now();     \
+    (S).t[k] += now_ - (S).last;      \
+    (S).last = now_;                  \
+  } while (0)
+#else
+struct Stamps {};
+#define TPZ_STAMP(S, k) \
+  do {                  \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------ per-block decode
 struct Out {
-  uint8_t* keys;
-  uint8_t* vals;
+  uint8_t* data;
   u32* ends;
   u32* count;
   uint8_t* status;
@@ -354,59 +387,41 @@ __device__ __forceinline__ uint4 merge_at(uint4 a, uint4 w, int m) {
   return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
 }
 
-// One output column of a block: its entry table, its chunk map (LDS: map[t] = 1 + the compact
-// index of an entry whose end lies in (16(t-1), 16t], written by the parse), entry count,
-// byte count and destination slot.
-template <class Col, class MapT>
-struct ColOut {
-  Col col;
-  const MapT* map;
-  u32 nk, tot;
-  uint8_t* dst;
-  __device__ __forceinline__ u32 nchunks() const { return (tot + 15) >> 4; }
-  __device__ __forceinline__ u32 npad() const { return (nchunks() + 7) & ~7u; }  // whole 128-B lines
-};
-
 // Source of the copy: the staged LDS window.
 struct Src16 {
   const uint8_t* win;
   __device__ __forceinline__ uint4 operator()(int x) const { return lds_window16(win, x); }
 };
 
-// Output-driven copy of both columns: the wave takes 64 output chunks of 16 B per window (lane l
-// chunk c = t0 + l), so every store is a coalesced 1 KiB; key windows first, then value windows.
-//   1. chunk -> entry: the parse scattered (1 + compact index) of every entry into the chunk map
-//      at t = ceil(end / 16), the first chunk starting at or after the entry's end, so a wave
-//      prefix max of map[c] (carried across the column's windows) is the number of entries that
-//      end at or before the chunk start = the entry j holding its first byte. (Two entries ending
-//      in one chunk race for one map byte; a lane that got the smaller index walks forward.)
-//   2. entries j and j + 1 from the entry table.
-//   3. the chunk's bytes from LDS at x0 + delta_j; a chunk crossing entry j's end takes entry
+// Output-driven copy of a block's stream (tot bytes: the keys, a gap to the next 16-byte
+// boundary, the values): the wave takes 64 output chunks of 16 B per window (lane l: chunk
+// c = 64 w + l), so every store is a coalesced 1 KiB.
+//   1. chunk -> segment: the parse scattered (1 + table index) of every segment into the chunk
+//      map at t = ceil(end / 16), the first chunk starting at or after the segment's end, so a
+//      wave prefix max of map[c] (carried across windows) is the number of segments that end at
+//      or before the chunk start = the segment j holding its first byte. (Two segments ending in
+//      one chunk race for one map slot; a lane that got the smaller index walks forward.)
+//   2. segments j and j + 1 from the entry table.
+//   3. the chunk's bytes from LDS at x0 + delta_j; a chunk crossing segment j's end takes segment
 //      j+1's bytes after it (exec-masked second read + 64-bit mask select); chunks spanning 3+
-//      entries (entries shorter than 16 B) take a loop.
+//      segments (entries shorter than 16 B) take a loop. The key/value gap is such a crossing:
+//      its bytes are unspecified.
 //   4. store; pad chunks up to the 128-byte line are zeroed.
 template <class Col, class MapT, class S>
-__device__ __forceinline__ void copy_columns(const S& src, const ColOut<Col, MapT>& K,
-                                             const ColOut<Col, MapT>& V, u32 map_len) {
+__device__ __forceinline__ void copy_stream(const S& src, const Col& col, const MapT* map, u32 nk,
+                                            u32 tot, uint8_t* dst, u32 map_len) {
   const u32 lane = lane_id();
-  const u32 nwk = (K.npad() + 63) >> 6;
-  const u32 nw = nwk + ((V.npad() + 63) >> 6);
+  const u32 nch = (tot + 15) >> 4;
+  const u32 npad = (nch + 7) & ~7u;                   // whole 128-byte lines
+  const u32 nw = (npad + 63) >> 6;
+  const u32 last = nk ? nk - 1 : 0u;
 #ifdef TPZ_ABL_MEMONLY
-  for (u32 c = lane; c < K.npad(); c += 64) *reinterpret_cast<uint4*>(K.dst + c * 16) = make_uint4(c, 0, 0, 0);
-  for (u32 c = lane; c < V.npad(); c += 64) *reinterpret_cast<uint4*>(V.dst + c * 16) = make_uint4(c, 0, 0, 0);
+  for (u32 c = lane; c < npad; c += 64) *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(c, 0, 0, 0);
   return;
 #endif
   u32 carry = 0;
   for (u32 w = 0; w < nw; w++) {
-    const bool isk = w < nwk;
-    if (w == nwk) carry = 0;                          // first value window
-    const Col col = isk ? K.col : V.col;
-    const MapT* map = isk ? K.map : V.map;
-    const u32 nk = isk ? K.nk : V.nk, nch = isk ? K.nchunks() : V.nchunks();
-    const u32 npad = isk ? K.npad() : V.npad();
-    uint8_t* dst = isk ? K.dst : V.dst;
-    const u32 last = nk ? nk - 1 : 0u;
-    const u32 c = 64 * (isk ? w : w - nwk) + lane;
+    const u32 c = 64 * w + lane;
     const u32 x0 = 16 * c;
     const bool act = c < nch;
     // 1. chunk -> entry: prefix max of the map, carried across the column's windows
@@ -460,12 +475,12 @@ __device__ __forceinline__ void copy_columns(const S& src, const ColOut<Col, Map
   }
 }
 
-// Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. kmap / vmap are
-// the column chunk maps (kMapLen entries each, LDS, contiguous: vmap = kmap + kMapLen).
+// Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. `map` is the
+// stream's chunk map (kMapLen slots, LDS), `col` its entry table.
 template <class Col, class MapT, int kMapLen, bool BIG>
-__device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& kcol,
-                                             const Col& vcol, MapT* kmap, MapT* vmap, u32 a0,
-                                             u32 len, u32 b, u64 ext_b, const Out& o) {
+__device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
+                                             MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
+                                             const Out& o, Stamps& S) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
@@ -501,12 +516,30 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
     const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
     {
-      // clear the chunk maps up to the largest chunk index this block can produce
+      // clear the chunk map up to the largest chunk index a non-OVERLAP block can produce
+      // (stream <= len + 2 bytes)
       constexpr u32 per = 16 / sizeof(MapT);
-      const u32 nz = min((u32)kMapLen, ((len >> 4) + 2 + per - 1) / per * per);
-      for (u32 i = lane; i < nz / per; i += 64) {
-        reinterpret_cast<uint4*>(kmap)[i] = make_uint4(0, 0, 0, 0);
-        reinterpret_cast<uint4*>(vmap)[i] = make_uint4(0, 0, 0, 0);
+      const u32 nz = min((u32)kMapLen, ((len >> 4) + 3 + per - 1) / per * per);
+      for (u32 i = lane; i < nz / per; i += 64)
+        reinterpret_cast<uint4*>(map)[i] = make_uint4(0, 0, 0, 0);
+    }
+    // The value segments follow the key segments in the table, and the values start at the
+    // 16-byte boundary after the keys: both need the block's key totals before the first table
+    // write. One parse round (n <= 64) has them after its scan; longer blocks count first.
+    u32 ktot = 0, knz_all = 0;
+    if (n > 64) {
+      for (u32 g0 = 0; g0 < n; g0 += 64) {
+        const u32 i = g0 + lane;
+        u32 kl = 0;
+        if (i < n) {
+          const u32 off = lds_be16(win, a0 + 2 + 2 * i);
+          if (off + 2 <= dl) {
+            kl = lds_be16(win, db + off);
+            if (off + 4 + kl > dl) kl = 0;
+          }
+        }
+        knz_all += __builtin_popcountll(__ballot(kl != 0));
+        ktot += readlane(wave_scan_incl(kl), 63);
       }
     }
     u32 kc = 0, vc = 0, knz = 0, vnz = 0;
@@ -527,19 +560,25 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       const u32 ki = wave_scan_incl(kl) + kc;
       const u32 vi = wave_scan_incl(vl) + vc;
       const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+      if (n <= 64) {
+        ktot = readlane(ki, 63);
+        knz_all = __builtin_popcountll(kmask);
+      }
+      const u32 vs = (ktot + 15) & ~15u;  // value stream start (tpz_value_start)
       if (slots_fit && i < n_pad) ends_g[i] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
       if (act && slots_fit) {
         // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
-        // after the entry's end (entries whose end overflows the map only occur in OVERLAP blocks)
+        // after the segment's end (ends beyond the map only occur in OVERLAP blocks)
         if (kl) {
           const u32 m = knz + lanes_below(kmask);
-          kcol.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
-          if (((ki + 15) >> 4) < (u32)kMapLen) kmap[(ki + 15) >> 4] = (MapT)(m + 1);
+          col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
+          if (((ki + 15) >> 4) < (u32)kMapLen) map[(ki + 15) >> 4] = (MapT)(m + 1);
         }
         if (vl) {
-          const u32 m = vnz + lanes_below(vmask);
-          vcol.put(m, vi, (int)(db + off + 4 + kl) - (int)(vi - vl));
-          if (((vi + 15) >> 4) < (u32)kMapLen) vmap[(vi + 15) >> 4] = (MapT)(m + 1);
+          const u32 m = knz_all + vnz + lanes_below(vmask);
+          const u32 ve = vs + vi;
+          col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
+          if (((ve + 15) >> 4) < (u32)kMapLen) map[(ve + 15) >> 4] = (MapT)(m + 1);
         }
       }
       knz += __builtin_popcountll(kmask);
@@ -548,10 +587,12 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       vc = readlane(vi, 63);
     }
 
+    const u32 vs = (kc + 15) & ~15u;
+    TPZ_STAMP(S, 2);
     if (bad) {
       st = TPZ_BLOCK_MALFORMED;
       cnt = 0;
-    } else if (!slots_fit || kc > len || vc > len) {
+    } else if (!slots_fit || vs + vc > len + 2) {   // the slot holds len + 129 bytes
       st = TPZ_BLOCK_OVERLAP;
     } else {
       if (BIG) {
@@ -559,13 +600,12 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       }
       __builtin_amdgcn_wave_barrier();
-      const u64 kb = key_base(ext_b, b);
 #ifndef TPZ_ABL_NOCOPY
-      const ColOut<Col, MapT> K{kcol, kmap, knz, kc, o.keys + kb};
-      const ColOut<Col, MapT> V{vcol, vmap, vnz, vc, o.vals + kb};
-      copy_columns(Src16{win}, K, V, (u32)kMapLen);
+      copy_stream(Src16{win}, col, map, knz + vnz, vs + vc, o.data + slot_base(ext_b, b),
+                  (u32)kMapLen);
 #endif
     }
+    TPZ_STAMP(S, 3);
 #endif
   }
   __builtin_amdgcn_wave_barrier();
@@ -597,6 +637,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     st = TPZ_BLOCK_CHECKSUM_MISMATCH;
     cnt = 0;
   }
+  TPZ_STAMP(S, 4);
   put_meta(o, b, st, cnt, crc);
 }
 
@@ -655,28 +696,52 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   uint8_t* slot = lds + kTableBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
-  const ColSmall kcol{reinterpret_cast<u32*>(etab)};
-  const ColSmall vcol{reinterpret_cast<u32*>(etab + 256 * 4)};
-  uint8_t* kmap = etab + 256 * 8;
-  uint8_t* vmap = kmap + kWaveMapLen;
+  const ColSmall col{reinterpret_cast<u32*>(etab)};
+  uint16_t* map = reinterpret_cast<uint16_t*>(etab + 512 * 4);
 
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   const u32 nw = gridDim.x * kWavesPerWG;
   u32 b = blockIdx.x * kWavesPerWG + wid;
+  Stamps S;
+#ifdef TPZ_ABL_STAMPS
+  S.last = stamp_now();
+#endif
+
+  // Extents of this wave's blocks, 64 at a time: lane l of a group holds ext[] of the wave's
+  // block 64 g + l (block index b0 + k nw). The next group is loaded one group ahead with vector
+  // loads that complete behind the block prefetch, so a block's extent is two readlanes instead
+  // of a memory round trip on the critical path.
+  const u32 b0 = b;
+  u64 gs_cur, ge_cur, gs_nxt, ge_nxt;
+  auto load_group = [&](u32 g, u64& gs, u64& ge) {
+    // lanes past the batch re-read the last extent (unconditional: the load writes its
+    // destination registers directly, nothing waits for it until the group is used)
+    u64 bb = (u64)b0 + ((u64)g * 64 + lane) * nw;
+    bb = bb < p.n_blocks ? bb : p.n_blocks - 1;
+    gs = p.ext[bb];
+    ge = p.ext[bb + 1];
+  };
+  auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
+  load_group(0, gs_cur, ge_cur);
+  load_group(1, gs_nxt, ge_nxt);
 
   // prefetch state for block b
   uint4 v[kWinRounds];
   u64 s_cur = 0, e_cur = 0;
-  auto issue = [&](u32 bb, u64& s, u64& e) {
+  auto issue = [&](u32 bb, u32 k, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
-    s = uni64(p.ext[bb]);
-    e = uni64(p.ext[bb + 1]);
+    s = lane64(gs_cur, k & 63);
+    e = lane64(ge_cur, k & 63);
     const u64 len = e - s;
     if (len > kWaveMaxLen) return;
     const u64 ws = s & ~15ull;
     const u32 nbytes = (u32)(e - ws);
     const u32 rounds = (nbytes + 1023) >> 10;
-    __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, p.src_bytes, ws);
+    // the descriptor ends at the block's last 16-byte piece: lanes past it fetch nothing (the
+    // next block's bytes are loaded once, by the wave that decodes it)
+    const u64 e16 = (e + 15) & ~(u64)15;
+    const u64 lim = p.src_bytes < e16 ? p.src_bytes : e16;
+    __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, lim, ws);
 #pragma unroll
     for (int r = 0; r < kWinRounds; r++)
       if ((u32)r < rounds) v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
@@ -686,7 +751,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
         if ((u32)r < rounds) fix_tail(v[r], p.src, ws + r * 1024 + lane * 16, p.src_bytes);
     }
   };
-  issue(b, s_cur, e_cur);
+  u32 k = 0;  // this wave's block counter
+  issue(b, 0, s_cur, e_cur);
 
   while (b < p.n_blocks) {
     const u64 s = s_cur, e = e_cur;
@@ -700,20 +766,34 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
         if ((u32)r < rounds && r * 1024 + lane * 16 < (u32)kWinBytes)
           *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
     }
+    TPZ_STAMP(S, 0);
     const u32 bcur = b;
     b += nw;
-    issue(b, s_cur, e_cur);          // next block's loads fly while this one decodes
+    k++;
+    if ((k & 63) == 0) {             // next extent group (its loads completed long ago)
+      gs_cur = gs_nxt;
+      ge_cur = ge_nxt;
+      load_group((k >> 6) + 1, gs_nxt, ge_nxt);
+    }
+    issue(b, k, s_cur, e_cur);       // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
+    TPZ_STAMP(S, 1);
     if (fits) {
-      decode_block<ColSmall, uint8_t, kWaveMapLen, false>(tab, win, kcol, vcol, kmap, vmap,
-                                                          (u32)(s & 15u), len64, bcur, s, p.out);
+      decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
+                                                           len64, bcur, s, p.out, S);
     } else if (len64 > kBigMaxLen) {
       put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
     } else if (lane == 0) {
       p.out.defer_list[atomicAdd(p.out.defer_count, 1u)] = bcur;
     }
     __builtin_amdgcn_wave_barrier();
+    TPZ_STAMP(S, 5);
   }
+#ifdef TPZ_ABL_STAMPS
+  const u32 gw = blockIdx.x * kWavesPerWG + wid;
+  if (lane == 0 && gw < (u32)kStampWaves)
+    for (int k = 0; k < 6; k++) g_stamps[gw * 8 + k] = S.t[k];
+#endif
 }
 
 // ------------------------------------------------------------------ big path kernel
@@ -724,10 +804,9 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
   const u32 lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[lane] = make_uint4(0, 0, 0, 0);
-  const ColBig kcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
-  const ColBig vcol{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots + kBigMaxSlots};
-  uint16_t* kmap = reinterpret_cast<uint16_t*>(win + kBigWinBytes + 32);
-  uint16_t* vmap = kmap + kBigMapLen;
+  const ColBig col{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
+  uint16_t* map = reinterpret_cast<uint16_t*>(win + kBigWinBytes + 32);
+  Stamps S;
   const u32 cnt = uni(*p.out.defer_count);
   for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
     const u32 b = uni(p.out.defer_list[it]);
@@ -735,7 +814,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
     const u32 len = (u32)(e - s);
     const u64 ws = s & ~15ull;
     const u32 nbytes = (u32)(e - ws);
-    __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, p.src_bytes, ws);
+    const u64 e16 = (e + 15) & ~(u64)15;
+    __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, p.src_bytes < e16 ? p.src_bytes : e16, ws);
     for (u32 off = 0; off < nbytes; off += 4096) {
       uint4 t[4];
 #pragma unroll
@@ -749,8 +829,8 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, uint16_t, kBigMapLen, true>(tab, win, kcol, vcol, kmap, vmap,
-                                                     (u32)(s & 15u), len, b, s, p.out);
+    decode_block<ColBig, uint16_t, kBigMapLen, true>(tab, win, col, map, (u32)(s & 15u), len, b,
+                                                     s, p.out, S);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -763,7 +843,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
   p.big_scratch = a.big_scratch;
-  p.out = Out{a.keys, a.vals, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count};
+  p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count};
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
@@ -772,3 +852,11 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
 }
 
 }  // namespace tpz
+
+#ifdef TPZ_ABL_STAMPS
+// Diagnostic build only: copies the per-wave phase sums (8 u64 per wave, 6 used) to the host.
+extern "C" int tpz_debug_stamps(unsigned long long* host, int n_waves) {
+  if (n_waves > tpz::kStampWaves) n_waves = tpz::kStampWaves;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tpz::g_stamps), (size_t)n_waves * 8 * 8);
+}
+#endif

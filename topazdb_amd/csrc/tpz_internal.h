@@ -8,7 +8,7 @@
 
 namespace tpz {
 
-// CRC-32 lookup tables uploaded once per context (see tpz_api.cpp: build_crc_tables):
+// CRC-32 lookup tables of the block decode, uploaded once per context (tpz_api.cpp):
 // ids 0..15 = T_0..T_15 (slice-by-16); ids 16+4j+i = T_{n_j-1-i}: the shift-by-n_j operator,
 // n_j = kCrcShiftBytes[j] = 80 * 2^j (the lane-position shifts of the CRC combine; 2 x 2560 B
 // chains the 5120-B super-rounds of long blocks);
@@ -17,11 +17,19 @@ constexpr int kNumCrcTables = 41;
 constexpr int kCrcInvTable = 40;
 constexpr int kCrcLaneBytes = 80;
 constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
-// Big path entry-table capacity per block: slots are only written when 6n <= len.
+// Big path entry-table capacity per block and column: slots are only written when 6n <= len
+// (the unified key+value table holds 2 x this).
 constexpr uint32_t kBigMaxSlots = TPZ_MAX_BLOCK_BYTES / 6 + 16;
 
+// Range CRC (tpz_crc.hip): shift-by-16*2^j operators j = 0..kRangeShiftOps-1 in the global
+// range tables (ranges up to 16 * 2^kRangeShiftOps bytes), and the 32-fold replicated
+// slice-by-4 table (4 x 256 x 32 u32).
+constexpr int kRangeShiftOps = 32;
+constexpr int kRangeTables = 16 + 4 * kRangeShiftOps;
+constexpr int kCrcRepWords = 4 * 256 * 32;
+
 // Slotted layout (include/tpz_gpu.h), callable from device code.
-__host__ __device__ inline uint64_t key_base(uint64_t ext_i, uint64_t i) {
+__host__ __device__ inline uint64_t slot_base(uint64_t ext_i, uint64_t i) {
   return ((ext_i + 127u) & ~(uint64_t)127u) + 256u * i;
 }
 __host__ __device__ inline uint64_t entry_base(uint64_t ext_i, uint64_t i) {
@@ -34,8 +42,7 @@ struct LaunchArgs {
   uint64_t src_bytes;
   uint32_t n_blocks;
   const uint32_t* crc_tables;
-  uint8_t* keys;
-  uint8_t* vals;
+  uint8_t* data;
   uint32_t* ends;
   uint32_t* count;
   uint8_t* status;
@@ -48,5 +55,22 @@ struct LaunchArgs {
 };
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
+
+struct CrcLaunch {
+  const uint8_t* src;
+  const uint64_t* ext;
+  uint64_t src_bytes;
+  uint32_t n_ranges;
+  uint32_t trailer;       // 0 (plain ranges) or 4 (FileObject: BE u32 trailer after the CRC)
+  const uint32_t* tables; // kRangeTables x 256
+  const uint32_t* rep;    // kCrcRepWords
+  uint32_t* acc;          // workspace: n_ranges, zeroed before the launch
+  uint32_t* acc_last;     // workspace: n_ranges, zeroed before the launch
+  uint32_t* crc;
+  uint8_t* status;        // null for plain ranges
+  uint32_t num_cus;
+};
+
+void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream);
 
 }  // namespace tpz

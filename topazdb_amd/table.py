@@ -1,0 +1,473 @@
+"""topazdb's read-side API over the MI355X decode path (the host mirror of the Rust interface).
+
+Same names, argument meaning and error behaviour as the reference:
+  FileObject        src/table/file_object.rs:13-91   open() verifies the whole-file CRC on the GPU
+  BlockMeta         src/table.rs:21-60
+  SsTable           src/table.rs:62-188               open() decodes every block of the table in one
+                                                      tpz_decode_blocks launch; read_block(_cached)
+                                                      serves the decoded blocks (the block cache)
+  Block             src/block.rs:21-65                decode() runs the one-block GPU decode
+  BlockIterator     src/block/iterator.rs:9-110
+  SsTableIterator   src/table/iterator.rs:10-96
+  Bloom.may_contain src/bloom.rs:72-84 (host; the filter is not on the decode path)
+
+Errors: where the reference returns an anyhow::Error, this raises BlockError whose text is the
+reference's message ("checksum: expected E, actual A", "data is empty", "invaild data"); where
+the reference panics (a malformed block, a file shorter than its checksum, seek_to_last on an
+empty block, ...) it raises ReferencePanic. Blocks the device does not decode yet (snappy/lz4,
+SURVEY.md §8f) raise BlockError("unsupported codec") — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import bisect
+import os
+import struct
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY, BLOCK_MALFORMED,
+                   BLOCK_OK, Context)
+from .batch import DeviceBatch, decode_batch, verify_files
+
+CHECKSUM_SIZE = 4  # src/checksum.rs:4
+SIZEOF_U16 = 2
+SIZEOF_U32 = 4
+
+
+class BlockError(RuntimeError):
+    """An anyhow::Error of the reference; str() is the reference's message."""
+
+
+class ReferencePanic(RuntimeError):
+    """The reference panics here (a Rust panic, not an Err)."""
+
+
+def _be32(b: bytes) -> int:
+    return struct.unpack(">I", b)[0]
+
+
+def _status_error(status: int, crc_expected: int, crc_actual: int) -> Exception:
+    msg = _lib.format_block_error(int(status), int(crc_expected), int(crc_actual))
+    if status == BLOCK_MALFORMED:
+        return ReferencePanic(msg)
+    return BlockError(msg)
+
+
+# ------------------------------------------------------------------------------- Block
+class Block:
+    """A decoded block (src/block.rs:21-24) held as its entries: key/value bytes plus positions.
+
+    Built from the device's decoded columns; `offsets()`/`data()` rebuild the reference's private
+    fields for a block written by BlockBuilder (entries back to back, src/block/builder.rs:26-57).
+    """
+
+    __slots__ = ("keys", "kpos", "vals", "vpos", "payload_len")
+
+    def __init__(self, keys: bytes, kpos, vals: bytes, vpos, payload_len: int | None = None):
+        self.keys, self.vals = keys, vals
+        self.kpos = [int(x) for x in kpos]
+        self.vpos = [int(x) for x in vpos]
+        n = len(self.kpos) - 1
+        self.payload_len = payload_len if payload_len is not None else (
+            SIZEOF_U16 + n * (SIZEOF_U16 * 3) + len(keys) + len(vals))
+
+    @property
+    def num_entries(self) -> int:
+        return len(self.kpos) - 1
+
+    def key_at(self, i: int) -> bytes:
+        return self.keys[self.kpos[i]:self.kpos[i + 1]]
+
+    def value_at(self, i: int) -> bytes:
+        return self.vals[self.vpos[i]:self.vpos[i + 1]]
+
+    def uncompress_size(self) -> int:
+        """src/block.rs:27-29: 2 + 2 * n + data.len() = the decoded payload length."""
+        return self.payload_len
+
+    def offsets(self) -> list[int]:
+        out, p = [], 0
+        for i in range(self.num_entries):
+            out.append(p)
+            p += 4 + (self.kpos[i + 1] - self.kpos[i]) + (self.vpos[i + 1] - self.vpos[i])
+        return out
+
+    def data(self) -> bytes:
+        return b"".join(struct.pack(">H", len(k)) + k + struct.pack(">H", len(v)) + v
+                        for k, v in ((self.key_at(i), self.value_at(i))
+                                     for i in range(self.num_entries)))
+
+    @staticmethod
+    def from_dense(d, b: int, payload_len: int | None = None) -> "Block":
+        e0, e1 = int(d.entry_base[b]), int(d.entry_base[b + 1])
+        k0, k1 = int(d.kpos[e0]), int(d.kpos[e1])
+        v0, v1 = int(d.vpos[e0]), int(d.vpos[e1])
+        return Block(d.keys[k0:k1].tobytes(), d.kpos[e0:e1 + 1] - k0,
+                     d.vals[v0:v1].tobytes(), d.vpos[e0:e1 + 1] - v0, payload_len)
+
+    @staticmethod
+    def decode(data: bytes, ctx: Context) -> "Block":
+        """Block::decode (src/block.rs:46-65) on the GPU: one block, one launch."""
+        blocks = _decode_region(ctx, bytes(data), np.array([0, len(data)], np.uint64))
+        r = blocks[0]
+        if isinstance(r, Exception):
+            raise r
+        return r
+
+
+def _decode_region(ctx: Context, region: bytes, ext: np.ndarray) -> list:
+    """Decode blocks [ext[i], ext[i+1]) of `region` in one tpz_decode_blocks launch. Returns per
+    block a Block or the exception the reference's Block::decode / iteration would raise."""
+    src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
+    batch = DeviceBatch(src, ext, ctx.device)
+    cols = decode_batch(ctx, batch)
+    torch.cuda.synchronize(torch.device("cuda", ctx.device))
+    d = cols.dense(batch.ext_host)
+    out = []
+    for b in range(batch.n_blocks):
+        st = int(d.status[b])
+        lo, hi = int(ext[b]), int(ext[b + 1])
+        if st == BLOCK_OK:
+            out.append(Block.from_dense(d, b, hi - lo - 5))
+        else:
+            expected = _be32(region[hi - 5:hi - 1]) if hi - lo >= 5 else 0
+            out.append(_status_error(st, expected, int(d.crc_actual[b])))
+    return out
+
+
+# ------------------------------------------------------------------------------- iterators
+class BlockIterator:
+    """src/block/iterator.rs:9-110 over a decoded Block."""
+
+    def __init__(self, block: Block):
+        self.block = block
+        self._key = b""
+        self._value = b""
+        self.idx = 0
+
+    @classmethod
+    def create_and_seek_to_first(cls, block: Block) -> "BlockIterator":
+        it = cls(block)
+        it.seek_to_first()
+        return it
+
+    @classmethod
+    def create_and_seek_to_key(cls, block: Block, key: bytes) -> "BlockIterator":
+        it = cls(block)
+        it.seek_to_key(key)
+        return it
+
+    def key(self) -> bytes:
+        return self._key
+
+    def value(self) -> bytes:
+        return self._value
+
+    def is_valid(self) -> bool:
+        """iterator.rs:50-52: valid while the current key is non-empty."""
+        return len(self._key) > 0
+
+    def seek_to_first(self) -> None:
+        self._seek_to(0)
+
+    def seek_to_last(self) -> None:
+        n = self.block.num_entries
+        if n == 0:  # offsets.len() - 1 underflows (iterator.rs:60)
+            raise ReferencePanic("attempt to subtract with overflow")
+        self._seek_to(n - 1)
+
+    def _seek_to(self, idx: int) -> None:
+        self._key = b""
+        self._value = b""
+        n = self.block.num_entries
+        if idx >= n:
+            self.idx = n
+            return
+        self.idx = idx
+        self._key = self.block.key_at(idx)
+        self._value = self.block.value_at(idx)
+
+    def next(self) -> None:
+        self._seek_to(self.idx + 1)
+
+    def seek_to_key(self, key: bytes) -> None:
+        """iterator.rs:91-109: binary search; an equal key returns early, else the lower bound."""
+        left, right = 0, self.block.num_entries
+        while left < right:
+            mid = (right - left) // 2 + left
+            mk = self.block.key_at(mid)
+            if mk > key:
+                right = mid
+            elif mk < key:
+                left = mid + 1
+            else:
+                self._seek_to(mid)
+                return
+        self._seek_to(left)
+
+
+# ------------------------------------------------------------------------------- files
+class FileObject:
+    """src/table/file_object.rs:13-91 (the file is kept in host memory once read)."""
+
+    def __init__(self, path: str, data: bytes):
+        self.file_name = path
+        self._data = data  # the whole file, trailer included
+        self._size = len(data) - CHECKSUM_SIZE
+        self._remove = True
+
+    def read(self, offset: int, length: int) -> bytes:
+        """file_object.rs:23-27: read_exact_at; a short read is an io error."""
+        if offset < 0 or length < 0 or offset + length > len(self._data):
+            raise BlockError("failed to fill whole buffer")
+        return self._data[offset:offset + length]
+
+    def size(self) -> int:
+        return self._size
+
+    @staticmethod
+    def create(path: str, data: bytes, ctx: Context) -> "FileObject":
+        """file_object.rs:33-54: write data + BE crc32(data), then open (create_new: the file
+        must not exist)."""
+        crc = _lib.lib().tpz_host_crc32
+        import ctypes as C
+        crc.argtypes = [C.c_char_p, C.c_uint64]
+        crc.restype = C.c_uint32
+        with open(path, "xb") as f:
+            f.write(data)
+            f.write(struct.pack(">I", crc(bytes(data), len(data))))
+        return FileObject.open(path, ctx)
+
+    @staticmethod
+    def open(path: str, ctx: Context) -> "FileObject":
+        """file_object.rs:57-78: read the whole file, verify its CRC (on the GPU)."""
+        with open(path, "rb") as f:
+            data = f.read()
+        return FileObject.open_many([(path, data)], ctx)[0]
+
+    @staticmethod
+    def open_many(files: list[tuple[str, bytes]], ctx: Context) -> list["FileObject"]:
+        """Many FileObject::open checks in one tpz_verify_files launch (LsmStorage::open opens
+        every live SST, src/level.rs:63-99)."""
+        lens = [len(d) for _, d in files]
+        ext = np.zeros(len(files) + 1, np.uint64)
+        np.cumsum(lens, out=ext[1:])
+        region = b"".join(d for _, d in files)
+        batch = DeviceBatch(np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8),
+                            ext, ctx.device)
+        crc, st = verify_files(ctx, batch)
+        torch.cuda.synchronize(torch.device("cuda", ctx.device))
+        crc = crc[:len(files)].cpu().numpy().view(np.uint32)
+        st = st[:len(files)].cpu().numpy()
+        out = []
+        for i, (path, data) in enumerate(files):
+            if st[i] == BLOCK_MALFORMED:
+                raise ReferencePanic(f"{path}: file shorter than its checksum")
+            if st[i] != BLOCK_OK:
+                raise _status_error(int(st[i]), _be32(data[-4:]), int(crc[i]))
+            out.append(FileObject(path, data))
+        return out
+
+    def save(self) -> None:
+        self._remove = False
+
+    def close(self) -> None:
+        """Drop (file_object.rs:85-91): the file is removed unless save() was called."""
+        if self._remove and os.path.exists(self.file_name):
+            os.remove(self.file_name)
+        self._remove = False
+
+
+# ------------------------------------------------------------------------------- table
+class BlockMeta:
+    """src/table.rs:21-60."""
+
+    __slots__ = ("offset", "first_key")
+
+    def __init__(self, offset: int, first_key: bytes):
+        self.offset, self.first_key = offset, first_key
+
+    def __eq__(self, o):
+        return isinstance(o, BlockMeta) and (self.offset, self.first_key) == (o.offset, o.first_key)
+
+    def __repr__(self):
+        return f"BlockMeta({self.offset}, {self.first_key!r})"
+
+    @staticmethod
+    def encode_block_meta(metas: list["BlockMeta"]) -> bytes:
+        return b"".join(struct.pack(">IH", m.offset & 0xFFFFFFFF, len(m.first_key) & 0xFFFF)
+                        + m.first_key for m in metas)
+
+    @staticmethod
+    def decode_block_meta(buf: bytes) -> list["BlockMeta"]:
+        metas, p = [], 0
+        while p < len(buf):
+            if p + 6 > len(buf):  # Buf::get_u32 / get_u16 past the end panics
+                raise ReferencePanic("advance out of bounds")
+            off, kl = struct.unpack(">IH", buf[p:p + 6])
+            if p + 6 + kl > len(buf):
+                raise ReferencePanic("copy_to_bytes out of bounds")
+            metas.append(BlockMeta(off, bytes(buf[p + 6:p + 6 + kl])))
+            p += 6 + kl
+        return metas
+
+
+class Bloom:
+    """src/bloom.rs:37-95 (decode + may_contain)."""
+
+    def __init__(self, filt: bytes):
+        self.filter = bytes(filt)
+
+    def may_contain(self, h: int) -> bool:
+        mask = (1 << 64) - 1
+        delta = ((h >> 34) | (h << 30)) & mask
+        k = self.filter[-1]
+        limit = (len(self.filter) - 1) * 8
+        for _ in range(k):
+            pos = h % limit
+            if not (self.filter[pos // 8] >> (pos % 8)) & 1:
+                return False
+            h = (h + delta) & mask
+        return True
+
+    def __eq__(self, o):
+        return isinstance(o, Bloom) and self.filter == o.filter
+
+
+class SsTable:
+    """src/table.rs:62-188. open() decodes the whole data region on the GPU in one launch and
+    keeps the decoded blocks, keyed by block index, as its block cache (read_block_cached,
+    src/table.rs:167-175)."""
+
+    def __init__(self, id: int, file: FileObject, metas, meta_off, bloom, blocks):
+        self.id = id
+        self.file = file
+        self.block_metas = metas
+        self.block_meta_offset = meta_off
+        self.bloom = bloom
+        self._blocks = blocks
+        self.size = file.size()
+        self.smallest_key = b""
+        self.biggest_key = b""
+
+    @staticmethod
+    def _read_bloom(file: FileObject):
+        """table.rs:75-87."""
+        size = file.size()
+        if size < SIZEOF_U32:
+            raise ReferencePanic("attempt to subtract with overflow")
+        offset = _be32(file.read(size - SIZEOF_U32, SIZEOF_U32))
+        if size == offset + SIZEOF_U32:
+            return offset, None
+        if offset + SIZEOF_U32 > size:
+            raise ReferencePanic("attempt to subtract with overflow")
+        return offset, Bloom(file.read(offset, size - SIZEOF_U32 - offset))
+
+    @classmethod
+    def open(cls, id: int, file: FileObject, ctx: Context) -> "SsTable":
+        """table.rs:91-112 + init_samllest_biggest_key (:143-151)."""
+        offset, bloom = cls._read_bloom(file)
+        if offset < SIZEOF_U32:
+            raise ReferencePanic("attempt to subtract with overflow")
+        meta_offset = _be32(file.read(offset - SIZEOF_U32, SIZEOF_U32))
+        if meta_offset > offset - SIZEOF_U32:
+            raise ReferencePanic("attempt to subtract with overflow")
+        metas = BlockMeta.decode_block_meta(
+            file.read(meta_offset, offset - SIZEOF_U32 - meta_offset))
+        ext = np.array([m.offset for m in metas] + [meta_offset], np.uint64)
+        if len(metas) and (np.diff(ext.astype(np.int64)) < 0).any():
+            raise ReferencePanic("range start index out of range")  # read_block's end - offset
+        region = file.read(0, meta_offset)
+        blocks = _decode_region(ctx, region, ext) if metas else []
+        t = cls(id, file, metas, meta_offset, bloom, blocks)
+        t.init_samllest_biggest_key()
+        return t
+
+    def may_contain(self, key: bytes) -> bool:
+        """table.rs:114-119 (xxh3_64 of the key)."""
+        if self.bloom is None:
+            return True
+        import xxhash
+        return self.bloom.may_contain(xxhash.xxh3_64_intdigest(key))
+
+    def init_samllest_biggest_key(self) -> None:
+        if not self.block_metas:
+            raise ReferencePanic("index out of bounds: the len is 0 but the index is 0")
+        self.smallest_key = self.block_metas[0].first_key
+        it = BlockIterator.create_and_seek_to_first(self.read_block(self.num_of_blocks() - 1))
+        it.seek_to_last()
+        if not it.is_valid():
+            raise ReferencePanic("assertion failed: iter.is_valid()")
+        self.biggest_key = it.key()
+
+    def read_block(self, block_idx: int) -> Block:
+        """table.rs:154-164 (served from the batch decoded at open)."""
+        if not 0 <= block_idx < len(self.block_metas):
+            raise ReferencePanic("index out of bounds")
+        r = self._blocks[block_idx]
+        if isinstance(r, Exception):
+            raise r
+        return r
+
+    def read_block_cached(self, block_idx: int) -> Block:
+        return self.read_block(block_idx)
+
+    def find_block_idx(self, key: bytes) -> int:
+        """table.rs:178-182: partition_point(first_key <= key) - 1, saturating."""
+        return max(bisect.bisect_right([m.first_key for m in self.block_metas], key) - 1, 0)
+
+    def num_of_blocks(self) -> int:
+        return len(self.block_metas)
+
+
+class SsTableIterator:
+    """src/table/iterator.rs:10-96 (StorageIterator: key, value, is_valid, next)."""
+
+    def __init__(self, table: SsTable, idx: int, block_iter: BlockIterator):
+        self.table, self.idx, self.block_iter = table, idx, block_iter
+
+    @staticmethod
+    def _seek_to_first_inner(table: SsTable, idx: int) -> BlockIterator:
+        return BlockIterator.create_and_seek_to_first(table.read_block_cached(idx))
+
+    @classmethod
+    def create_and_seek_to_first(cls, table: SsTable) -> "SsTableIterator":
+        return cls(table, 0, cls._seek_to_first_inner(table, 0))
+
+    def seek_to_first(self) -> None:
+        self.idx = 0
+        self.block_iter = self._seek_to_first_inner(self.table, 0)
+
+    @classmethod
+    def _seek_to_key_inner(cls, table: SsTable, key: bytes):
+        idx = table.find_block_idx(key)
+        block_iter = BlockIterator.create_and_seek_to_key(table.read_block_cached(idx), key)
+        if not block_iter.is_valid() and idx + 1 < table.num_of_blocks():
+            idx += 1
+            block_iter = cls._seek_to_first_inner(table, idx)
+        return idx, block_iter
+
+    @classmethod
+    def create_and_seek_to_key(cls, table: SsTable, key: bytes) -> "SsTableIterator":
+        idx, it = cls._seek_to_key_inner(table, key)
+        return cls(table, idx, it)
+
+    def seek_to_key(self, key: bytes) -> None:
+        self.idx, self.block_iter = self._seek_to_key_inner(self.table, key)
+
+    def key(self) -> bytes:
+        return self.block_iter.key()
+
+    def value(self) -> bytes:
+        return self.block_iter.value()
+
+    def is_valid(self) -> bool:
+        return self.block_iter.is_valid()
+
+    def next(self) -> None:
+        self.block_iter.next()
+        if not self.block_iter.is_valid() and self.idx < self.table.num_of_blocks() - 1:
+            self.idx += 1
+            self.block_iter = self._seek_to_first_inner(self.table, self.idx)
