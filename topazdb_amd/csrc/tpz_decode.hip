@@ -104,13 +104,15 @@ __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
-// 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: one
-// ds_read_b128 at the byte address (gfx950 replays it: 64 LDS cycles, no VALU). Variants: three
-// 8-byte-aligned ds_read_b64 + a one-bit dword select + alignbyte (TPZ_ABL_F64, 9 VALU), two
+// 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: three
+// 8-byte-aligned ds_read_b64 + a one-bit dword select + alignbyte (9 VALU). Diagnostic variants:
+// one ds_read_b128 at the byte address (TPZ_ABL_U128; gfx950 replays it: 64 LDS cycles), two
 // aligned ds_read_b128 + a two-bit select (TPZ_ABL_FUNNEL, 16 VALU).
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
+#if defined(TPZ_ABL_U128) || defined(TPZ_ABL_FUNNEL)
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-#if !defined(TPZ_ABL_F64) && !defined(TPZ_ABL_FUNNEL)
+#endif
+#if defined(TPZ_ABL_U128)
   typedef u32x4 u32x4_u __attribute__((aligned(1)));
   const u32x4 v = *reinterpret_cast<const u32x4_u*>(base + x);
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -130,7 +132,8 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
   const u32 w4 = q < 2 ? (q == 0 ? b.x : b.y) : (q == 2 ? b.z : b.w);
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
                     __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
-#else  // TPZ_ABL_F64
+#else  // default: three 8-byte-aligned ds_read_b64 (2 LDS cycles each instead of a 64-cycle
+       // unaligned ds_read_b128 replay) + a one-bit dword select + alignbyte
   typedef u32 u32x2 __attribute__((ext_vector_type(2)));
   const u32x2* p = reinterpret_cast<const u32x2*>(base + (x & ~7));
   u32x2 a = p[0], b = p[1], c = p[2];
@@ -198,6 +201,26 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
   return make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
 }
 
+// Combine the lanes' run CRCs (lane l's run ends 80*l bytes before the end) into R0 of the whole
+// range, as a tree: at level k the lanes l = 2^k (mod 2^(k+1)) shift their value by 80 * 2^k
+// (exec-masked lookups: only those lanes touch LDS, so the random-index bank conflicts shrink
+// with every level) and DPP hands it to lane l - 2^k, which XORs it in. Rows of 16 lanes finish
+// in lanes 0, 16, 32, 48; those are shifted by 1280 / 2560 B and read out.
+__device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
+  const u32 lane = lane_id();
+  if ((lane & 1u) == 1u) A = crc_shift<0>(tab, A);
+  A ^= dpp<kRowShl + 1>(A);
+  if ((lane & 3u) == 2u) A = crc_shift<1>(tab, A);
+  A ^= dpp<kRowShl + 2>(A);
+  if ((lane & 7u) == 4u) A = crc_shift<2>(tab, A);
+  A ^= dpp<kRowShl + 4>(A);
+  if ((lane & 15u) == 8u) A = crc_shift<3>(tab, A);
+  A ^= dpp<kRowShl + 8>(A);
+  if ((lane & 31u) == 16u) A = crc_shift<4>(tab, A);
+  if ((lane & 47u) == 32u) A = crc_shift<5>(tab, A);  // lanes 32 and 48
+  return readlane(A, 0) ^ readlane(A, 16) ^ readlane(A, 32) ^ readlane(A, 48);
+}
+
 // Raw CRC R0 of the LDS bytes [pb, pb + Pa), where pb + Pa is 16-byte aligned: the payload
 // (first four bytes already complemented: init 0xFFFFFFFF folded into the message) followed by
 // the zero bytes that pad it to the 16-byte boundary (the caller compares in that shifted domain).
@@ -227,19 +250,7 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
     }
     A = (r + 1 == S) ? c : (crc_shift<5>(tab, crc_shift<5>(tab, A)) ^ c);
   }
-  // lane l: shift by 80 * l
-  A = (lane & 1u) ? crc_shift<0>(tab, A) : A;
-  A = (lane & 2u) ? crc_shift<1>(tab, A) : A;
-  A = (lane & 4u) ? crc_shift<2>(tab, A) : A;
-  A = (lane & 8u) ? crc_shift<3>(tab, A) : A;
-  A = (lane & 16u) ? crc_shift<4>(tab, A) : A;
-  A = (lane & 32u) ? crc_shift<5>(tab, A) : A;
-  // XOR over the wave
-  A ^= dpp<kRowShr + 1>(A);
-  A ^= dpp<kRowShr + 2>(A);
-  A ^= dpp<kRowShr + 4>(A);
-  A ^= dpp<kRowShr + 8>(A);
-  return readlane(A, 15) ^ readlane(A, 31) ^ readlane(A, 47) ^ readlane(A, 63);
+  return crc_combine(tab, A);
 }
 
 // ------------------------------------------------------------------ entry tables
@@ -407,6 +418,67 @@ struct Src16 {
 //      segments (entries shorter than 16 B) take a loop. The key/value gap is such a crossing:
 //      its bytes are unspecified.
 //   4. store; pad chunks up to the 128-byte line are zeroed.
+// One window of the copy (chunks 64 w .. 64 w + 63); returns the carry for the next window.
+template <class Col, class MapT, class S>
+__device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const MapT* map, u32 nk,
+                                           u32 nch, u32 npad, uint8_t* dst, u32 map_len, u32 w,
+                                           u32 carry) {
+  const u32 lane = lane_id();
+  const u32 last = nk ? nk - 1 : 0u;
+  const u32 c = 64 * w + lane;
+  const u32 x0 = 16 * c;
+  const bool act = c < nch;
+  // 1. chunk -> entry: prefix max of the map, carried across the column's windows
+  u32 j = map[min(c, map_len - 1)];
+  j = max(wave_scan_max(act ? j : 0u), carry);
+  const u32 carry_out = readlane(j, 63);
+  // 2. entries j and j + 1 (one ds_read2_b32)
+  u32 e0, e1;
+  int d0, d1;
+  col.get2(min(j, last), e0, d0, e1, d1);
+  // 3. the chunk's bytes; a chunk crossing entry j's end also reads entry j+1's bytes
+  //    (exec-masked). Reads are issued before the rare-case checks so they overlap.
+  uint4 acc = src(act ? (int)x0 + d0 : 0);
+  bool cross = act && j + 1 < nk && e0 < x0 + 16;
+  uint4 nx = make_uint4(0, 0, 0, 0);
+  if (cross) nx = src((int)x0 + d1);
+  if (__ballot(act && e0 <= x0)) {
+    // a lost map race (two entries ended in one chunk): walk forward to the holding entry
+    while (act && e0 <= x0) {
+      j++;
+      col.get2(min(j, last), e0, d0, e1, d1);
+    }
+    acc = src(act ? (int)x0 + d0 : 0);
+    cross = act && j + 1 < nk && e0 < x0 + 16;
+    if (cross) nx = src((int)x0 + d1);
+  }
+  if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
+  // chunks spanning three or more entries (entries shorter than 16 B)
+  if (__ballot(cross && e1 < x0 + 16 && j + 2 < nk)) {
+    u32 k = j + 1, end = e1;
+    while (cross && end < x0 + 16 && k + 1 < nk) {
+      const int lo = (int)(end - x0);
+      k++;
+      int delta;
+      col.get(k, end, delta);
+      const int hi = min((int)(end - x0), 16);
+      const uint4 v = src((int)x0 + delta);
+      acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
+      acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
+      acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
+      acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
+    }
+  }
+  // 4. store (pad chunks up to the 128-byte line are zeroed)
+  const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
+#ifdef TPZ_ABL_NOSTORE
+  asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+#else
+  if (c < npad) *reinterpret_cast<uint4*>(dst + x0) = v;
+#endif
+  return carry_out;
+}
+
 template <class Col, class MapT, class S>
 __device__ __forceinline__ void copy_stream(const S& src, const Col& col, const MapT* map, u32 nk,
                                             u32 tot, uint8_t* dst, u32 map_len) {
@@ -414,65 +486,103 @@ __device__ __forceinline__ void copy_stream(const S& src, const Col& col, const 
   const u32 nch = (tot + 15) >> 4;
   const u32 npad = (nch + 7) & ~7u;                   // whole 128-byte lines
   const u32 nw = (npad + 63) >> 6;
-  const u32 last = nk ? nk - 1 : 0u;
 #ifdef TPZ_ABL_MEMONLY
   for (u32 c = lane; c < npad; c += 64) *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(c, 0, 0, 0);
   return;
 #endif
   u32 carry = 0;
-  for (u32 w = 0; w < nw; w++) {
-    const u32 c = 64 * w + lane;
-    const u32 x0 = 16 * c;
-    const bool act = c < nch;
-    // 1. chunk -> entry: prefix max of the map, carried across the column's windows
-    u32 j = map[min(c, map_len - 1)];
-    j = max(wave_scan_max(act ? j : 0u), carry);
-    carry = readlane(j, 63);
-    // 2. entries j and j + 1 (one ds_read2_b32)
-    u32 e0, e1;
-    int d0, d1;
-    col.get2(min(j, last), e0, d0, e1, d1);
-    // 3. the chunk's bytes; a chunk crossing entry j's end also reads entry j+1's bytes
-    //    (exec-masked). Reads are issued before the rare-case checks so they overlap.
-    uint4 acc = src(act ? (int)x0 + d0 : 0);
-    bool cross = act && j + 1 < nk && e0 < x0 + 16;
-    uint4 nx = make_uint4(0, 0, 0, 0);
-    if (cross) nx = src((int)x0 + d1);
-    if (__ballot(act && e0 <= x0)) {
-      // a lost map race (two entries ended in one chunk): walk forward to the holding entry
-      while (act && e0 <= x0) {
-        j++;
-        col.get2(min(j, last), e0, d0, e1, d1);
-      }
-      acc = src(act ? (int)x0 + d0 : 0);
-      cross = act && j + 1 < nk && e0 < x0 + 16;
-      if (cross) nx = src((int)x0 + d1);
-    }
-    if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
-    // chunks spanning three or more entries (entries shorter than 16 B)
-    if (__ballot(cross && e1 < x0 + 16 && j + 2 < nk)) {
-      u32 k = j + 1, end = e1;
-      while (cross && end < x0 + 16 && k + 1 < nk) {
-        const int lo = (int)(end - x0);
-        k++;
-        int delta;
-        col.get(k, end, delta);
-        const int hi = min((int)(end - x0), 16);
-        const uint4 v = src((int)x0 + delta);
-        acc.x = (acc.x & ~byte_mask(lo, hi, 0)) | (v.x & byte_mask(lo, hi, 0));
-        acc.y = (acc.y & ~byte_mask(lo, hi, 1)) | (v.y & byte_mask(lo, hi, 1));
-        acc.z = (acc.z & ~byte_mask(lo, hi, 2)) | (v.z & byte_mask(lo, hi, 2));
-        acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
-      }
-    }
-    // 4. store (pad chunks up to the 128-byte line are zeroed)
-    const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
-#ifdef TPZ_ABL_NOSTORE
-    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-#else
-    if (c < npad) *reinterpret_cast<uint4*>(dst + x0) = v;
-#endif
+  for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, nch, npad, dst, map_len, w, carry);
+}
+
+// ------------------------------------------------------------------ fused copy + CRC (wave path)
+// A wave-path block has at most 5 copy windows (stream <= len + 2 <= 4338 B) and its CRC at most
+// five 80-byte slice-by-16 steps per lane (P + k <= 4351 B). The copy's LDS round trips (map ->
+// scan -> entry table -> source) and the CRC's lookups are independent chains: here step t of
+// both runs in one straight-line block, so each hides the other's LDS latency. The copy takes only
+// its common path (one entry per chunk, or a crossing into the next entry): branch-free reads (an
+// idle lane reads the zeroed guard), the stores through a descriptor that ends at the slot's last
+// line (no exec masking). A window where any lane needs the rare path (a lost map race, a chunk
+// spanning 3+ entries) is recorded and rewritten afterwards by copy_window.
+struct CrcLane {
+  int seg;      // the lane's run [seg, seg + 80) relative to the payload start (end-aligned)
+  bool act;     // the run overlaps the payload
+  u32 c;        // the run's raw CRC so far
+};
+
+__device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
+                                         int t) {
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+  const int a = L.act ? pb + L.seg + 16 * t : -kGuard;  // 16-byte aligned either way
+  const u32x4 w = *reinterpret_cast<const u32x4*>(win + a);
+  L.c = slice16(tab, w.x ^ L.c, w.y, w.z, w.w);
+}
+
+struct FastWin {
+  u32 nk, nch, npad, last;
+  __amdgpu_buffer_rsrc_t out;  // the slot, npad * 16 bytes
+};
+
+// The common path of copy_window, branch-free; returns the carry, sets bit w of `rare` when any
+// lane of the window needs copy_window's rare path.
+template <class S>
+__device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, const uint16_t* map,
+                                         const FastWin& F, u32 w, u32 carry, u32& rare) {
+  const u32 lane = lane_id();
+  const u32 c = 64 * w + lane;
+  const u32 x0 = 16 * c;
+  const bool act = c < F.nch;
+  u32 j = map[min(c, (u32)kWaveMapLen - 1)];
+  j = max(wave_scan_max(act ? j : 0u), carry);
+  const u32 carry_out = readlane(j, 63);
+  u32 e0, e1;
+  int d0, d1;
+  col.get2(min(j, F.last), e0, d0, e1, d1);
+  const bool cross = act && j + 1 < F.nk && e0 < x0 + 16;
+  uint4 acc = src(act ? (int)x0 + d0 : -kGuard);
+  const uint4 nx = src(cross ? (int)x0 + d1 : -kGuard);
+  if (__ballot(act && (e0 <= x0 || (cross && e1 < x0 + 16 && j + 2 < F.nk)))) rare |= 1u << w;
+  if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
+  // an idle lane read the zeroed guard: its pad chunk stores zeros without a select
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
+                                         F.out, x0, 0, 0);
+  return carry_out;
+}
+
+// Copy of a wave-path block's stream fused with its CRC: returns R0(payload' || 0^k) as
+// wave_crc does (the caller prepared the window the same way).
+template <class S>
+__device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
+                                              const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
+                                              const uint8_t* win, int pb, u32 Pa) {
+  const u32 lane = lane_id();
+  FastWin F;
+  F.nk = nk;
+  F.nch = (tot + 15) >> 4;
+  F.npad = (F.nch + 7) & ~7u;
+  F.last = nk ? nk - 1 : 0u;
+  F.out = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)(F.npad * 16), 0x00020000);
+  const u32 nw = (F.npad + 63) >> 6;
+  CrcLane L;
+  L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
+  L.act = L.seg + kCrcLaneBytes > 0;
+  L.c = 0;
+  u32 carry = 0, rare = 0, cw[5];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    cw[t] = carry;
+    crc_step(tab, win, pb, L, t);
+    carry = copy_fast(src, col, map, F, (u32)t, carry, rare);
   }
+  cw[4] = carry;
+  crc_step(tab, win, pb, L, 4);
+  if (nw > 4) carry = copy_fast(src, col, map, F, 4u, carry, rare);
+  const u32 R = crc_combine(tab, L.c);
+  if (rare) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rewrite lands after the fast stores
+    for (u32 w = 0; w < nw; w++)
+      if (rare & (1u << w)) copy_window(src, col, map, nk, F.nch, F.npad, dst, (u32)kWaveMapLen, w, cw[w]);
+  }
+  return R;
 }
 
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. `map` is the
@@ -502,6 +612,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   // s_waitcnt on the prefetch loads (loads and stores share vmcnt on gfx950). A block whose CRC
   // turns out wrong reports CHECKSUM_MISMATCH with count 0; its slot holds unspecified bytes.
   u32 st = TPZ_BLOCK_OK, cnt = n;
+  bool fuse = false;           // copy fused with the CRC (wave path)
+  u32 f_nk = 0, f_tot = 0;
+  uint8_t* f_dst = nullptr;
   if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
     st = TPZ_BLOCK_MALFORMED;
     cnt = 0;
@@ -601,6 +714,14 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       }
       __builtin_amdgcn_wave_barrier();
 #ifndef TPZ_ABL_NOCOPY
+#if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY) && !defined(TPZ_ABL_NOFUSE)
+      if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
+        fuse = true;
+        f_nk = knz + vnz;
+        f_tot = vs + vc;
+        f_dst = o.data + slot_base(ext_b, b);
+      } else
+#endif
       copy_stream(Src16{win}, col, map, knz + vnz, vs + vc, o.data + slot_base(ext_b, b),
                   (u32)kMapLen);
 #endif
@@ -622,7 +743,12 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 #if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
     crc = stored;
 #else
-    const u32 R = wave_crc(tab, win, pb, P + k);
+    u32 R;
+    if (!BIG && fuse)
+      R = copy_crc_fused(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb, P + k);
+    else
+      R = wave_crc(tab, win, pb, P + k);
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
 #endif
   } else {
