@@ -13,6 +13,7 @@
  *   tpz_crc32_ranges        checksum::calculate_checksum (src/checksum.rs:6-10) over many ranges
  *   tpz_verify_files        FileObject::open's whole-file CRC (src/table/file_object.rs:57-78),
  *                           batched over SST file images (SsTable::open, src/table.rs:91-112)
+ *   tpz_decompress_blocks   compress::decode's snappy step (src/block/compress.rs:104-107)
  *   tpz_format_block_error  the reference's error strings (checksum.rs:18-21, compress.rs:97,102)
  *
  * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
@@ -57,8 +58,12 @@ typedef enum {
                                       6*n > len or value_start(K) + V > len + 2 (K, V = the
                                       block's key and value bytes).
                                       topazdb's BlockBuilder never writes such a block.      */
-  TPZ_BLOCK_TOO_LARGE = 7          /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
-                                      block_size <= 64 KiB BlockBuilder emits)               */
+  TPZ_BLOCK_TOO_LARGE = 7,         /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
+                                      block_size <= 64 KiB BlockBuilder emits); for a snappy
+                                      block: compressed > 64 KiB - 24 or uncompressed >
+                                      TPZ_MAX_BLOCK_BYTES - 1                                */
+  TPZ_BLOCK_CODEC_ERROR = 8        /* Err of the codec: snap's decompress_vec rejects the
+                                      stream (compress.rs:104-107)                           */
 } tpz_block_status;
 
 #define TPZ_MAX_BLOCK_BYTES 94192u
@@ -163,6 +168,26 @@ tpz_err tpz_crc32_ranges(tpz_ctx* ctx, const tpz_batch* ranges, uint32_t* d_crc,
  * `buf[size - CHECKSUM_SIZE..]` panics). Asynchronous on `stream`. */
 tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
                          uint8_t* d_status, void* stream);
+
+/* ---- codec step of compress::decode (src/block/compress.rs:95-113) ------------------------
+ * Snappy (tag 2) blocks are decompressed on the device into their Uncompress (tag 1) form, so
+ * tpz_decode_blocks then verifies and decodes them like any block:
+ *   1. tpz_decompressed_sizes: d_size[i] = the length block i has once decompressed and
+ *      re-tagged: the snappy preamble's length + 1 for a tag 2 block (0 if the preamble is
+ *      invalid, 1 if the length exceeds TPZ_MAX_BLOCK_BYTES - 1), the block's own length for
+ *      any other block.
+ *   2. the caller forms d_dst_ext = exclusive prefix sums of d_size (n_blocks + 1 entries) and
+ *      allocates d_dst (d_dst_ext[n] bytes).
+ *   3. tpz_decompress_blocks writes block i's uncompressed form to d_dst[d_dst_ext[i] ..
+ *      d_dst_ext[i+1]) (other tags are copied unchanged) and d_status[i] = TPZ_BLOCK_OK,
+ *      TPZ_BLOCK_CODEC_ERROR (snap's Err) or TPZ_BLOCK_TOO_LARGE. A failed block's range ends in
+ *      tag 0, so decoding it reports BAD_TAG; its d_status is the reference's outcome.
+ *   4. tpz_decode_blocks over (d_dst, d_dst_ext).
+ * LZ4 (tag 3) blocks are copied unchanged for now (the decode reports UNSUPPORTED_CODEC). */
+tpz_err tpz_decompressed_sizes(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_size,
+                               void* stream);
+tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_dst,
+                              const uint64_t* d_dst_ext, uint8_t* d_status, void* stream);
 
 /* ---- host write side (inputs for benches and the table facade) ---------------------------
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule

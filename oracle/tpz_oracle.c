@@ -124,13 +124,35 @@ typedef struct {
   size_t data_len;
 } blockview;
 
-/* compress::decode (src/block/compress.rs:95-113) + Block::decode (src/block.rs:46-65). */
+/* compress::decode's codec step (src/block/compress.rs:95-113) for snappy (tag 2): the block's
+ * Uncompress form (payload | crc | 1) in *buf (malloc'd, caller frees) and its length; the
+ * block itself for any other tag. Returns 0, or TPZO_CODEC where snap returns Err. */
+static int codec_step(const uint8_t* b, size_t len, uint8_t** buf, const uint8_t** out,
+                      size_t* out_len) {
+  *buf = NULL;
+  *out = b;
+  *out_len = len;
+  if (len == 0 || b[len - 1] != 2) return 0;
+  uint64_t want = 0;
+  if (tpzo_snappy_uncompressed_len(b, len - 1, &want) != 0) return TPZO_CODEC;
+  if (want + 1 > 94192) return TPZO_TOO_LARGE; /* the device's limit (TPZ_MAX_BLOCK_BYTES) */
+  *buf = (uint8_t*)malloc(want + 1);
+  uint64_t got = 0;
+  if (tpzo_snappy_decompress(b, len - 1, *buf, want, &got) != 0) return TPZO_CODEC;
+  (*buf)[got] = 1;
+  *out = *buf;
+  *out_len = got + 1;
+  return 0;
+}
+
+/* compress::decode (src/block/compress.rs:95-113) + Block::decode (src/block.rs:46-65), on a
+ * block whose codec step is done (tag 2 has become tag 1). */
 static void block_decode(const uint8_t* b, size_t len, blockview* v) {
   memset(v, 0, sizeof(*v));
   if (len == 0) { v->status = TPZO_EMPTY; return; }             /* compress.rs:96-98 */
   uint8_t tag = b[len - 1];                                      /* compress.rs:99 */
   if (tag == 0 || tag > 3) { v->status = TPZO_BAD_TAG; return; } /* compress.rs:44-53,102 */
-  if (tag != 1) { v->status = TPZO_UNSUPPORTED; return; }        /* snappy / lz4 */
+  if (tag != 1) { v->status = TPZO_UNSUPPORTED; return; }        /* lz4 */
   size_t dlen = len - 1;                                         /* compress.rs:100,103 */
   if (dlen < 4) { v->status = TPZO_MALFORMED; return; }          /* block.rs:49 split_to */
   size_t plen = dlen - 4;
@@ -186,9 +208,15 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
   uint64_t ne = 0, kb = 0, vb = 0;
   for (uint32_t i = 0; i < n_blocks; i++) {
     blockview v;
-    uint64_t kt, vt;
-    block_full(src + ext[i], ext[i + 1] - ext[i], &v, &kt, &vt);
-    if (v.status == TPZO_OK || v.status == TPZO_OVERLAP) { ne += v.n; kb += kt; vb += vt; }
+    uint64_t kt = 0, vt = 0;
+    uint8_t* buf;
+    const uint8_t* blk;
+    size_t blen;
+    if (codec_step(src + ext[i], ext[i + 1] - ext[i], &buf, &blk, &blen) == 0) {
+      block_full(blk, blen, &v, &kt, &vt);
+      if (v.status == TPZO_OK || v.status == TPZO_OVERLAP) { ne += v.n; kb += kt; vb += vt; }
+    }
+    free(buf);
   }
   *n_entries = ne;
   *key_bytes = kb;
@@ -203,12 +231,21 @@ int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
   for (uint32_t i = 0; i < n_blocks; i++) {
     blockview v;
     uint64_t kt, vt;
-    block_full(src + ext[i], ext[i + 1] - ext[i], &v, &kt, &vt);
+    uint8_t* buf;
+    const uint8_t* blk;
+    size_t blen;
+    const int cs = codec_step(src + ext[i], ext[i + 1] - ext[i], &buf, &blk, &blen);
+    if (cs) {
+      memset(&v, 0, sizeof v);
+      v.status = cs;
+    } else {
+      block_full(blk, blen, &v, &kt, &vt);
+    }
     status[i] = (uint8_t)v.status;
     crc_actual[i] = v.crc_actual;
     crc_expected[i] = v.crc_expected;
     count[i] = 0;
-    if (v.status != TPZO_OK && v.status != TPZO_OVERLAP) continue;
+    if (v.status != TPZO_OK && v.status != TPZO_OVERLAP) { free(buf); continue; }
     count[i] = v.n;
     for (uint32_t j = 0; j < v.n; j++, e++) {
       const uint8_t *k, *val;
@@ -221,6 +258,7 @@ int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
       kp += kl;
       vp += vl;
     }
+    free(buf);
   }
   return 0;
 }
@@ -268,6 +306,7 @@ struct tpzo_sst_iter {
   uint32_t idx;
   /* BlockIterator (block/iterator.rs:9-14) over the current block */
   blockview blk;
+  uint8_t* blkbuf; /* the current block's Uncompress form when it was snappy */
   uint32_t bidx;
   uint8_t *key, *val;
   size_t kl, vl, kcap, vcap;
@@ -314,7 +353,15 @@ static void biter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen
 
 /* SsTable::read_block (table.rs:154-164) into the iterator's current block. */
 static int read_block(tpzo_sst_iter* it, uint32_t i) {
-  block_decode(it->file + it->ext[i], it->ext[i + 1] - it->ext[i], &it->blk);
+  free(it->blkbuf);
+  const uint8_t* b;
+  size_t len;
+  if (codec_step(it->file + it->ext[i], it->ext[i + 1] - it->ext[i], &it->blkbuf, &b, &len)) {
+    memset(&it->blk, 0, sizeof it->blk);
+    it->blk.status = TPZO_CODEC;
+    return -1;
+  }
+  block_decode(b, len, &it->blk);
   return it->blk.status == TPZO_OK ? 0 : -1;
 }
 
@@ -345,6 +392,7 @@ void tpzo_sst_iter_destroy(tpzo_sst_iter* it) {
   free(it->mk_len);
   free(it->key);
   free(it->val);
+  free(it->blkbuf);
   free(it);
 }
 

@@ -27,10 +27,12 @@ enum {
   TPZO_OK = 0,          /* Block::decode Ok                                   */
   TPZO_EMPTY = 1,       /* Err("data is empty")      src/block/compress.rs:96-98 */
   TPZO_BAD_TAG = 2,     /* Err("invaild data")       src/block/compress.rs:102   */
-  TPZO_UNSUPPORTED = 3, /* tag 2/3: snappy / lz4     src/block/compress.rs:104-111 */
+  TPZO_UNSUPPORTED = 3, /* tag 3: lz4                src/block/compress.rs:108-111 */
   TPZO_CHECKSUM = 4,    /* Err("checksum: ...")      src/checksum.rs:12-21       */
   TPZO_MALFORMED = 5,   /* the reference panics      src/block.rs:49-59, iterator.rs:74-82 */
-  TPZO_OVERLAP = 6      /* decodes in the reference; exceeds the device's per-block slot */
+  TPZO_OVERLAP = 6,     /* decodes in the reference; exceeds the device's per-block slot */
+  TPZO_TOO_LARGE = 7,   /* a snappy block decompressing past the device limit (94192 B) */
+  TPZO_CODEC = 8        /* snap's decompress_vec returns Err  src/block/compress.rs:104-107 */
 };
 
 /* CRC-32/ISO-HDLC bit by bit (crc32fast's function): src/checksum.rs:6-10. */
@@ -43,8 +45,9 @@ uint32_t tpzo_crc32_fast(const uint8_t* p, size_t n);
 void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint64_t* n_entries, uint64_t* key_bytes, uint64_t* val_bytes);
 
-/* Block::decode (src/block.rs:46-65) + BlockIterator::seek_to for every index
- * (src/block/iterator.rs:63-83) over blocks [ext[i], ext[i+1]). Dense outputs in block order:
+/* Block::decode (src/block.rs:46-65, snappy blocks decompressed first as compress.rs:104-107)
+ * + BlockIterator::seek_to for every index (src/block/iterator.rs:63-83) over blocks
+ * [ext[i], ext[i+1]). Dense outputs in block order:
  * entries are emitted for TPZO_OK and TPZO_OVERLAP blocks. crc_actual is the CRC the reference
  * computes over the payload (0 when it never gets that far). Returns 0. */
 int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
@@ -72,6 +75,15 @@ int tpzo_sst_iter_is_valid(const tpzo_sst_iter* it);                     /* :84-
 const uint8_t* tpzo_sst_iter_key(const tpzo_sst_iter* it, size_t* len);
 const uint8_t* tpzo_sst_iter_value(const tpzo_sst_iter* it, size_t* len);
 uint32_t tpzo_sst_iter_block_idx(const tpzo_sst_iter* it);
+
+/* ---- snappy raw format (tpz_snappy.c; codec 2, src/block/compress.rs:66-71, 104-107) ------
+ * decompress: 0 and *out_len on success, -1 where snap's decoder returns Err.
+ * compress: a valid stream for fixtures (dst >= 64 + 2n); mode 0 = copy-1/copy-2,
+ * 1 = copy-2 only, 2 = copy-4 only, 3 = literals only. */
+int tpzo_snappy_uncompressed_len(const uint8_t* src, size_t n, uint64_t* len);
+int tpzo_snappy_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
+                           uint64_t* out_len);
+size_t tpzo_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst, int mode);
 
 /* ---- CPU baseline: benches/sstable_iter_read.rs:60-79 restated --------------------------
  * SsTableIterator::create_and_seek_to_first + `while is_valid { next }` over SST files on

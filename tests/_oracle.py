@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 
-OK, EMPTY, BAD_TAG, UNSUPPORTED, CHECKSUM, MALFORMED, OVERLAP = range(7)
+OK, EMPTY, BAD_TAG, UNSUPPORTED, CHECKSUM, MALFORMED, OVERLAP, TOO_LARGE, CODEC = range(9)
 
 _lib = None
 
@@ -45,6 +45,10 @@ def lib() -> C.CDLL:
         L.tpzo_sst_iter_key.restype = C.c_void_p
         L.tpzo_sst_iter_value.argtypes = [C.c_void_p, C.POINTER(C.c_size_t)]
         L.tpzo_sst_iter_value.restype = C.c_void_p
+        L.tpzo_snappy_uncompressed_len.argtypes = [C.c_void_p, C.c_size_t, u64p]
+        L.tpzo_snappy_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, u64p]
+        L.tpzo_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
+        L.tpzo_snappy_compress.restype = C.c_size_t
         L.tpzo_bench_iter_read.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
                                            C.c_uint32, u64p, u64p]
         L.tpzo_bench_iter_read.restype = C.c_double
@@ -163,3 +167,44 @@ def bench_iter_read(paths: list[str], threads: int, iters: int):
     if dt < 0:
         raise RuntimeError("tpzo_bench_iter_read failed")
     return dt, by.value, en.value
+
+
+# ---- snappy (oracle/tpz_snappy.c) ---------------------------------------------------------
+def snappy_compress(b: bytes, mode: int = 0) -> bytes:
+    src = np.frombuffer(b, np.uint8) if b else np.zeros(1, np.uint8)
+    dst = np.zeros(64 + 2 * len(b), np.uint8)  # copy-4 elements expand 4 bytes to 5
+    n = lib().tpzo_snappy_compress(_ptr(src), len(b), _ptr(dst), mode)
+    return dst[:n].tobytes()
+
+
+def snappy_decompress(b: bytes):
+    """The decompressed bytes, or None where snap's decoder returns Err."""
+    src = np.frombuffer(b, np.uint8) if b else np.zeros(1, np.uint8)
+    want = C.c_uint64()
+    if lib().tpzo_snappy_uncompressed_len(_ptr(src), len(b), C.byref(want)) != 0:
+        return None
+    if want.value > (1 << 28):
+        return None  # fixture-sized oracle
+    dst = np.zeros(max(want.value, 1), np.uint8)
+    out = C.c_uint64()
+    if lib().tpzo_snappy_decompress(_ptr(src), len(b), _ptr(dst), want.value, C.byref(out)) != 0:
+        return None
+    return dst[:out.value].tobytes()
+
+
+def snappy_block(tag1_block: bytes, mode: int = 0) -> bytes:
+    """compress::encode with CompressOptions::Snappy (src/block/compress.rs:66-71) applied to
+    the bytes an Uncompress block holds before its tag (payload | crc)."""
+    assert tag1_block[-1] == 1
+    return snappy_compress(tag1_block[:-1], mode) + b"\x02"
+
+
+def decompress_block(blk: bytes):
+    """compress::decode's codec step (src/block/compress.rs:95-113) for tag 2, re-tagged as an
+    Uncompress block: (status, bytes). Other tags pass through unchanged with status OK."""
+    if len(blk) == 0 or blk[-1] != 2:
+        return OK, blk
+    d = snappy_decompress(blk[:-1])
+    if d is None:
+        return CODEC, b""
+    return OK, d + b"\x01"

@@ -83,10 +83,120 @@ def block_payload(offsets: list[int], data: bytes) -> bytes:
     return bytes(out)
 
 
+# --------------------------------------------------------------------------- snappy raw format
+# The reference's codec 2 calls the `snap` crate (compress.rs:66-71, 104-107). Restated from the
+# published format description, independently of oracle/tpz_snappy.c.
+def snappy_decompress(b: bytes):
+    """snap::raw::Decoder::decompress_vec: the bytes, or None where it returns Err."""
+    want, shift, i = 0, 0, 0
+    while True:                                            # varint preamble
+        if i >= len(b) or i >= 10:
+            return None
+        want |= (b[i] & 0x7F) << shift
+        shift += 7
+        i += 1
+        if not b[i - 1] & 0x80:
+            break
+    if want > 0xFFFFFFFF:
+        return None
+    out = bytearray()
+    while i < len(b):
+        tag = b[i]
+        i += 1
+        kind = tag & 3
+        if kind == 0:                                      # literal
+            n = (tag >> 2) + 1
+            if tag >> 2 >= 60:
+                nb = (tag >> 2) - 59
+                if i + nb > len(b):
+                    return None
+                n = int.from_bytes(b[i:i + nb], "little") + 1
+                i += nb
+            if i + n > len(b) or len(out) + n > want:
+                return None
+            out += b[i:i + n]
+            i += n
+            continue
+        if kind == 1:
+            if i + 1 > len(b):
+                return None
+            n, off = 4 + ((tag >> 2) & 7), ((tag >> 5) << 8) | b[i]
+            i += 1
+        elif kind == 2:
+            if i + 2 > len(b):
+                return None
+            n, off = 1 + (tag >> 2), int.from_bytes(b[i:i + 2], "little")
+            i += 2
+        else:
+            if i + 4 > len(b):
+                return None
+            n, off = 1 + (tag >> 2), int.from_bytes(b[i:i + 4], "little")
+            i += 4
+        if off == 0 or off > len(out) or len(out) + n > want:
+            return None
+        for _ in range(n):                                  # overlapping copies repeat
+            out.append(out[-off])
+    return bytes(out) if len(out) == want else None
+
+
+def snappy_compress(b: bytes) -> bytes:
+    """A valid snappy stream for b (greedy matches on 4-byte substrings, copy-1 when it fits)."""
+    out = bytearray()
+    v = len(b)
+    while True:
+        out.append((v & 0x7F) | (0x80 if v > 0x7F else 0))
+        v >>= 7
+        if not v:
+            break
+
+    def literal(lo, hi):
+        n = hi - lo
+        if n <= 0:
+            return
+        if n - 1 < 60:
+            out.append((n - 1) << 2)
+        else:
+            nb = (n - 1).bit_length() + 7 >> 3
+            out.append((59 + nb) << 2)
+            out.extend((n - 1).to_bytes(nb, "little"))
+        out.extend(b[lo:hi])
+
+    last, i, seen = 0, 0, {}
+    while i + 4 <= len(b):
+        k = b[i:i + 4]
+        c = seen.get(k)
+        seen[k] = i
+        if c is None or i - c >= 65536:
+            i += 1
+            continue
+        m = 4
+        while i + m < len(b) and b[c + m] == b[i + m]:
+            m += 1
+        literal(last, i)
+        off, rem = i - c, m
+        while rem:
+            n = min(rem, 64)
+            if rem > 64 and rem - 64 < 4:
+                n = 60
+            if 4 <= n <= 11 and off < 2048:
+                out += bytes([1 | (n - 4) << 2 | (off >> 8) << 5, off & 0xFF])
+            else:
+                out += bytes([2 | (n - 1) << 2]) + off.to_bytes(2, "little")
+            rem -= n
+        i += m
+        last = i
+    literal(last, len(b))
+    return bytes(out)
+
+
 def encode_block(offsets: list[int], data: bytes, tag: int = TAG_NONE) -> bytes:
-    """Block::encode (src/block.rs:31-44) with the Uncompress codec (compress.rs:85-89)."""
+    """Block::encode (src/block.rs:31-44) with the Uncompress (compress.rs:85-89) or Snappy
+    (compress.rs:66-71) codec."""
     p = block_payload(offsets, data)
-    return p + struct.pack(">I", crc32(p)) + bytes([tag])
+    body = p + struct.pack(">I", crc32(p))
+    if tag == TAG_SNAPPY:
+        return snappy_compress(body) + bytes([TAG_SNAPPY])
+    return body + bytes([tag])
 
 
 def bloom_from_keys(hashes: list[int], fpp: float) -> bytes:
@@ -169,6 +279,7 @@ class SsTableBuilder:
 
 # --------------------------------------------------------------------------- read side
 ST_OK, ST_EMPTY, ST_BAD_TAG, ST_UNSUPPORTED, ST_CHECKSUM, ST_MALFORMED, ST_OVERLAP = range(7)
+ST_CODEC = 8
 
 
 def decode_block(blk: bytes) -> dict:
@@ -183,10 +294,16 @@ def decode_block(blk: bytes) -> dict:
     if tag not in (1, 2, 3):
         r["status"] = ST_BAD_TAG                           # compress.rs:102
         return r
-    if tag != TAG_NONE:
+    if tag == TAG_SNAPPY:                                  # compress.rs:104-107
+        data = snappy_decompress(blk[:-1])
+        if data is None:
+            r["status"] = ST_CODEC
+            return r
+    elif tag != TAG_NONE:
         r["status"] = ST_UNSUPPORTED
         return r
-    data = blk[:-1]
+    else:
+        data = blk[:-1]
     if len(data) < 4:                                      # block.rs:49 split_to underflow panics
         r["status"] = ST_MALFORMED
         return r
@@ -226,7 +343,8 @@ def decode_block(blk: bytes) -> dict:
         # Device slot contract (include/tpz_gpu.h): the block's decoded stream (keys, values
         # from the next 16-byte boundary) must fit its slot (len + 2 bytes). Only blocks whose offsets overlap can break it; topazdb's writer
         # never emits them, the reference iterator decodes them, the device reports OVERLAP.
-        if n * 6 > len(blk) or (ktot + 15) // 16 * 16 + vtot > len(blk) + 2:
+        blen = len(data) + 1                                # the Uncompress form the device decodes
+        if n * 6 > blen or (ktot + 15) // 16 * 16 + vtot > blen + 2:
             r["status"] = ST_OVERLAP
     return r
 
@@ -457,7 +575,43 @@ def main() -> None:
     with open(os.path.join(HERE, "blocks_edge.json"), "w") as fj:
         json.dump({"ext": ext, "blocks": out}, fj, indent=0)
 
-    # 9. CRC known answers (pins crc32fast == CRC-32/ISO-HDLC; src/checksum.rs:27-33 string).
+    # 9. Snappy (codec 2, compress.rs:66-71, 104-107): SSTs with snappy blocks, and known
+    #    answers for hand-built streams of every element kind (format description) and for the
+    #    streams snap's decoder rejects.
+    sst_fixture("sst_snappy_bench", SsTableBuilder(4096, tag=TAG_SNAPPY),
+                [(key_of(i), value_of(i)) for i in range(1000)])
+    g = splitmix64(0x5EED0004)
+    kv = [(struct.pack(">Q", i) + rand_bytes(g, 8), rand_bytes(g, 100)) for i in range(34 * 6)]
+    sst_fixture("sst_snappy_4k", SsTableBuilder(4096, tag=TAG_SNAPPY), kv)
+    lit = lambda n: bytes([(n - 1) << 2])                   # literal tag, n <= 60
+    kat = [
+        ("literal", b"\x03" + lit(3) + b"abc", b"abc"),
+        ("copy1_overlap", b"\x09" + lit(3) + b"abc" + bytes([1 | (6 - 4) << 2, 3]), b"abcabcabc"),
+        ("copy1_run", b"\x0c" + lit(1) + b"z" + bytes([1 | (11 - 4) << 2, 1]), b"z" * 12),
+        ("copy2", b"\x0a" + lit(5) + b"hello" + bytes([2 | (5 - 1) << 2, 5, 0]), b"hellohello"),
+        ("copy4", b"\x08" + lit(4) + b"wxyz" + bytes([3 | (4 - 1) << 2, 4, 0, 0, 0]), b"wxyzwxyz"),
+        ("literal_ext1", b"\x40" + bytes([60 << 2, 63]) + bytes(range(64)), bytes(range(64))),
+        ("literal_ext2", b"\x80\x02" + bytes([61 << 2, 0xFF, 0]) + bytes(256), bytes(256)),
+        ("empty", b"\x00", b""),
+        ("varint_2byte", b"\x81\x01" + lit(60) + bytes(60) + bytes([2 | 63 << 2, 60, 0])
+         + bytes([2 | 4 << 2, 1, 0]), bytes(129)),
+        ("err_no_header", b"", None),
+        ("err_truncated_varint", b"\x80", None),
+        ("err_offset_zero", b"\x06" + lit(2) + b"ab" + bytes([1, 0]), None),
+        ("err_offset_past", b"\x06" + lit(2) + b"ab" + bytes([1, 3]), None),
+        ("err_literal_past_input", b"\x05" + lit(5) + b"abc", None),
+        ("err_over_length", b"\x02" + lit(3) + b"abc", None),
+        ("err_under_length", b"\x04" + lit(3) + b"abc", None),
+        ("err_truncated_copy2", b"\x06" + lit(2) + b"ab" + bytes([2 | 3 << 2, 1]), None),
+        ("err_truncated_copy4", b"\x06" + lit(2) + b"ab" + bytes([3 | 3 << 2, 1, 0, 0]), None),
+    ]
+    for name, stream, want in kat:
+        assert snappy_decompress(stream) == want, name
+    with open(os.path.join(HERE, "snappy_kat.json"), "w") as fj:
+        json.dump([{"name": n, "stream": st.hex(), "out": None if w is None else w.hex()}
+                   for n, st, w in kat], fj, indent=0)
+
+    # 10. CRC known answers (pins crc32fast == CRC-32/ISO-HDLC; src/checksum.rs:27-33 string).
     kat = {s.hex(): crc32(s) for s in [b"", b"a", b"123456789", b"12312nskjdhsdi9823r1y3r9",
                                         bytes(range(256)) * 5, b"\x00" * 4150, b"\xff" * 17]}
     with open(os.path.join(HERE, "crc_kat.json"), "w") as fj:

@@ -13,7 +13,7 @@ import torch
 import _oracle as O
 from conftest import GOLDEN, read_golden
 from topazdb_amd import _lib, synth
-from topazdb_amd.batch import DeviceBatch, decode_batch
+from topazdb_amd.batch import DeviceBatch, decode_batch, decompress_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -33,10 +33,22 @@ def ctx():
 
 
 def gpu_decode(ctx, src, ext):
-    b = DeviceBatch(np.ascontiguousarray(src, np.uint8), np.asarray(ext, np.uint64))
+    """The device path of Block::decode for a batch: the codec step for snappy blocks
+    (tpz_decompress_blocks), then tpz_decode_blocks; a failed codec step's status wins."""
+    src = np.ascontiguousarray(src, np.uint8)
+    ext = np.asarray(ext, np.uint64)
+    b = DeviceBatch(src, ext)
+    codec = None
+    if any(ext[i + 1] > ext[i] and src[int(ext[i + 1]) - 1] == 2 for i in range(len(ext) - 1)):
+        b, st = decompress_batch(ctx, b)
+        codec = st[:len(ext) - 1].cpu().numpy()
     cols = decode_batch(ctx, b)
     torch.cuda.synchronize()
-    return cols, cols.dense(b.ext_host)
+    g = cols.dense(b.ext_host)
+    if codec is not None:
+        bad = codec != _lib.BLOCK_OK
+        g.status = np.where(bad, codec, g.status).astype(np.uint8)
+    return cols, g
 
 
 def assert_parity(ctx, src, ext, expect_all_ok=False):
@@ -76,7 +88,7 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
 
 
 SSTS = ["sst_100_b128", "sst_b16", "sst_bloom3", "sst_bench_1000", "sst_4k_k16_v100",
-        "sst_zipf", "sst_64k_k32_v1k"]
+        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k"]
 
 
 @pytest.mark.parametrize("name", SSTS)

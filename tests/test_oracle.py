@@ -116,7 +116,7 @@ def test_block_iterator_sequence():
 
 # ---------------------------------------------------------------- SST fixtures
 SSTS = ["sst_100_b128", "sst_b16", "sst_bloom3", "sst_bench_1000", "sst_4k_k16_v100",
-        "sst_zipf", "sst_64k_k32_v1k"]
+        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k"]
 
 
 @pytest.mark.parametrize("name", SSTS)

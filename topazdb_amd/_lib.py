@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
- BLOCK_MALFORMED, BLOCK_OVERLAP, BLOCK_TOO_LARGE) = range(8)
+ BLOCK_MALFORMED, BLOCK_OVERLAP, BLOCK_TOO_LARGE, BLOCK_CODEC_ERROR) = range(9)
 MAX_BLOCK_BYTES = 94192
 
 
@@ -72,6 +72,12 @@ def lib() -> C.CDLL:
         L.tpz_verify_files.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
                                        C.c_void_p]
         L.tpz_verify_files.restype = C.c_int
+        L.tpz_decompressed_sizes.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p,
+                                             C.c_void_p]
+        L.tpz_decompressed_sizes.restype = C.c_int
+        L.tpz_decompress_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]
+        L.tpz_decompress_blocks.restype = C.c_int
         L.tpz_format_block_error.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_char_p,
                                              C.c_size_t]
         L.tpz_last_error.restype = C.c_char_p
@@ -148,6 +154,21 @@ class Context:
         c = Columns(*[cols[f] for f in COLUMN_FIELDS])
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")
+
+    def decompressed_sizes_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
+                                d_size: int, stream: int = 0) -> None:
+        """tpz_decompressed_sizes (compress::decode's codec step, compress.rs:95-113)."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        check(lib().tpz_decompressed_sizes(self.handle, C.byref(b), C.c_void_p(d_size),
+                                           C.c_void_p(stream)), "tpz_decompressed_sizes")
+
+    def decompress_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int, d_dst: int,
+                        d_dst_ext: int, d_status: int, stream: int = 0) -> None:
+        """tpz_decompress_blocks: snappy blocks to their Uncompress form."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        check(lib().tpz_decompress_blocks(self.handle, C.byref(b), C.c_void_p(d_dst),
+                                          C.c_void_p(d_dst_ext), C.c_void_p(d_status),
+                                          C.c_void_p(stream)), "tpz_decompress_blocks")
 
     def crc32_ptrs(self, d_src: int, d_ext: int, n_ranges: int, src_bytes: int, d_crc: int,
                    stream: int = 0) -> None:

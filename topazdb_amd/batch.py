@@ -165,3 +165,28 @@ def verify_files(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | N
     ctx.verify_files_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
                           batch.src_bytes, crc.data_ptr(), st.data_ptr(), s.cuda_stream)
     return crc, st
+
+
+def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None):
+    """compress::decode's codec step (src/block/compress.rs:95-113) on the GPU: snappy (tag 2)
+    blocks become Uncompress blocks (tpz_decompressed_sizes, a device prefix sum of the sizes,
+    tpz_decompress_blocks). Returns (DeviceBatch of the uncompressed blocks, codec status
+    tensor); decode the former with decode_batch and take the codec status for blocks whose codec
+    step failed."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    nb = batch.n_blocks
+    size = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
+    ctx.decompressed_sizes_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
+                                size.data_ptr(), s.cuda_stream)
+    with torch.cuda.stream(s):
+        ext = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(size[:nb], 0, out=ext[1:])
+    ext_host = ext.cpu().numpy()
+    total = int(ext_host[-1])
+    dst = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+    st = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+    ctx.decompress_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
+                        dst.data_ptr(), ext.data_ptr(), st.data_ptr(), s.cuda_stream)
+    out = DeviceBatch(dst, ext, ctx.device)
+    return out, st

@@ -313,6 +313,52 @@ static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint
   return TPZ_SUCCESS;
 }
 
+tpz_err tpz_decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size, void* stream) {
+  if (!c || !b || !d_size) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks == 0) return TPZ_SUCCESS;
+  if (!b->d_src || !b->d_ext) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz::CodecLaunch a{};
+  a.src = b->d_src;
+  a.ext = b->d_ext;
+  a.src_bytes = b->src_bytes;
+  a.n_blocks = b->n_blocks;
+  a.size = d_size;
+  tpz::launch_codec_sizes(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
+                              const uint64_t* d_dst_ext, uint8_t* d_status, void* stream) {
+  if (!c || !b || !d_dst || !d_dst_ext || !d_status) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks == 0) return TPZ_SUCCESS;
+  if (!b->d_src || !b->d_ext) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz_workspace* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = get_workspace(c, stream, b->n_blocks, &w);
+    if (r != TPZ_SUCCESS) return r;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 4, s));
+  tpz::CodecLaunch a{};
+  a.src = b->d_src;
+  a.ext = b->d_ext;
+  a.src_bytes = b->src_bytes;
+  a.n_blocks = b->n_blocks;
+  a.dst = d_dst;
+  a.dst_ext = d_dst_ext;
+  a.status = d_status;
+  a.defer_count = w->d_defer;
+  a.defer_list = w->d_defer + 1;
+  a.num_cus = c->num_cus;
+  tpz::launch_decompress(a, s);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
 tpz_err tpz_crc32_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t* d_crc, void* stream) {
   return crc_ranges(c, r, 0, d_crc, nullptr, stream);
 }
@@ -337,6 +383,7 @@ int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actua
     case TPZ_BLOCK_MALFORMED: std::snprintf(tmp, sizeof tmp, "malformed block"); break;
     case TPZ_BLOCK_OVERLAP: std::snprintf(tmp, sizeof tmp, "overlapping entries"); break;
     case TPZ_BLOCK_TOO_LARGE: std::snprintf(tmp, sizeof tmp, "block too large"); break;
+    case TPZ_BLOCK_CODEC_ERROR: std::snprintf(tmp, sizeof tmp, "decompression failed"); break;
     default: std::snprintf(tmp, sizeof tmp, "unknown status %d", status); break;
   }
   int n = (int)std::strlen(tmp);

@@ -73,4 +73,21 @@ struct CrcLaunch {
 
 void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream);
 
+struct CodecLaunch {
+  const uint8_t* src;
+  const uint64_t* ext;
+  uint64_t src_bytes;
+  uint32_t n_blocks;
+  uint64_t* size;          // tpz_decompressed_sizes output
+  uint8_t* dst;            // tpz_decompress_blocks output
+  const uint64_t* dst_ext;
+  uint8_t* status;
+  uint32_t* defer_list;    // workspace: n_blocks entries
+  uint32_t* defer_count;   // workspace: zeroed before the launch
+  uint32_t num_cus;
+};
+
+void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream);
+void launch_decompress(const CodecLaunch& a, hipStream_t stream);
+
 }  // namespace tpz

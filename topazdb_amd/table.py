@@ -14,8 +14,10 @@ Same names, argument meaning and error behaviour as the reference:
 Errors: where the reference returns an anyhow::Error, this raises BlockError whose text is the
 reference's message ("checksum: expected E, actual A", "data is empty", "invaild data"); where
 the reference panics (a malformed block, a file shorter than its checksum, seek_to_last on an
-empty block, ...) it raises ReferencePanic. Blocks the device does not decode yet (snappy/lz4,
-SURVEY.md §8f) raise BlockError("unsupported codec") — there is no CPU fallback.
+empty block, ...) it raises ReferencePanic. Snappy blocks are decompressed on the device
+first; a stream snap rejects raises BlockError("decompression failed"). LZ4 blocks (not decoded
+on the device yet) raise BlockError("unsupported codec") — there is no CPU
+fallback.
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ import torch
 from . import _lib
 from ._lib import (BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY, BLOCK_MALFORMED,
                    BLOCK_OK, Context)
-from .batch import DeviceBatch, decode_batch, verify_files
+from .batch import DeviceBatch, decode_batch, decompress_batch, verify_files
 
 CHECKSUM_SIZE = 4  # src/checksum.rs:4
 SIZEOF_U16 = 2
@@ -118,21 +120,34 @@ class Block:
 
 
 def _decode_region(ctx: Context, region: bytes, ext: np.ndarray) -> list:
-    """Decode blocks [ext[i], ext[i+1]) of `region` in one tpz_decode_blocks launch. Returns per
-    block a Block or the exception the reference's Block::decode / iteration would raise."""
+    """Decode blocks [ext[i], ext[i+1]) of `region`: snappy blocks first go through the device
+    codec step (compress.rs:104-107), then one tpz_decode_blocks launch decodes the batch.
+    Returns per block a Block or the exception the reference's Block::decode / iteration would
+    raise."""
     src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
     batch = DeviceBatch(src, ext, ctx.device)
+    nb = batch.n_blocks
+    codec = None
+    if any(int(ext[b + 1]) > int(ext[b]) and region[int(ext[b + 1]) - 1] == 2 for b in range(nb)):
+        batch, st = decompress_batch(ctx, batch)
+        codec = st[:nb].cpu().numpy()
     cols = decode_batch(ctx, batch)
     torch.cuda.synchronize(torch.device("cuda", ctx.device))
     d = cols.dense(batch.ext_host)
+    dext = batch.ext_host.astype(np.int64)
     out = []
-    for b in range(batch.n_blocks):
+    for b in range(nb):
+        if codec is not None and codec[b] != BLOCK_OK:
+            out.append(_status_error(int(codec[b]), 0, 0))
+            continue
         st = int(d.status[b])
-        lo, hi = int(ext[b]), int(ext[b + 1])
+        lo, hi = int(dext[b]), int(dext[b + 1])
         if st == BLOCK_OK:
             out.append(Block.from_dense(d, b, hi - lo - 5))
         else:
-            expected = _be32(region[hi - 5:hi - 1]) if hi - lo >= 5 else 0
+            expected = 0
+            if hi - lo >= 5:
+                expected = _be32(batch.src[hi - 5:hi - 1].cpu().numpy().tobytes())
             out.append(_status_error(st, expected, int(d.crc_actual[b])))
     return out
 
