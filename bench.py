@@ -249,6 +249,48 @@ def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10
             "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def snappy_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, nb: int = 1 << 18,
+                steps: int = 10) -> dict:
+    """The same blocks with the Snappy codec (topazdb's default, src/opt.rs:48): device codec step
+    (tpz_decompress_blocks, compress.rs:104-107) + tpz_decode_blocks per step, inputs resident.
+    Checks that the decompressed batch equals the Uncompress one. Not the metric; DESIGN.md §4."""
+    from topazdb_amd.batch import decompress_batch
+    nb = min(nb, len(ext) - 1)
+    raw = src[:int(ext[nb])]
+    s2, e2 = synth.snappy_blocks(raw, ext[:nb + 1])
+    batch = DeviceBatch(s2, e2, dev.index)
+    out, st = decompress_batch(ctx, batch)
+    torch.cuda.synchronize(dev)
+    assert int((st[:nb] != 0).sum()) == 0, "codec step failed"
+    assert torch.equal(out.src[:out.src_bytes].cpu(), torch.from_numpy(raw)), "decompressed bytes"
+    cols = SlottedColumns(nb, out.src_bytes, dev.index)
+    stream = torch.cuda.current_stream(dev)
+
+    def codec():
+        ctx.decompress_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
+                            out.src.data_ptr(), out.ext.data_ptr(), st.data_ptr(),
+                            stream.cuda_stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    codec()
+    decode_batch(ctx, out, cols, stream)
+    ev[0].record(stream)
+    for _ in range(steps):
+        codec()
+    ev[1].record(stream)
+    for _ in range(steps):
+        decode_batch(ctx, out, cols, stream)
+    ev[2].record(stream)
+    torch.cuda.synchronize(dev)
+    assert int((cols.status[:nb] != 0).sum()) == 0, "snappy blocks did not decode"
+    ms_codec = ev[0].elapsed_time(ev[1]) / steps
+    ms_dec = ev[1].elapsed_time(ev[2]) / steps
+    t = (ms_codec + ms_dec) * 1e-3
+    return {"blocks": nb, "compressed_bytes": int(e2[-1]), "uncompressed_bytes": int(ext[nb]),
+            "ms_codec": round(ms_codec, 4), "ms_decode": round(ms_dec, 4),
+            "gib_s_compressed_input": round(int(e2[-1]) / t / GIB, 1),
+            "gib_s_uncompressed": round(int(ext[nb]) / t / GIB, 1)}
+
+
 DEFAULT_BLOCKS = {"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}
 
 
@@ -298,6 +340,7 @@ def main():
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-file-crc", action="store_true")
+    ap.add_argument("--no-snappy", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -364,6 +407,13 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"file CRC measurement failed: {ex}")
 
+    snappy = None
+    if rank == 0 and not args.no_snappy:
+        try:
+            snappy = snappy_rate(ctx, src, ext, dev)
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"snappy measurement failed: {ex}")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
@@ -403,6 +453,7 @@ def main():
             "cpu_baseline": cpu,
             "e2e_h2d_d2h_gib_s": e2e,
             "file_crc": fcrc,
+            "snappy": snappy,
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -60,7 +60,7 @@ typedef enum {
                                       topazdb's BlockBuilder never writes such a block.      */
   TPZ_BLOCK_TOO_LARGE = 7,         /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
                                       block_size <= 64 KiB BlockBuilder emits); for a snappy
-                                      block: compressed > 64 KiB - 24 or uncompressed >
+                                      block: compressed > 64 KiB - 31 or uncompressed >
                                       TPZ_MAX_BLOCK_BYTES - 1                                */
   TPZ_BLOCK_CODEC_ERROR = 8        /* Err of the codec: snap's decompress_vec rejects the
                                       stream (compress.rs:104-107)                           */
@@ -200,6 +200,13 @@ int tpz_build_blocks(const uint8_t* h_keys, const uint64_t* h_kpos, const uint8_
                      const uint64_t* h_vpos, uint64_t n_entries, uint32_t block_size,
                      uint8_t* h_out, uint64_t out_cap, uint64_t* h_ext, uint64_t ext_cap,
                      uint64_t* n_blocks, uint64_t* out_len);
+/* compress::encode with CompressOptions::Snappy (src/block/compress.rs:66-71) over a batch of
+ * Uncompress blocks: every tag-1 block i = h_src[h_ext[i] .. h_ext[i+1]) is written to h_out as
+ * snappy_raw(payload | crc) | 2, other blocks unchanged; h_out_ext gets n_blocks + 1 extents.
+ * Host memory only; out_cap >= 32 * n_blocks + 2 * h_ext[n_blocks] always suffices. */
+int tpz_snappy_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64_t n_blocks,
+                             uint8_t* h_out, uint64_t out_cap, uint64_t* h_out_ext,
+                             uint64_t* out_len);
 /* CRC-32/ISO-HDLC on the host (checksum::calculate_checksum, src/checksum.rs:6-10). */
 uint32_t tpz_host_crc32(const uint8_t* h_buf, uint64_t len);
 

@@ -135,7 +135,8 @@ static int codec_step(const uint8_t* b, size_t len, uint8_t** buf, const uint8_t
   if (len == 0 || b[len - 1] != 2) return 0;
   uint64_t want = 0;
   if (tpzo_snappy_uncompressed_len(b, len - 1, &want) != 0) return TPZO_CODEC;
-  if (want + 1 > 94192) return TPZO_TOO_LARGE; /* the device's limit (TPZ_MAX_BLOCK_BYTES) */
+  /* the device's limits (TPZ_MAX_BLOCK_BYTES; a 64 KiB staging window less 32 bytes of slack) */
+  if (want + 1 > 94192 || len - 1 > 65504) return TPZO_TOO_LARGE;
   *buf = (uint8_t*)malloc(want + 1);
   uint64_t got = 0;
   if (tpzo_snappy_decompress(b, len - 1, *buf, want, &got) != 0) return TPZO_CODEC;

@@ -114,3 +114,14 @@ def test_synth_regions_decode_on_oracle(config, nb):
 def test_product_library_does_not_link_the_oracle():
     so = open(_lib.LIB_PATH, "rb").read()
     assert b"tpzo_" not in so and b"liboracle" not in so
+
+
+@pytest.mark.parametrize("config", ["4k", "zipf", "64k"])
+def test_host_snappy_encoder_round_trips(config):
+    """tpz_snappy_encode_blocks (compress::encode with Snappy, compress.rs:66-71) emits streams
+    the oracle's snappy restatement decodes back to the Uncompress blocks."""
+    src, ext = synth.make_region(config, 6 if config == "64k" else 60)
+    s2, e2 = synth.snappy_blocks(src, ext)
+    for i in range(len(ext) - 1):
+        st, out = O.decompress_block(s2[int(e2[i]):int(e2[i + 1])].tobytes())
+        assert st == O.OK and out == src[int(ext[i]):int(ext[i + 1])].tobytes()

@@ -96,7 +96,7 @@ def test_large_snappy_blocks(ctx):
     blocks = [O.snappy_block(src[int(ext[i]):int(ext[i + 1])].tobytes(), i % 4)
               for i in range(40)]
     rng = np.random.default_rng(5)
-    blocks += snappy_random_blocks(rng, 40, max_target=60000)  # compressed <= 64 KiB - 24
+    blocks += snappy_random_blocks(rng, 40, max_target=60000)  # compressed <= 64 KiB - 31
     s2, e2 = batch_of(blocks)
     assert_parity(ctx, s2, e2)
 
@@ -106,3 +106,23 @@ def test_config_batch_snappy(ctx):
     blocks = [O.snappy_block(src[int(ext[i]):int(ext[i + 1])].tobytes()) for i in range(5000)]
     s2, e2 = batch_of(blocks)
     assert_parity(ctx, s2, e2, expect_all_ok=True)
+
+
+def test_compressed_size_limit(ctx):
+    """A snappy block whose compressed form exceeds the 64 KiB staging window (64 KiB - 31
+    bytes with its tag) is TOO_LARGE on the device and in the oracle's codec step, although its
+    uncompressed length fits; one byte below the limit it decodes."""
+    rng = np.random.default_rng(11)
+    blocks, want = [], []
+    for clen in (65505, 65506, 70000):
+        # a literal-only stream (mode 3): 3-byte varint + 3-byte literal header + payload
+        raw = rng.bytes(clen - 1 - 6)
+        b = O.snappy_compress(raw, 3) + b"\x02"
+        assert len(b) >= clen
+        blocks.append(b)
+        want.append(_lib.BLOCK_OK if len(b) <= 65505 else _lib.BLOCK_TOO_LARGE)
+    outs, st = device_codec(ctx, blocks)
+    assert list(st) == want
+    assert outs[0] == O.snappy_decompress(blocks[0][:-1]) + b"\x01"
+    s2, e2 = batch_of(blocks)
+    assert_parity(ctx, s2, e2)

@@ -34,9 +34,38 @@ constexpr int kWave = 64;
 constexpr int kSmallWaves = 16;
 constexpr u32 kSmallIn = 4608, kSmallOut = 5120;     // per-wave windows of the 16-wave kernel
 constexpr u32 kBigIn = 65536, kBigOut = 94208;       // the one-wave kernel
-constexpr u32 kInSlack = 16 + 8;                     // staging offset (< 16) + header overread
-static_assert(kSmallWaves * (kSmallIn + kSmallOut) <= 163840, "small LDS");
-static_assert(kBigIn + kBigOut <= 163840, "big LDS");
+constexpr u32 kGuard = 16;                           // readable bytes before each input window
+constexpr u32 kInSlack = 16 + 16;                    // staging offset (< 16) + header overread
+static_assert(kSmallWaves * (kGuard + kSmallIn + kSmallOut) <= 163840, "small LDS");
+static_assert(kGuard + kBigIn + kBigOut <= 163840, "big LDS");
+
+#ifdef TPZ_CODEC_STAMPS
+// Diagnostic build only (make -C topazdb_amd/csrc codec-variants): per-phase wave cycles.
+__device__ unsigned long long g_cstamps[8];
+struct Stamps {
+  u64 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 t = __builtin_amdgcn_s_memtime();
+  __device__ void hit(int i) {
+    const u64 n = __builtin_amdgcn_s_memtime();
+    acc[i] += n - t;
+    t = n;
+  }
+  __device__ void add(int i, u64 v) { acc[i] += v; }
+  __device__ void flush(bool lane0) {
+    if (lane0)
+      for (int i = 0; i < 8; i++) atomicAdd(&g_cstamps[i], (unsigned long long)acc[i]);
+  }
+};
+#define STAMP(i) st_.hit(i)
+#define SCOUNT(i, v) st_.add(i, v)
+#define STAMPS_ARG , Stamps& st_
+#define STAMPS_PASS , st_
+#else
+#define STAMP(i) (void)0
+#define SCOUNT(i, v) (void)0
+#define STAMPS_ARG
+#define STAMPS_PASS
+#endif
 
 __device__ __forceinline__ u32 lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -48,10 +77,16 @@ __device__ __forceinline__ u64 uni64(u64 x) {
   return ((u64)hi << 32) | lo;
 }
 
-// Little-endian u32 at any LDS byte offset (two aligned reads + alignbyte), wave-uniform.
+// Little-endian u32 at any LDS byte address: two aligned reads + alignbyte. (Pointer arithmetic
+// only, so the accesses stay ds_read: a round trip through an integer would make them flat.)
+__device__ __forceinline__ u32 lds_u32_lane(const uint8_t* p) {
+  const u32 al = (u32)reinterpret_cast<uintptr_t>(p) & 3u;
+  const u32* q = reinterpret_cast<const u32*>(p - al);
+  return __builtin_amdgcn_alignbyte(q[1], q[0], al);
+}
+// The same, wave-uniform.
 __device__ __forceinline__ u32 lds_u32(const uint8_t* base, u32 a) {
-  const u32* p = reinterpret_cast<const u32*>(base + (a & ~3u));
-  return uni(__builtin_amdgcn_alignbyte(p[1], p[0], a & 3u));
+  return uni(lds_u32_lane(base + a));
 }
 
 // Snappy varint preamble from global memory (at most 10 bytes, inside the block). Returns the
@@ -101,125 +136,179 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
 }
 
 // ------------------------------------------------------------------ per-block work
-// Copies LDS bytes [lo, lo + n) of `win` to global [g, g + n): 16-byte stores for the aligned
-// pieces strictly inside, byte stores for the (shared) edge pieces.
-__device__ __forceinline__ void store_bytes(const uint8_t* win, u32 lo, uint8_t* g, u32 n) {
+// Copies LDS bytes to global [g, g + n). The bytes sit at win[(g & 15) ..], i.e. LDS and global
+// share their alignment, so every whole 16-byte piece is one ds_read_b128 + one global store;
+// the (shared) edge pieces take byte stores.
+__device__ __forceinline__ void store_aligned(const uint8_t* win, uint8_t* g, u32 n) {
   const u32 lane = lane_id();
   if (n == 0) return;
-  const uintptr_t ga = reinterpret_cast<uintptr_t>(g);
-  const u32 head = (u32)((16 - (ga & 15)) & 15);           // bytes before the first aligned piece
+  const u32 a = (u32)(reinterpret_cast<uintptr_t>(g) & 15);
+  const u32 head = (16 - a) & 15;
   const u32 h = head < n ? head : n;
   const u32 body = (n - h) & ~15u;
-  for (u32 k = lane; k < h; k += kWave) g[k] = win[lo + k];
-  for (u32 k = 16 * lane; k < body; k += 16 * kWave) {
-    const uint8_t* s = win + lo + h + k;
-    uint4 v;
-    v.x = (u32)s[0] | (u32)s[1] << 8 | (u32)s[2] << 16 | (u32)s[3] << 24;
-    v.y = (u32)s[4] | (u32)s[5] << 8 | (u32)s[6] << 16 | (u32)s[7] << 24;
-    v.z = (u32)s[8] | (u32)s[9] << 8 | (u32)s[10] << 16 | (u32)s[11] << 24;
-    v.w = (u32)s[12] | (u32)s[13] << 8 | (u32)s[14] << 16 | (u32)s[15] << 24;
-    *reinterpret_cast<uint4*>(g + h + k) = v;
-  }
-  for (u32 k = h + body + lane; k < n; k += kWave) g[k] = win[lo + k];
+  for (u32 k = lane; k < h; k += kWave) g[k] = win[a + k];
+  for (u32 k = 16 * lane; k < body; k += 16 * kWave)
+    *reinterpret_cast<uint4*>(g + h + k) = *reinterpret_cast<const uint4*>(win + a + h + k);
+  for (u32 k = h + body + lane; k < n; k += kWave) g[k] = win[a + k];
 }
 
-// Stages global bytes [s, s + n) into win[0 .. n) (byte-exact).
-__device__ __forceinline__ void stage_bytes(const uint8_t* src, u64 s, u32 n, uint8_t* win) {
+// Stages global bytes [s, s + n) into LDS at win[(s & 15) ..]: 16-byte aligned loads, four
+// 1 KiB rounds in flight per step (the bytes around the range are don't-care).
+__device__ __forceinline__ void stage_aligned(const uint8_t* src, u64 src_bytes, u64 s, u32 n,
+                                              uint8_t* win) {
   const u32 lane = lane_id();
-  for (u32 k = lane; k < n; k += kWave) win[k] = src[s + k];
+  const u64 ws = s & ~15ull;
+  const u32 nb = (u32)(s + n - ws);
+  const u64 lim = src_bytes - ws < 0x7FFFFFF0ull ? src_bytes - ws : 0x7FFFFFF0ull;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(src + ws), (short)0, (int)lim, 0x00020000);
+  for (u32 off = 0; off < nb; off += 4096) {
+    uint4 t[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      t[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + r * 1024 + lane * 16, 0, 0));
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (off + r * 1024 + lane * 16 < nb) *reinterpret_cast<uint4*>(win + off + r * 1024 + lane * 16) = t[r];
+  }
+  // a piece straddling the end of the buffer came back zeroed: refill its in-range bytes
+  const u64 last = (s + n - 1) & ~15ull;
+  if (last + 16 > src_bytes)
+    for (u32 k = lane; k < 16; k += kWave)
+      if (last + k < s + n) win[last - ws + k] = src[last + k];
 }
 
-// Decompresses the snappy stream in[0 .. n) into out[0 .. want). Wave-uniform control flow.
+// out[d .. d + len) = in[ip .. ip + len) in LDS. The bytes up to the next 4-byte boundary of
+// the output are written one per lane; the rest as whole aligned dwords (two aligned input reads
+// + alignbyte), the last of which may write up to 3 bytes past the literal: those bytes belong to
+// later elements, whose writes come after in LDS order, and nothing reads past `d`.
+__device__ __forceinline__ void literal_copy(const uint8_t* in, u32 ip, uint8_t* out, u32 d,
+                                             u32 len) {
+  const u32 lane = lane_id();
+  const u32 pad0 = (0u - (u32)reinterpret_cast<uintptr_t>(out + d)) & 3u;
+  const u32 pad = pad0 < len ? pad0 : len;
+  if (lane < pad) out[d + lane] = in[ip + lane];
+  const u32 nd = (len - pad + 3) >> 2;
+  u32* o = reinterpret_cast<u32*>(out + d + pad);
+  const uint8_t* i = in + ip + pad;
+  for (u32 t = lane; t < nd; t += kWave) o[t] = lds_u32_lane(i + 4 * t);
+}
+
+// Decompresses the snappy stream in[0 .. n) (elements from `ip`) into out[0 .. want).
+// Wave-uniform control flow, kept lean: the loop is bound by scalar issue (one SALU instruction
+// per SIMD every 4 cycles, shared by the SIMD's waves), so the header is decoded with selects and
+// every check folds into one branch. The next element's header is read before the current
+// element's bytes are copied, so its LDS latency overlaps the copy (the input is never written).
 __device__ __forceinline__ bool snappy_decode(const uint8_t* in, u32 n, u32 ip, uint8_t* out,
-                                              u32 want) {
+                                              u32 want STAMPS_ARG) {
   const u32 lane = lane_id();
   u32 d = 0;
+  // the next header as three aligned dwords in VGPRs (+ its alignment): combined only at the top
+  // of the next iteration
+  u32 al = (u32)reinterpret_cast<uintptr_t>(in + ip) & 3u;
+  const u32* q = reinterpret_cast<const u32*>(in + ip - al);
+  u32 r0 = q[0], r1 = q[1], r2 = q[2];
   while (ip < n) {
-    const u32 w0 = lds_u32(in, ip), w1 = lds_u32(in, ip + 4);
-    const u32 tag = w0 & 0xFF;
-    ip += 1;
-    u32 len, off;
-    const u32 kind = tag & 3;
-    if (kind == 0) {                                          // literal
-      len = (tag >> 2) + 1;
-      if ((tag >> 2) >= 60) {
-        const u32 nb = (tag >> 2) - 59;
-        const u64 v = ((u64)w1 << 24 | (w0 >> 8)) & ((1ull << (8 * nb)) - 1);
-        if (ip + nb > n || v + 1 > 0xFFFFFFFFull) return false;
-        ip += nb;
-        len = (u32)v + 1;
-      }
-      if ((u64)ip + len > n || (u64)d + len > want) return false;
-      for (u32 k = lane; k < len; k += kWave) out[d + k] = in[ip + k];
-      ip += len;
-      d += len;
-      continue;
+    const u32 w0 = uni(__builtin_amdgcn_alignbyte(r1, r0, al));
+    const u32 w1 = uni(__builtin_amdgcn_alignbyte(r2, r1, al));
+    const u32 tag = w0 & 0xFF, kind = tag & 3, t6 = tag >> 2;
+    const u32 x = (w0 >> 8) | (w1 << 24);                     // the 4 bytes after the tag
+    // literal: length - 1 in t6, or in the next t6 - 59 bytes when t6 >= 60
+    const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
+    u32 lx = nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1));
+    lx = lx < 0x7FFFFFFFu ? lx : 0x7FFFFFFFu;                 // past any window: fails below
+    const u32 len = kind == 0 ? lx + 1 : (kind == 1 ? 4 + (t6 & 7) : t6 + 1);
+    const u32 hl = kind == 0 ? 1 + nb : (0x5320u >> (4 * kind)) & 15;
+    const u32 off = kind == 1 ? ((tag >> 5) << 8) | (x & 0xFF) : (kind == 2 ? x & 0xFFFF : x);
+    const u32 next = ip + hl + (kind == 0 ? len : 0u);
+    // snap's Err: output overrun, element past the input, copy offset 0 or before the output
+    if (d + len > want || next > n || (kind != 0 && off - 1 >= d)) return false;
+    al = (u32)reinterpret_cast<uintptr_t>(in + next) & 3u;    // prefetch the next header
+    q = reinterpret_cast<const u32*>(in + next - al);
+    r0 = q[0];
+    r1 = q[1];
+    r2 = q[2];
+    if (kind == 0) {
+      literal_copy(in, ip + hl, out, d, len);
+    } else if (lane < len) {
+      // copies are at most 64 bytes: one byte per lane; an overlapping copy (off < len) repeats
+      // with period off (lane % off from a float reciprocal: exact for lane, off <= 64)
+      const u32 qq = (u32)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+      const u32 r = off >= len ? lane : lane - qq * off;
+      out[d + lane] = out[d - off + r];
     }
-    if (kind == 1) {                                          // copy, 1-byte offset
-      if (ip + 1 > n) return false;
-      len = 4 + ((tag >> 2) & 7);
-      off = ((tag >> 5) << 8) | ((w0 >> 8) & 0xFF);
-      ip += 1;
-    } else if (kind == 2) {                                   // copy, 2-byte offset
-      if (ip + 2 > n) return false;
-      len = 1 + (tag >> 2);
-      off = (w0 >> 8) & 0xFFFF;
-      ip += 2;
-    } else {                                                  // copy, 4-byte offset
-      if (ip + 4 > n) return false;
-      len = 1 + (tag >> 2);
-      off = (w0 >> 8) | (w1 << 24);
-      ip += 4;
-    }
-    if (off == 0 || off > d || (u64)d + len > want) return false;
-    // the source run precedes the copy; an overlapping copy repeats with period `off`
-    for (u32 k = lane; k < len; k += kWave) out[d + k] = out[d - off + (off >= len ? k : k % off)];
+    ip = next;
     d += len;
+    SCOUNT(6, 1);
   }
   return d == want;
 }
 
+struct BlockMeta {
+  u64 s, e, D0, D1;
+  u32 tag;
+};
+
 // One block. Returns false when it does not fit the windows (the caller defers it).
 template <u32 kIn, u32 kOut>
-__device__ __forceinline__ bool codec_block(const CodecParams& p, u32 b, uint8_t* in,
-                                            uint8_t* out, bool last_resort) {
+__device__ __forceinline__ bool codec_block(const CodecParams& p, u32 b, const BlockMeta& m,
+                                            uint8_t* in_win, uint8_t* out_win,
+                                            bool last_resort STAMPS_ARG) {
   const u32 lane = lane_id();
-  const u64 s = uni64(p.ext[b]), e = uni64(p.ext[b + 1]);
-  const u64 len = e - s;
-  const u64 D0 = uni64(p.dst_ext[b]), D1 = uni64(p.dst_ext[b + 1]);
-  uint8_t* dst = p.dst + D0;
-  const u64 dn = D1 - D0;
-  const u32 tag = len ? uni(p.src[e - 1]) : 0u;
-  if (len == 0 || tag != 2) {                                 // copied unchanged
+  const u64 s = m.s, len = m.e - m.s;
+  uint8_t* dst = p.dst + m.D0;
+  const u64 dn = m.D1 - m.D0;
+  if (len == 0 || m.tag != 2) {                               // copied unchanged
     const u64 n = len < dn ? len : dn;
     for (u64 k = lane; k < n; k += kWave) dst[k] = p.src[s + k];
     if (lane == 0) p.status[b] = TPZ_BLOCK_OK;
     return true;
   }
+  const bool fits = len - 1 + kInSlack <= kIn && dn + 16 <= kOut;
   u64 want = 0;
-  const u32 h = snappy_header(p.src + s, len - 1, want);
-  bool ok = h != 0 && want + 1 == dn;
-  u32 st = TPZ_BLOCK_CODEC_ERROR;
-  if (ok) {
-    if (len - 1 + kInSlack > kIn || want + 1 > kOut) {
-      if (!last_resort) return false;
-      ok = false;
-      st = TPZ_BLOCK_TOO_LARGE;
+  u32 h = 0, st = TPZ_BLOCK_CODEC_ERROR;
+  bool ok = false;
+  const u32 a_in = (u32)(s & 15), a_out = (u32)(reinterpret_cast<uintptr_t>(dst) & 15);
+  uint8_t* in = in_win + a_in;
+  uint8_t* out = out_win + a_out;
+  if (fits) {
+    STAMP(5);
+    stage_aligned(p.src, p.src_bytes, s, (u32)(len - 1), in_win);
+    __builtin_amdgcn_wave_barrier();
+    STAMP(1);
+    // varint preamble from the staged bytes (at most 10, inside the block)
+    const u32 v0 = lds_u32(in, 0), v1 = lds_u32(in, 4), v2 = lds_u32(in, 8);
+    u64 v = 0;
+    for (u32 i = 0; i < 10 && i < len - 1; i++) {
+      const u32 c = ((i < 4 ? v0 : i < 8 ? v1 : v2) >> (8 * (i & 3))) & 0xFF;
+      v |= (u64)(c & 0x7F) << (7 * i);
+      if (!(c & 0x80)) {
+        if (v <= 0xFFFFFFFFull) {
+          want = v;
+          h = i + 1;
+        }
+        break;
+      }
     }
-  } else if (h != 0 && want + 1 > TPZ_MAX_BLOCK_BYTES) {
-    st = TPZ_BLOCK_TOO_LARGE;                                  // the sizes kernel gave it 1 byte
+  } else {
+    if (!last_resort) return false;
+    h = snappy_header(p.src + s, len - 1, want);
+    if (h != 0) st = TPZ_BLOCK_TOO_LARGE;
   }
-  if (ok) {
-    stage_bytes(p.src, s, (u32)(len - 1), in);
+  if (h != 0 && want + 1 > TPZ_MAX_BLOCK_BYTES) st = TPZ_BLOCK_TOO_LARGE;  // sizes gave 1 byte
+  if (fits && h != 0 && want + 1 == dn) {
+    STAMP(2);
+    ok = snappy_decode(in, (u32)(len - 1), h, out, (u32)want STAMPS_PASS);
     __builtin_amdgcn_wave_barrier();
-    ok = snappy_decode(in, (u32)(len - 1), h, out, (u32)want);
-    __builtin_amdgcn_wave_barrier();
+    STAMP(3);
   }
   if (ok) {
     if (lane == 0) out[want] = 1;                              // re-tagged Uncompress
     __builtin_amdgcn_wave_barrier();
-    store_bytes(out, 0, dst, (u32)(want + 1));
+    store_aligned(out_win, dst, (u32)(want + 1));
     if (lane == 0) p.status[b] = TPZ_BLOCK_OK;
+    STAMP(4);
+    SCOUNT(7, 1);
   } else {
     if (lane == 0) {
       if (dn) dst[dn - 1] = 0;                                 // decodes as BAD_TAG
@@ -230,25 +319,84 @@ __device__ __forceinline__ bool codec_block(const CodecParams& p, u32 b, uint8_t
   return true;
 }
 
+__device__ __forceinline__ u64 readlane64(u64 x, u32 k) {
+  return ((u64)__builtin_amdgcn_readlane((u32)(x >> 32), k) << 32) |
+         __builtin_amdgcn_readlane((u32)x, k);
+}
+
+// Each wave takes blocks wave0, wave0 + S, wave0 + 2S, ... (S = waves in the grid); their
+// extents and tag bytes are loaded 64 blocks at a time, one block per lane.
 __global__ __launch_bounds__(kWave * kSmallWaves) void codec_wave_kernel(CodecParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kSmallWaves * (kSmallIn + kSmallOut)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kSmallWaves * (kGuard + kSmallIn + kSmallOut)];
+  const u32 lane = lane_id();
   const u32 wid = uni(threadIdx.x >> 6);
-  uint8_t* in = lds + wid * (kSmallIn + kSmallOut);
-  uint8_t* out = in + kSmallIn;
-  for (u32 b = blockIdx.x * kSmallWaves + wid; b < p.n_blocks; b += gridDim.x * kSmallWaves) {
-    if (!codec_block<kSmallIn, kSmallOut>(p, b, in, out, false) && lane_id() == 0)
-      p.defer_list[atomicAdd(p.defer_count, 1u)] = b;
+  uint8_t* in_win = lds + wid * (kGuard + kSmallIn + kSmallOut) + kGuard;
+  uint8_t* out_win = in_win + kSmallIn;
+  const u32 S = gridDim.x * kSmallWaves;
+#ifdef TPZ_CODEC_STAMPS
+  Stamps st_;
+#endif
+  for (u32 g = blockIdx.x * kSmallWaves + wid; g < p.n_blocks; g += kWave * S) {
+    const u32 bj = g + lane * S;
+    const u32 bc = bj < p.n_blocks ? bj : p.n_blocks - 1;
+    BlockMeta mj;
+    mj.s = p.ext[bc];
+    mj.e = p.ext[bc + 1];
+    mj.D0 = p.dst_ext[bc];
+    mj.D1 = p.dst_ext[bc + 1];
+    mj.tag = mj.e > mj.s ? p.src[mj.e - 1] : 0u;
+    const u32 cnt = uni((p.n_blocks - g + S - 1) / S < (u32)kWave ? (p.n_blocks - g + S - 1) / S
+                                                                  : (u32)kWave);
+    STAMP(0);
+    for (u32 k = 0; k < cnt; k++) {
+      BlockMeta m;
+      m.s = readlane64(mj.s, k);
+      m.e = readlane64(mj.e, k);
+      m.D0 = readlane64(mj.D0, k);
+      m.D1 = readlane64(mj.D1, k);
+      m.tag = __builtin_amdgcn_readlane(mj.tag, k);
+      const u32 b = g + k * S;
+      if (!codec_block<kSmallIn, kSmallOut>(p, b, m, in_win, out_win, false STAMPS_PASS) &&
+          lane == 0)
+        p.defer_list[atomicAdd(p.defer_count, 1u)] = b;
+      STAMP(5);
+    }
   }
+#ifdef TPZ_CODEC_STAMPS
+  st_.flush(lane == 0);
+#endif
 }
 
 __global__ __launch_bounds__(kWave) void codec_big_kernel(CodecParams p) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kBigIn + kBigOut];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kGuard + kBigIn + kBigOut];
   const u32 cnt = uni(*p.defer_count);
-  for (u32 it = blockIdx.x; it < cnt; it += gridDim.x)
-    codec_block<kBigIn, kBigOut>(p, uni(p.defer_list[it]), lds, lds + kBigIn, true);
+  for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const u32 b = uni(p.defer_list[it]);
+    BlockMeta m;
+    m.s = uni64(p.ext[b]);
+    m.e = uni64(p.ext[b + 1]);
+    m.D0 = uni64(p.dst_ext[b]);
+    m.D1 = uni64(p.dst_ext[b + 1]);
+    m.tag = m.e > m.s ? uni(p.src[m.e - 1]) : 0u;
+#ifdef TPZ_CODEC_STAMPS
+    Stamps st_;
+#endif
+    codec_block<kBigIn, kBigOut>(p, b, m, lds + kGuard, lds + kGuard + kBigIn, true STAMPS_PASS);
+  }
 }
 
 }  // namespace
+
+#ifdef TPZ_CODEC_STAMPS
+extern "C" int tpz_debug_codec_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(g_cstamps)) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_cstamps), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
 
 void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream) {
   CodecParams p{};

@@ -3,10 +3,13 @@
 // Restates src/block/builder.rs:26-85 (fill rule, Entry::encode), src/block.rs:31-44
 // (Block::encode: u16 n | u16 off[n] | entries | u32 crc32 | codec tag) and
 // src/table/builder.rs:49-85 (SsTableBuilder::add / block_build: one block after another,
-// back to back) for the Uncompress codec (src/block/compress.rs:85-89). It produces SST data
-// regions for bench.py and for the table facade; it is not on the decode path.
+// back to back) for the Uncompress codec (src/block/compress.rs:85-89), and re-encodes blocks
+// with the Snappy codec (compress.rs:66-71; a greedy LZ77 emitter of the snappy raw format, the
+// role snap::raw::Encoder plays). It produces SST data regions for bench.py and for the table
+// facade; it is not on the decode path.
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../../include/tpz_gpu.h"
 
@@ -51,9 +54,92 @@ inline void put32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
 
+// Snappy raw-format encoder: varint length, then literals and copies found with a 4-byte hash
+// (copy-1 for lengths 4..11 within 2 KiB, else copy-2; offsets < 64 KiB). Returns the length.
+size_t snappy_encode(const uint8_t* s, size_t n, uint8_t* o) {
+  size_t p = 0;
+  for (uint64_t v = n;; v >>= 7) {
+    o[p++] = (uint8_t)((v & 0x7F) | (v > 0x7F ? 0x80 : 0));
+    if (v <= 0x7F) break;
+  }
+  auto literal = [&](size_t lo, size_t hi) {
+    if (hi <= lo) return;
+    const size_t v = hi - lo - 1;
+    if (v < 60) {
+      o[p++] = (uint8_t)(v << 2);
+    } else {
+      const int nb = v < (1u << 8) ? 1 : v < (1u << 16) ? 2 : v < (1u << 24) ? 3 : 4;
+      o[p++] = (uint8_t)((59 + nb) << 2);
+      for (int k = 0; k < nb; k++) o[p++] = (uint8_t)(v >> (8 * k));
+    }
+    std::memcpy(o + p, s + lo, hi - lo);
+    p += hi - lo;
+  };
+  constexpr int kBits = 13;
+  thread_local std::vector<int32_t> table(1 << kBits);
+  std::fill(table.begin(), table.end(), -1);
+  size_t lit = 0, i = 0;
+  while (i + 4 <= n) {
+    uint32_t w;
+    std::memcpy(&w, s + i, 4);
+    const uint32_t h = (w * 0x1E35A7BDu) >> (32 - kBits);
+    const int32_t c = table[h];
+    table[h] = (int32_t)i;
+    uint32_t cw;
+    if (c < 0 || i - (size_t)c >= 65536 || (std::memcpy(&cw, s + c, 4), cw != w)) {
+      i++;
+      continue;
+    }
+    size_t m = 4;
+    while (i + m < n && s[c + m] == s[i + m]) m++;
+    literal(lit, i);
+    const size_t off = i - (size_t)c;
+    for (size_t rem = m; rem;) {
+      size_t l = rem > 64 ? (rem - 64 < 4 ? 60 : 64) : rem;
+      if (l >= 4 && l <= 11 && off < 2048) {
+        o[p++] = (uint8_t)(1 | ((l - 4) << 2) | ((off >> 8) << 5));
+        o[p++] = (uint8_t)off;
+      } else {
+        o[p++] = (uint8_t)(2 | ((l - 1) << 2));
+        o[p++] = (uint8_t)off;
+        o[p++] = (uint8_t)(off >> 8);
+      }
+      rem -= l;
+    }
+    i += m;
+    lit = i;
+  }
+  literal(lit, n);
+  return p;
+}
+
 }  // namespace
 
 extern "C" {
+
+int tpz_snappy_encode_blocks(const uint8_t* src, const uint64_t* ext, uint64_t n_blocks,
+                             uint8_t* out, uint64_t out_cap, uint64_t* out_ext,
+                             uint64_t* out_len) {
+  if (!src || !ext || !out || !out_ext || !out_len) return TPZ_ERR_INVALID_ARG;
+  uint64_t o = 0;
+  for (uint64_t b = 0; b < n_blocks; b++) {
+    const uint8_t* blk = src + ext[b];
+    const uint64_t len = ext[b + 1] - ext[b];
+    out_ext[b] = o;
+    if (len == 0 || blk[len - 1] != 1) {  // only Uncompress blocks are re-encoded
+      if (o + len > out_cap) return TPZ_ERR_NOMEM;
+      std::memcpy(out + o, blk, len);
+      o += len;
+      continue;
+    }
+    if (o + 32 + 2 * len > out_cap) return TPZ_ERR_NOMEM;
+    o += snappy_encode(blk, len - 1, out + o);  // payload | crc, before the codec tag
+    out[o++] = 2;                                  // compress.rs:69 Snappy tag
+  }
+  out_ext[n_blocks] = o;
+  *out_len = o;
+  return TPZ_SUCCESS;
+}
 
 uint32_t tpz_host_crc32(const uint8_t* p, uint64_t n) { return crc()(p, (size_t)n); }
 

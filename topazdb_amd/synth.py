@@ -113,3 +113,22 @@ def reference_bench_entries(n: int = 1000):
     np.cumsum([len(v) for v in vs], out=vpos[1:])
     return (np.frombuffer(b"".join(ks), np.uint8), kpos, np.frombuffer(b"".join(vs), np.uint8),
             vpos)
+
+
+def snappy_blocks(src: np.ndarray, ext: np.ndarray):
+    """Re-encode a region's Uncompress blocks with the Snappy codec (tpz_snappy_encode_blocks,
+    compress::encode, src/block/compress.rs:66-71): (src, ext)."""
+    L = _lib.lib()
+    L.tpz_snappy_encode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                           C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
+    nb = len(ext) - 1
+    src = np.ascontiguousarray(src, np.uint8)
+    ext = np.ascontiguousarray(ext, np.uint64)
+    cap = 32 * nb + 2 * int(ext[-1]) + 64
+    out = np.empty(cap, np.uint8)
+    oext = np.empty(nb + 1, np.uint64)
+    n = C.c_uint64()
+    _lib.check(L.tpz_snappy_encode_blocks(src.ctypes.data, ext.ctypes.data, nb, out.ctypes.data,
+                                          cap, oext.ctypes.data, C.byref(n)),
+               "tpz_snappy_encode_blocks")
+    return out[:n.value], oext
