@@ -72,10 +72,11 @@ def test_crc_known_answers(ctx):
 
 @pytest.mark.parametrize("shift", [0, 1, 7, 15])
 def test_window_boundaries(ctx, shift):
-    """Lengths around the 16-byte tail split and the 16 KiB window, at every d_src alignment."""
+    """Lengths around the 16-byte tail split and the window sizes (8 KiB shipped; 4 and 16 KiB
+    in the diagnostic builds), at every d_src alignment."""
     rng = np.random.default_rng(100 + shift)
-    lens = [0, 1, 3, 4, 5, 15, 16, 17, 31, 255, 256, 257, 4095, 4096, 16383, 16384, 16385,
-            16400, 32768, 49151, 70001, 0, 2, 131072 + 9]
+    lens = [0, 1, 3, 4, 5, 15, 16, 17, 31, 255, 256, 257, 4095, 4096, 8191, 8192, 8193, 8208,
+            16383, 16384, 16385, 16400, 24576, 32768, 49151, 70001, 0, 2, 131072 + 9]
     buf = rng.bytes(sum(lens))
     ext = ranges_of(lens)
     np.testing.assert_array_equal(gpu_crcs(ctx, buf, ext, shift), expected(buf, ext))

@@ -119,7 +119,7 @@ struct tpz_workspace {
   uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
   uint32_t defer_cap = 0;
   uint64_t* d_big_scratch = nullptr;
-  uint32_t* d_acc = nullptr;    // 2 x acc_cap: per-range accumulators of tpz_crc32_ranges
+  uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
   uint32_t acc_cap = 0;
 };
 
@@ -147,7 +147,7 @@ tpz_err get_acc(tpz_ctx* c, void* stream, uint32_t n, uint32_t** out) {
   tpz_workspace& w = c->ws[stream];
   if (!w.d_acc || w.acc_cap < n) {
     uint32_t* d = nullptr;
-    TPZ_HIP(hipMalloc(&d, (size_t)2 * n * 4));
+    TPZ_HIP(hipMalloc(&d, (size_t)n * 4));
     if (w.d_acc) {
       (void)hipStreamSynchronize((hipStream_t)stream);
       (void)hipFree(w.d_acc);
@@ -294,7 +294,7 @@ static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint
     if (e != TPZ_SUCCESS) return e;
   }
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipMemsetAsync(acc, 0, (size_t)2 * r->n_blocks * 4, s));
+  TPZ_HIP(hipMemsetAsync(acc, 0, (size_t)r->n_blocks * 4, s));
   tpz::CrcLaunch a{};
   a.src = r->d_src;
   a.ext = r->d_ext;
@@ -304,7 +304,6 @@ static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint
   a.tables = c->d_range_tables;
   a.rep = c->d_rep_tables;
   a.acc = acc;
-  a.acc_last = acc + r->n_blocks;
   a.crc = d_crc;
   a.status = d_status;
   a.num_cus = c->num_cus;

@@ -9,17 +9,20 @@
 //   crc32(M) = ~(R0(M) ^ Z_|M|(0xFFFFFFFF)),  Z_n(a) = the register after n zero bytes from a,
 // and R0 is linear: R0(A || B) = Z_|B|(R0(A)) ^ R0(B); leading zero bytes leave R0 unchanged.
 //
-// Work split: the buffer is cut into absolute 16 KiB windows (addresses taken
+// Work split: the buffer is cut into absolute 8 KiB windows (addresses taken
 // from d_src rounded down to 16 B). Every wave owns a contiguous span of windows. For each
 // (window, range) overlap it computes R0 of the overlap's "main" part (the range up to its last
-// 16-byte boundary): lane l folds the 256-byte run that ends 256*l bytes before the overlap's end
-// (16 aligned dwordx4 loads straight into registers, bytes before the range masked to zero) with
-// slice-by-4 lookups, shifts it by 256*l with the shift-by-16*2^j operators (bits of l), and the
-// wave XORs the lanes. The overlap's distance to the range's last window is a whole number q of
-// windows: the wave shifts by q*16 KiB and XORs the result into the range's accumulator
-// (atomicXor, order-free). The range's last window stores its R0 separately. A per-range finish
-// kernel applies the last window's length, the init term, the (< 16) tail bytes, the xorout and,
-// for files, the trailer compare.
+// 16-byte boundary): lane l folds the 128-byte run that ends 128*l bytes before the overlap's end
+// (8 aligned dwordx4 loads straight into registers, bytes before the range masked to zero) with
+// slice-by-4 lookups, shifts it by 128*l with the shift-by-16*2^j operators (bits of l), and the
+// wave XORs the lanes. While a window is folded, the next one's loads are in flight when the same
+// range covers it. The wave folds the parts of one range in order (Horner: acc = Z_d(acc) ^ part,
+// d = the distance between the two parts' ends, one window for whole windows), and when it leaves
+// the range shifts acc to the end of the range's main part and XORs it into the range's
+// accumulator (atomicXor, order-free: one atomic per wave and range). The current range's
+// geometry stays in registers, so whole windows of one range load no extents. A per-range finish
+// kernel applies the init term, the (< 16) tail bytes, the xorout and, for files, the trailer
+// compare.
 //
 // The hot lookups are conflict-free: the slice-by-4 tables sit in LDS replicated 32 times, word
 // ((t*256 + b)*32 + r) = T_t[b], and lane l reads replica l % 32, so a ds_read_b32 of 32 lanes
@@ -46,14 +49,18 @@ typedef uint64_t u64;
 constexpr int kWave = 64;
 constexpr int kWaves = 16;
 constexpr int kThreads = kWave * kWaves;
-constexpr u32 kLaneRun = 256;                      // bytes folded per lane per window
-constexpr int kWinLog = 14;
-constexpr u64 kWin = 1ull << kWinLog;              // 16 KiB = 64 lanes x 256 B
+#ifndef TPZ_CRC_RUN_LOG
+#define TPZ_CRC_RUN_LOG 7                          // diagnostic builds vary the lane run
+#endif
+constexpr u32 kLaneRun = 1u << TPZ_CRC_RUN_LOG;    // bytes folded per lane per window (128)
+constexpr int kWinLog = TPZ_CRC_RUN_LOG + 6;
+constexpr u64 kWin = 1ull << kWinLog;              // 8 KiB = 64 lanes x 128 B
 static_assert(kWin == (u64)kLaneRun * kWave, "window");
-constexpr int kJLane = 4;                          // lane l shifts by 256*l: operators j = 4..9
+constexpr int kJLane = TPZ_CRC_RUN_LOG - 4;        // lane l shifts by 128*l: operators j = 3..8
 constexpr int kLaneOps = 6;
+constexpr int kJWin = kWinLog - 4;                 // the shift-by-one-window operator
 constexpr int kRepWords = kCrcRepWords;            // 4 x 256 x 32
-constexpr int kLdsWords = kRepWords + kLaneOps * 4 * 256;
+constexpr int kLdsWords = kRepWords + (kLaneOps + 1) * 4 * 256;  // + the window op
 static_assert(kLdsWords * 4 <= 163840, "LDS");
 
 __device__ __forceinline__ u32 lane_id() {
@@ -120,11 +127,25 @@ struct CrcParams {
   u64 n_windows;        // windows of the aligned space covering [0, src_bytes + delta)
   const u32* tables;    // global tables (ids above)
   const u32* rep;       // replicated slice-by-4 tables
-  u32* acc;             // per range: XOR of Z_{q*W}(R0(window part)) over non-last windows
-  u32* acc_last;        // per range: R0 of the main part's last window
+  u32* acc;             // per range: R0 of the main part (XOR of the waves' shifted folds)
   u32* crc;             // out
   uint8_t* status;      // out (verify mode) or null
 };
+
+// Z_n(a) for any n < 16 * 2^kRangeShiftOps: the n mod 16 bytes with the slice tables, then the
+// shift-by-16*2^j operators for the bits of n / 16.
+__device__ __forceinline__ u32 zshift_any(const u32* g, u32 a, u64 n) {
+  const u32 k = (u32)(n & 15);
+  if (k) {
+    u32 r = k >= 4 ? 0u : (a >> (8 * k));
+    for (u32 i = 0; i < 4 && i < k; i++) r ^= g[(k - 1 - i) * 256 + ((a >> (8 * i)) & 0xFF)];
+    a = r;
+  }
+  u64 m = n >> 4;
+  for (int j = 0; m; j++, m >>= 1)
+    if (m & 1) a = zop(gop(g, j), a);
+  return a;
+}
 
 // ------------------------------------------------------------------ window kernel
 __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
@@ -132,13 +153,16 @@ __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
   {
     const uint4* g = reinterpret_cast<const uint4*>(p.rep);
     const uint4* o = reinterpret_cast<const uint4*>(gop(p.tables, kJLane));
+    const uint4* w = reinterpret_cast<const uint4*>(gop(p.tables, kJWin));
     uint4* d = reinterpret_cast<uint4*>(lds);
+    constexpr int kRep4 = kRepWords / 4, kOps4 = kLaneOps * 256;
     for (int i = threadIdx.x; i < kLdsWords / 4; i += kThreads)
-      d[i] = i < kRepWords / 4 ? g[i] : o[i - kRepWords / 4];
+      d[i] = i < kRep4 ? g[i] : (i < kRep4 + kOps4 ? o[i - kRep4] : w[i - kRep4 - kOps4]);
     __syncthreads();
   }
   const u32* rep = lds;
-  const u32* lop = lds + kRepWords;  // lane-shift operator k at lop + 1024 k
+  const u32* lop = lds + kRepWords;                 // lane-shift operator k at lop + 1024 k
+  const u32* wop = lop + 1024 * kLaneOps;           // shift by one window
   const u32 lane = lane_id();
   const u32 rl = lane & 31u;
   const u64 nw = (u64)gridDim.x * kWaves;
@@ -159,68 +183,92 @@ __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
     }
     r = lo;
   }
+  u32 cur = ~0u, acc = 0;   // the range being folded, R0 of its parts so far ending at `last`
+  u64 last = 0, cur_A = 0;
+  // the next window's runs, loaded while the current one is folded when the range covers it
+  constexpr int kC = (int)(kLaneRun / 16);
+  uint4 pf[kC];
+  u64 pf_g = ~0ull;
+  u32 pf_r = ~0u;
+  // range r's geometry and end stay in registers: consecutive windows of one range (the common
+  // case, files are MiBs) need no extent loads; range r + 1 starts where r ends
+  u64 hiX = uni64(p.ext[r + 1]) + p.delta;
+  RangeGeo Gr = range_geo(uni64(p.ext[r]), hiX - p.delta, p.delta, p.trailer);
   for (u64 g = g0; g < g1 && r < p.n_ranges; g++) {
     const u64 w0 = g << kWinLog, w1 = w0 + kWin;
-    while (r < p.n_ranges && uni64(p.ext[r + 1]) + p.delta <= w0) r++;
-    for (u32 rr = r; rr < p.n_ranges; rr++) {
-      const RangeGeo G = range_geo(uni64(p.ext[rr]), uni64(p.ext[rr + 1]), p.delta, p.trailer);
-      if (G.s >= w1) break;
+    while (hiX <= w0 && r + 1 < p.n_ranges) {
+      r++;
+      const u64 lo = hiX - p.delta;
+      hiX = uni64(p.ext[r + 1]) + p.delta;
+      Gr = range_geo(lo, hiX - p.delta, p.delta, p.trailer);
+    }
+    if (hiX <= w0) break;
+    u32 rr = r;
+    RangeGeo G = Gr;
+    u64 rhi = hiX;
+    for (;;) {
       const u64 a = max(w0, G.s), b = min(w1, G.A);
-      if (!G.valid || a >= b) continue;
-      // lane l: the 256-byte run ending 256*l bytes before b (b is 16-aligned); chunks wholly
-      // before the range are not loaded (their address may lie before the buffer) and read as 0
-      const int64_t run0 = (int64_t)b - (int64_t)kLaneRun * (int64_t)(lane + 1);
-      uint4 v[kLaneRun / 16];
+      if (G.valid && a < b) {
+        // lane l: the run ending kLaneRun*l bytes before b (b is 16-aligned); chunks wholly
+        // before the range are not loaded (their address may lie before the buffer) and read as 0
+        const int64_t run0 = (int64_t)b - (int64_t)kLaneRun * (int64_t)(lane + 1);
+        uint4 v[kC];
+        if (pf_g == g && pf_r == rr && a == w0 && b == w1) {
 #pragma unroll
-      for (int c = 0; c < (int)(kLaneRun / 16); c++) {
-        const int64_t x = run0 + 16 * c;
-        v[c] = make_uint4(0, 0, 0, 0);
-        if (x + 16 > (int64_t)a) {
-          v[c] = *reinterpret_cast<const uint4*>(p.base + x);
-          if (x < (int64_t)a) v[c] = zero_below(v[c], (u32)((int64_t)a - x));
+          for (int c = 0; c < kC; c++) v[c] = pf[c];
+        } else {
+#pragma unroll
+          for (int c = 0; c < kC; c++) {
+            const int64_t x = run0 + 16 * c;
+            v[c] = make_uint4(0, 0, 0, 0);
+            if (x + 16 > (int64_t)a) {
+              v[c] = *reinterpret_cast<const uint4*>(p.base + x);
+              if (x < (int64_t)a) v[c] = zero_below(v[c], (u32)((int64_t)a - x));
+            }
+          }
         }
-      }
-      u32 R = 0;
+        if (g + 1 < g1 && G.A >= w1 + kWin) {       // the range covers the next window: load it
+          const uint8_t* nx = p.base + w1 + kWin - (u64)kLaneRun * (lane + 1);
 #pragma unroll
-      for (int c = 0; c < (int)(kLaneRun / 16); c++) {
-        R = slice4(rep, rl, R ^ v[c].x);
-        R = slice4(rep, rl, R ^ v[c].y);
-        R = slice4(rep, rl, R ^ v[c].z);
-        R = slice4(rep, rl, R ^ v[c].w);
-      }
-      // lane l sits 256*l bytes before b: Z_{256 l} = product of Z_{256*2^k} for the bits k of l
+          for (int c = 0; c < kC; c++) pf[c] = *reinterpret_cast<const uint4*>(nx + 16 * c);
+          pf_g = g + 1;
+          pf_r = rr;
+        }
+        u32 R = 0;
 #pragma unroll
-      for (int k = 0; k < kLaneOps; k++)
-        if (lane & (1u << k)) R = zop(lop + 1024 * k, R);
-      for (int o = 32; o >= 1; o >>= 1) R ^= __shfl_xor(R, o);
-      R = uni(R);
-      if (b == G.A) {
-        if (lane == 0) p.acc_last[rr] = R;
-      } else {
-        // q whole windows lie between this window and the range's last main window
-        const u64 glast = (G.A - 1) >> kWinLog;
-        u64 q = glast - g - 1;
-        for (int k = 0; q; k++, q >>= 1)
-          if (q & 1) R = zop(gop(p.tables, kWinLog - 4 + k), R);
-        if (lane == 0) atomicXor(p.acc + rr, R);
+        for (int c = 0; c < kC; c++) {
+          R = slice4(rep, rl, R ^ v[c].x);
+          R = slice4(rep, rl, R ^ v[c].y);
+          R = slice4(rep, rl, R ^ v[c].z);
+          R = slice4(rep, rl, R ^ v[c].w);
+        }
+        // lane l sits kLaneRun*l bytes before b: Z_{run*l} = product of Z_{run*2^k} for bits k of l
+#pragma unroll
+        for (int k = 0; k < kLaneOps; k++)
+          if (lane & (1u << k)) R = zop(lop + 1024 * k, R);
+        for (int o = 32; o >= 1; o >>= 1) R ^= __shfl_xor(R, o);
+        R = uni(R);
+        if (rr == cur) {
+          // the previous part ended at `last` = w0; this one ends at b
+          acc = (b - last == kWin ? zop(wop, acc) : zshift_any(p.tables, acc, b - last)) ^ R;
+        } else {
+          if (cur != ~0u && lane == 0)
+            atomicXor(p.acc + cur, zshift_any(p.tables, acc, cur_A - last));
+          cur = rr;
+          cur_A = G.A;
+          acc = R;
+        }
+        last = b;
       }
+      // the next range starts at this one's end: in this window only if that is before w1
+      if (rhi >= w1 || rr + 1 >= p.n_ranges) break;
+      rr++;
+      const u64 lo = rhi - p.delta;
+      rhi = uni64(p.ext[rr + 1]) + p.delta;
+      G = range_geo(lo, rhi - p.delta, p.delta, p.trailer);
     }
   }
-}
-
-// Z_n(a) for any n < 16 * 2^kRangeShiftOps: the n mod 16 bytes with the slice tables, then the
-// shift-by-16*2^j operators for the bits of n / 16.
-__device__ __forceinline__ u32 zshift_any(const u32* g, u32 a, u64 n) {
-  const u32 k = (u32)(n & 15);
-  if (k) {
-    u32 r = k >= 4 ? 0u : (a >> (8 * k));
-    for (u32 i = 0; i < 4 && i < k; i++) r ^= g[(k - 1 - i) * 256 + ((a >> (8 * i)) & 0xFF)];
-    a = r;
-  }
-  u64 m = n >> 4;
-  for (int j = 0; m; j++, m >>= 1)
-    if (m & 1) a = zop(gop(g, j), a);
-  return a;
+  if (cur != ~0u && lane == 0) atomicXor(p.acc + cur, zshift_any(p.tables, acc, cur_A - last));
 }
 
 // ------------------------------------------------------------------ finish kernel
@@ -233,11 +281,7 @@ __global__ __launch_bounds__(256) void crc_finish_kernel(CrcParams p) {
     if (p.status) p.status[r] = TPZ_BLOCK_MALFORMED;
     return;
   }
-  u32 R = 0;
-  if (G.A > G.s) {
-    const u64 glast = (G.A - 1) >> kWinLog;
-    R = zshift_any(p.tables, p.acc[r], G.A - (glast << kWinLog)) ^ p.acc_last[r];
-  }
+  u32 R = p.acc[r];                    // R0 of the main part [s, A)
   R ^= zshift_any(p.tables, 0xFFFFFFFFu, G.A - G.s);  // init 0xFFFFFFFF ahead of the main part
   for (u64 x = G.A; x < G.e; x++) R = (R >> 8) ^ p.tables[(R ^ p.base[x]) & 0xFF];
   const u32 crc = ~R;
@@ -263,7 +307,6 @@ void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream) {
   p.tables = a.tables;
   p.rep = a.rep;
   p.acc = a.acc;
-  p.acc_last = a.acc_last;
   p.crc = a.crc;
   p.status = a.status;
   // enough waves for the windows, at most one 16-wave workgroup per CU

@@ -65,7 +65,6 @@ struct CrcLaunch {
   const uint32_t* tables; // kRangeTables x 256
   const uint32_t* rep;    // kCrcRepWords
   uint32_t* acc;          // workspace: n_ranges, zeroed before the launch
-  uint32_t* acc_last;     // workspace: n_ranges, zeroed before the launch
   uint32_t* crc;
   uint8_t* status;        // null for plain ranges
   uint32_t num_cus;
