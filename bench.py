@@ -249,15 +249,17 @@ def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10
             "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-def snappy_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, nb: int = 1 << 18,
-                steps: int = 10) -> dict:
-    """The same blocks with the Snappy codec (topazdb's default, src/opt.rs:48): device codec step
-    (tpz_decompress_blocks, compress.rs:104-107) + tpz_decode_blocks per step, inputs resident.
-    Checks that the decompressed batch equals the Uncompress one. Not the metric; DESIGN.md §4."""
+def codec_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, codec: str = "snappy",
+               nb: int = 1 << 18, steps: int = 10) -> dict:
+    """The same blocks with the Snappy codec (topazdb's default, src/opt.rs:48) or the Lz4 one:
+    device codec step (tpz_decompress_blocks, compress.rs:104-111) + tpz_decode_blocks per step,
+    inputs resident. Checks that the decompressed batch equals the Uncompress one. Not the
+    metric; DESIGN.md §4."""
     from topazdb_amd.batch import decompress_batch
     nb = min(nb, len(ext) - 1)
     raw = src[:int(ext[nb])]
-    s2, e2 = synth.snappy_blocks(raw, ext[:nb + 1])
+    enc = synth.snappy_blocks if codec == "snappy" else synth.lz4_blocks
+    s2, e2 = enc(raw, ext[:nb + 1])
     batch = DeviceBatch(s2, e2, dev.index)
     out, st = decompress_batch(ctx, batch)
     torch.cuda.synchronize(dev)
@@ -266,7 +268,13 @@ def snappy_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, nb: int = 1 << 18,
     cols = SlottedColumns(nb, out.src_bytes, dev.index)
     stream = torch.cuda.current_stream(dev)
 
-    def codec():
+    size = torch.empty(nb, dtype=torch.int64, device=dev)
+
+    def codec():  # the whole codec step: sizes, their prefix sum, decompression
+        ctx.decompressed_sizes_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb,
+                                    batch.src_bytes, size.data_ptr(), stream.cuda_stream)
+        with torch.cuda.stream(stream):
+            torch.cumsum(size, 0, out=out.ext[1:nb + 1])
         ctx.decompress_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
                             out.src.data_ptr(), out.ext.data_ptr(), st.data_ptr(),
                             stream.cuda_stream)
@@ -281,7 +289,7 @@ def snappy_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, nb: int = 1 << 18,
         decode_batch(ctx, out, cols, stream)
     ev[2].record(stream)
     torch.cuda.synchronize(dev)
-    assert int((cols.status[:nb] != 0).sum()) == 0, "snappy blocks did not decode"
+    assert int((cols.status[:nb] != 0).sum()) == 0, codec + " blocks did not decode"
     ms_codec = ev[0].elapsed_time(ev[1]) / steps
     ms_dec = ev[1].elapsed_time(ev[2]) / steps
     t = (ms_codec + ms_dec) * 1e-3
@@ -341,6 +349,7 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-file-crc", action="store_true")
     ap.add_argument("--no-snappy", action="store_true")
+    ap.add_argument("--no-lz4", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -407,12 +416,17 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"file CRC measurement failed: {ex}")
 
-    snappy = None
+    snappy = lz4 = None
     if rank == 0 and not args.no_snappy:
         try:
-            snappy = snappy_rate(ctx, src, ext, dev)
+            snappy = codec_rate(ctx, src, ext, dev, "snappy")
         except Exception as ex:  # reported, never the metric
             log(rank, f"snappy measurement failed: {ex}")
+    if rank == 0 and not args.no_lz4:
+        try:
+            lz4 = codec_rate(ctx, src, ext, dev, "lz4")
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"lz4 measurement failed: {ex}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -454,6 +468,7 @@ def main():
             "e2e_h2d_d2h_gib_s": e2e,
             "file_crc": fcrc,
             "snappy": snappy,
+            "lz4": lz4,
         }
         print(json.dumps(out), flush=True)
     if dist:

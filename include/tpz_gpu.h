@@ -13,7 +13,8 @@
  *   tpz_crc32_ranges        checksum::calculate_checksum (src/checksum.rs:6-10) over many ranges
  *   tpz_verify_files        FileObject::open's whole-file CRC (src/table/file_object.rs:57-78),
  *                           batched over SST file images (SsTable::open, src/table.rs:91-112)
- *   tpz_decompress_blocks   compress::decode's snappy step (src/block/compress.rs:104-107)
+ *   tpz_decompress_blocks   compress::decode's codec step: snappy (src/block/compress.rs:104-107)
+ *                           and lz4 (:108-111) blocks to their Uncompress form
  *   tpz_format_block_error  the reference's error strings (checksum.rs:18-21, compress.rs:97,102)
  *
  * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
@@ -48,7 +49,8 @@ typedef enum {
   TPZ_BLOCK_OK = 0,                /* Ok(Block); all entries decoded                         */
   TPZ_BLOCK_EMPTY = 1,             /* Err("data is empty")          compress.rs:96-98        */
   TPZ_BLOCK_BAD_TAG = 2,           /* Err("invaild data")           compress.rs:102          */
-  TPZ_BLOCK_UNSUPPORTED_CODEC = 3, /* tag 2 (snappy) / 3 (lz4): not decoded on device yet    */
+  TPZ_BLOCK_UNSUPPORTED_CODEC = 3, /* tag 2 (snappy) / 3 (lz4) given to tpz_decode_blocks
+                                      without the codec step (tpz_decompress_blocks) first    */
   TPZ_BLOCK_CHECKSUM_MISMATCH = 4, /* Err("checksum: expected E, actual A") checksum.rs:18-21 */
   TPZ_BLOCK_MALFORMED = 5,         /* CRC-valid, but the reference panics on it: payload too
                                       short for n/offsets (block.rs:49-59) or an entry out of
@@ -60,7 +62,7 @@ typedef enum {
                                       topazdb's BlockBuilder never writes such a block.      */
   TPZ_BLOCK_TOO_LARGE = 7,         /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
                                       block_size <= 64 KiB BlockBuilder emits); for a snappy
-                                      block: compressed > 64 KiB - 31 or uncompressed >
+                                      or lz4 block: compressed > 64 KiB - 31 or uncompressed >
                                       TPZ_MAX_BLOCK_BYTES - 1                                */
   TPZ_BLOCK_CODEC_ERROR = 8        /* Err of the codec: snap's decompress_vec rejects the
                                       stream (compress.rs:104-107)                           */
@@ -170,20 +172,23 @@ tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
                          uint8_t* d_status, void* stream);
 
 /* ---- codec step of compress::decode (src/block/compress.rs:95-113) ------------------------
- * Snappy (tag 2) blocks are decompressed on the device into their Uncompress (tag 1) form, so
- * tpz_decode_blocks then verifies and decodes them like any block:
+ * Snappy (tag 2) and LZ4 (tag 3) blocks are decompressed on the device into their Uncompress
+ * (tag 1) form, so tpz_decode_blocks then verifies and decodes them like any block:
  *   1. tpz_decompressed_sizes: d_size[i] = the length block i has once decompressed and
- *      re-tagged: the snappy preamble's length + 1 for a tag 2 block (0 if the preamble is
- *      invalid, 1 if the length exceeds TPZ_MAX_BLOCK_BYTES - 1), the block's own length for
- *      any other block.
+ *      re-tagged: for tag 2 the snappy preamble's length + 1 (0 if the preamble is invalid, 1
+ *      if the length exceeds TPZ_MAX_BLOCK_BYTES - 1); for tag 3 the length LZ4_decompress_safe
+ *      decodes + 1 (lz4::block::decompress keeps only the decoded bytes, which may be fewer than
+ *      the size prefix; 1 for an Err or a block past the device limits); the block's own
+ *      length for any other block.
  *   2. the caller forms d_dst_ext = exclusive prefix sums of d_size (n_blocks + 1 entries) and
  *      allocates d_dst (d_dst_ext[n] bytes).
  *   3. tpz_decompress_blocks writes block i's uncompressed form to d_dst[d_dst_ext[i] ..
  *      d_dst_ext[i+1]) (other tags are copied unchanged) and d_status[i] = TPZ_BLOCK_OK,
- *      TPZ_BLOCK_CODEC_ERROR (snap's Err) or TPZ_BLOCK_TOO_LARGE. A failed block's range ends in
- *      tag 0, so decoding it reports BAD_TAG; its d_status is the reference's outcome.
+ *      TPZ_BLOCK_CODEC_ERROR (the codec's Err) or TPZ_BLOCK_TOO_LARGE. A failed block's range
+ *      ends in tag 0, so decoding it reports BAD_TAG; its d_status is the reference's outcome.
  *   4. tpz_decode_blocks over (d_dst, d_dst_ext).
- * LZ4 (tag 3) blocks are copied unchanged for now (the decode reports UNSUPPORTED_CODEC). */
+ * LZ4 acceptance is liblz4 1.9.3's LZ4_decompress_safe (the library the reference's lz4 crate
+ * binds; restated in oracle/tpz_lz4.c and pinned against liblz4 in tests/test_lz4_oracle.py). */
 tpz_err tpz_decompressed_sizes(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_size,
                                void* stream);
 tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_dst,
@@ -207,6 +212,13 @@ int tpz_build_blocks(const uint8_t* h_keys, const uint64_t* h_kpos, const uint8_
 int tpz_snappy_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64_t n_blocks,
                              uint8_t* h_out, uint64_t out_cap, uint64_t* h_out_ext,
                              uint64_t* out_len);
+/* compress::encode with CompressOptions::Lz4 (src/block/compress.rs:73-77): every tag-1 block
+ * becomes u32 LE size (payload | crc) | lz4_block(payload | crc) | 3 (lz4::block::compress with
+ * prepend_size), other blocks unchanged. Host memory only; out_cap >= 32 * n_blocks +
+ * 2 * h_ext[n_blocks] always suffices. */
+int tpz_lz4_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64_t n_blocks,
+                          uint8_t* h_out, uint64_t out_cap, uint64_t* h_out_ext,
+                          uint64_t* out_len);
 /* CRC-32/ISO-HDLC on the host (checksum::calculate_checksum, src/checksum.rs:6-10). */
 uint32_t tpz_host_crc32(const uint8_t* h_buf, uint64_t len);
 

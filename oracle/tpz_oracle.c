@@ -132,6 +132,22 @@ static int codec_step(const uint8_t* b, size_t len, uint8_t** buf, const uint8_t
   *buf = NULL;
   *out = b;
   *out_len = len;
+  if (len != 0 && b[len - 1] == 3) {
+    /* lz4::block::decompress(data, None) (compress.rs:108-111): size prefix, then
+     * LZ4_decompress_safe; the output is the decoded bytes (possibly fewer than the prefix) */
+    int64_t size = 0;
+    if (tpzo_lz4_prefixed_size(b, len - 1, &size) != 0) return TPZO_CODEC;
+    const int64_t r = tpzo_lz4_decompress_safe(b + 4, (int64_t)len - 5, NULL, size);
+    if (r < 0) return TPZO_CODEC;
+    /* the device's limits (TPZ_MAX_BLOCK_BYTES; a 64 KiB staging window less 32 bytes) */
+    if (r + 1 > 94192 || len - 1 > 65504) return TPZO_TOO_LARGE;
+    *buf = (uint8_t*)malloc((size_t)r + 1);
+    tpzo_lz4_decompress_safe(b + 4, (int64_t)len - 5, *buf, size);
+    (*buf)[r] = 1;
+    *out = *buf;
+    *out_len = (size_t)r + 1;
+    return 0;
+  }
   if (len == 0 || b[len - 1] != 2) return 0;
   uint64_t want = 0;
   if (tpzo_snappy_uncompressed_len(b, len - 1, &want) != 0) return TPZO_CODEC;

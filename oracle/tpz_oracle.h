@@ -27,12 +27,13 @@ enum {
   TPZO_OK = 0,          /* Block::decode Ok                                   */
   TPZO_EMPTY = 1,       /* Err("data is empty")      src/block/compress.rs:96-98 */
   TPZO_BAD_TAG = 2,     /* Err("invaild data")       src/block/compress.rs:102   */
-  TPZO_UNSUPPORTED = 3, /* tag 3: lz4                src/block/compress.rs:108-111 */
+  TPZO_UNSUPPORTED = 3, /* no longer produced: lz4 (tag 3) is decoded (tpz_lz4.c) */
   TPZO_CHECKSUM = 4,    /* Err("checksum: ...")      src/checksum.rs:12-21       */
   TPZO_MALFORMED = 5,   /* the reference panics      src/block.rs:49-59, iterator.rs:74-82 */
   TPZO_OVERLAP = 6,     /* decodes in the reference; exceeds the device's per-block slot */
-  TPZO_TOO_LARGE = 7,   /* a snappy block decompressing past the device limit (94192 B) */
-  TPZO_CODEC = 8        /* snap's decompress_vec returns Err  src/block/compress.rs:104-107 */
+  TPZO_TOO_LARGE = 7,   /* a snappy/lz4 block past the device limits (94192 B out, 64 KiB - 31 in) */
+  TPZO_CODEC = 8        /* the codec returns Err: snap's decompress_vec (compress.rs:104-107),
+                           lz4::block::decompress (compress.rs:108-111)                     */
 };
 
 /* CRC-32/ISO-HDLC bit by bit (crc32fast's function): src/checksum.rs:6-10. */
@@ -84,6 +85,17 @@ int tpzo_snappy_uncompressed_len(const uint8_t* src, size_t n, uint64_t* len);
 int tpzo_snappy_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
                            uint64_t* out_len);
 size_t tpzo_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst, int mode);
+
+/* ---- LZ4 block format (tpz_lz4.c; codec 3, src/block/compress.rs:73-77, 108-111) --------
+ * tpzo_lz4_decompress_safe: LZ4_decompress_safe as liblz4 1.9.3 accepts (out may be NULL:
+ * validity and length only); returns the decoded length or -1.
+ * tpzo_lz4_prefixed_size: lz4::block::decompress's size-prefix checks; 0 or -1.
+ * tpzo_lz4_compress: a valid raw block (dst >= 16 + n + n / 255) for fixtures; mode 1 =
+ * literals only. */
+int64_t tpzo_lz4_decompress_safe(const uint8_t* in, int64_t src_size, uint8_t* out,
+                                 int64_t out_size);
+int tpzo_lz4_prefixed_size(const uint8_t* src, size_t n, int64_t* size);
+size_t tpzo_lz4_compress(const uint8_t* src, size_t n, uint8_t* dst, int mode);
 
 /* ---- CPU baseline: benches/sstable_iter_read.rs:60-79 restated --------------------------
  * SsTableIterator::create_and_seek_to_first + `while is_valid { next }` over SST files on

@@ -49,6 +49,11 @@ def lib() -> C.CDLL:
         L.tpzo_snappy_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, u64p]
         L.tpzo_snappy_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
         L.tpzo_snappy_compress.restype = C.c_size_t
+        L.tpzo_lz4_decompress_safe.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+        L.tpzo_lz4_decompress_safe.restype = C.c_int64
+        L.tpzo_lz4_prefixed_size.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_int64)]
+        L.tpzo_lz4_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
+        L.tpzo_lz4_compress.restype = C.c_size_t
         L.tpzo_bench_iter_read.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
                                            C.c_uint32, u64p, u64p]
         L.tpzo_bench_iter_read.restype = C.c_double
@@ -199,12 +204,58 @@ def snappy_block(tag1_block: bytes, mode: int = 0) -> bytes:
     return snappy_compress(tag1_block[:-1], mode) + b"\x02"
 
 
+# ---- lz4 (oracle/tpz_lz4.c) ---------------------------------------------------------------
+def lz4_decompress_safe(src: bytes, out_size: int):
+    """The restated LZ4_decompress_safe (liblz4 1.9.3): decoded bytes or None."""
+    s = np.frombuffer(src or b"\0", np.uint8)
+    dst = np.zeros(max(out_size, 1), np.uint8)
+    r = lib().tpzo_lz4_decompress_safe(_ptr(s), len(src), _ptr(dst), out_size)
+    return None if r < 0 else dst[:r].tobytes()
+
+
+def lz4_compress(b: bytes, mode: int = 0) -> bytes:
+    src = np.frombuffer(b or b"\0", np.uint8)
+    dst = np.zeros(16 + len(b) + len(b) // 255 + 16, np.uint8)
+    n = lib().tpzo_lz4_compress(_ptr(src), len(b), _ptr(dst), mode)
+    return dst[:n].tobytes()
+
+
+def lz4_block_decompress(b: bytes):
+    """lz4::block::decompress(b, None) (src/block/compress.rs:108-111): bytes or None."""
+    s = np.frombuffer(b or b"\0", np.uint8)
+    size = C.c_int64()
+    if lib().tpzo_lz4_prefixed_size(_ptr(s), len(b), C.byref(size)) != 0:
+        return None
+    return lz4_decompress_safe(b[4:], size.value)
+
+
+def lz4_block(tag1_block: bytes, mode: int = 0) -> bytes:
+    """compress::encode with CompressOptions::Lz4 (src/block/compress.rs:73-77): size prefix +
+    LZ4 block + tag 3, over the bytes an Uncompress block holds before its tag."""
+    assert tag1_block[-1] == 1
+    body = tag1_block[:-1]
+    return len(body).to_bytes(4, "little") + lz4_compress(body, mode) + b"\x03"
+
+
+def liblz4():
+    """The system liblz4 (1.9.3 in this image; the library the lz4 crate binds), or None."""
+    try:
+        L = C.CDLL("liblz4.so.1")
+    except OSError:
+        return None
+    L.LZ4_decompress_safe.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
+    L.LZ4_compress_default.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
+    L.LZ4_compressBound.argtypes = [C.c_int]
+    L.LZ4_versionNumber.restype = C.c_int
+    return L
+
+
 def decompress_block(blk: bytes):
-    """compress::decode's codec step (src/block/compress.rs:95-113) for tag 2, re-tagged as an
-    Uncompress block: (status, bytes). Other tags pass through unchanged with status OK."""
-    if len(blk) == 0 or blk[-1] != 2:
+    """compress::decode's codec step (src/block/compress.rs:95-113) for tags 2 and 3, re-tagged
+    as an Uncompress block: (status, bytes). Other tags pass through unchanged with status OK."""
+    if len(blk) == 0 or blk[-1] not in (2, 3):
         return OK, blk
-    d = snappy_decompress(blk[:-1])
+    d = snappy_decompress(blk[:-1]) if blk[-1] == 2 else lz4_block_decompress(blk[:-1])
     if d is None:
         return CODEC, b""
     return OK, d + b"\x01"

@@ -189,6 +189,183 @@ def snappy_compress(b: bytes) -> bytes:
     return bytes(out)
 
 
+# --------------------------------------------------------------------------- LZ4 block format
+# The reference's codec 3 calls the `lz4` crate (liblz4): lz4::block::compress(data, None, true)
+# (4-byte LE size prefix, compress.rs:73-77) and lz4::block::decompress(data, None)
+# (compress.rs:108-111). Restated from LZ4_decompress_generic as liblz4 1.9.3 (this image)
+# builds LZ4_decompress_safe: the fast loop while 64 output bytes remain, then the safe loop
+# with its shortcut. main() cross-checks every LZ4 fixture against liblz4 when it loads.
+def lz4_decompress_safe(src: bytes, out_size: int):
+    """LZ4_decompress_safe(src, dst, len(src), out_size): the decoded bytes, or None (< 0)."""
+    if out_size == 0:
+        return b"" if (len(src) == 1 and src[0] == 0) else None
+    if len(src) == 0:
+        return None
+    iend, oend = len(src), out_size
+    out = bytearray()
+    ip = 0
+
+    def match(off, n):
+        if off == 0:
+            out.extend(bytes(n))                 # liblz4 1.9.3 fills an offset-0 match with 0
+        else:
+            for _ in range(n):
+                out.append(out[-off])
+
+    def ext_len(ip, limit, fatal):
+        """read_variable_length; returns (added, ip, failed)."""
+        n = 0
+        while True:
+            s = src[ip]
+            ip += 1
+            n += s
+            if ip >= limit:
+                return n, ip, fatal
+            if s != 255:
+                return n, ip, False
+
+    state = "fast" if oend >= 64 else "safe"
+    token = lit = ml = off = 0
+    while state == "fast":
+        token = src[ip]
+        ip += 1
+        lit = token >> 4
+        if lit == 15:
+            if ip >= iend - 15:
+                return None
+            add, ip, _ = ext_len(ip, iend - 15, False)
+            lit += add
+            if len(out) + lit > oend - 32 or ip + lit > iend - 32:
+                state = "lit"
+                break
+        elif ip > iend - 17:
+            state = "lit"
+            break
+        out += src[ip:ip + lit]
+        ip += lit
+        off = src[ip] | src[ip + 1] << 8
+        ip += 2
+        ml = token & 15
+        if ml == 15:
+            if off > len(out):
+                return None
+            add, ip, bad = ext_len(ip, iend - 4, True)
+            if bad:
+                return None
+            ml += add + 4
+            if len(out) + ml >= oend - 64:
+                state = "match"
+                break
+        else:
+            ml += 4
+            if len(out) + ml >= oend - 64:
+                state = "match"
+                break
+        if off > len(out):
+            return None
+        match(off, ml)
+    while True:
+        if state == "safe":
+            token = src[ip]
+            ip += 1
+            lit = token >> 4
+            if lit != 15 and ip < iend - 16 and len(out) <= oend - 32:
+                out += src[ip:ip + lit]
+                ip += lit
+                ml = token & 15
+                off = src[ip] | src[ip + 1] << 8
+                ip += 2
+                if ml != 15 and off >= 8 and off <= len(out):
+                    match(off, ml + 4)
+                    continue
+                state = "copy_match"
+            else:
+                if lit == 15:
+                    if ip >= iend - 15:
+                        return None
+                    add, ip, _ = ext_len(ip, iend - 15, False)
+                    lit += add
+                state = "lit"
+        if state == "lit":
+            if len(out) + lit > oend - 12 or ip + lit > iend - 8:
+                if ip + lit != iend or len(out) + lit > oend:
+                    return None
+                out += src[ip:ip + lit]
+                return bytes(out)
+            out += src[ip:ip + lit]
+            ip += lit
+            off = src[ip] | src[ip + 1] << 8
+            ip += 2
+            ml = token & 15
+            state = "copy_match"
+        if state == "copy_match":
+            if ml == 15:
+                add, ip, bad = ext_len(ip, iend - 4, True)
+                if bad:
+                    return None
+                ml += add
+            ml += 4
+            state = "match"
+        if state == "match":
+            if off > len(out) or len(out) + ml > oend - 5:
+                return None
+            match(off, ml)
+            state = "safe"
+
+
+def lz4_block_decompress(b: bytes):
+    """lz4::block::decompress(b, None): size prefix checks, then LZ4_decompress_safe."""
+    if len(b) < 4:
+        return None
+    size = struct.unpack("<i", b[:4])[0]
+    if size < 0 or size > 0x7E000000:
+        return None
+    return lz4_decompress_safe(b[4:], size)
+
+
+def lz4_compress(b: bytes) -> bytes:
+    """A valid LZ4 block for b (greedy 4-byte matches; the last match starts >= 12 bytes before
+    the end and the last 5 bytes are literals)."""
+    out = bytearray()
+
+    def seq(lits: bytes, off: int, mlen: int):
+        ll, mc = len(lits), mlen - 4
+        out.append((min(ll, 15) << 4) | (min(mc, 15) if mlen else 0))
+        if ll >= 15:
+            r = ll - 15
+            while r >= 255:
+                out.append(255)
+                r -= 255
+            out.append(r)
+        out.extend(lits)
+        if not mlen:
+            return
+        out.extend(off.to_bytes(2, "little"))
+        if mc >= 15:
+            r = mc - 15
+            while r >= 255:
+                out.append(255)
+                r -= 255
+            out.append(r)
+
+    n, anchor, i, seen = len(b), 0, 0, {}
+    while i + 4 <= n and i < n - 12:
+        k = b[i:i + 4]
+        c = seen.get(k)
+        seen[k] = i
+        if c is None or i - c > 65535:
+            i += 1
+            continue
+        m = 4
+        while i + m < n - 5 and b[c + m] == b[i + m]:
+            m += 1
+        seq(b[anchor:i], i - c, m)
+        i += m
+        anchor = i
+    seq(b[anchor:], 0, 0)
+    return bytes(out)
+
+
 def encode_block(offsets: list[int], data: bytes, tag: int = TAG_NONE) -> bytes:
     """Block::encode (src/block.rs:31-44) with the Uncompress (compress.rs:85-89) or Snappy
     (compress.rs:66-71) codec."""
@@ -196,6 +373,8 @@ def encode_block(offsets: list[int], data: bytes, tag: int = TAG_NONE) -> bytes:
     body = p + struct.pack(">I", crc32(p))
     if tag == TAG_SNAPPY:
         return snappy_compress(body) + bytes([TAG_SNAPPY])
+    if tag == TAG_LZ4:                                     # compress.rs:73-77
+        return struct.pack("<I", len(body)) + lz4_compress(body) + bytes([TAG_LZ4])
     return body + bytes([tag])
 
 
@@ -299,9 +478,11 @@ def decode_block(blk: bytes) -> dict:
         if data is None:
             r["status"] = ST_CODEC
             return r
-    elif tag != TAG_NONE:
-        r["status"] = ST_UNSUPPORTED
-        return r
+    elif tag == TAG_LZ4:                                   # compress.rs:108-111
+        data = lz4_block_decompress(blk[:-1])
+        if data is None:
+            r["status"] = ST_CODEC
+            return r
     else:
         data = blk[:-1]
     if len(data) < 4:                                      # block.rs:49 split_to underflow panics
@@ -611,11 +792,71 @@ def main() -> None:
         json.dump([{"name": n, "stream": st.hex(), "out": None if w is None else w.hex()}
                    for n, st, w in kat], fj, indent=0)
 
-    # 10. CRC known answers (pins crc32fast == CRC-32/ISO-HDLC; src/checksum.rs:27-33 string).
+    # 10. LZ4 (codec 3, compress.rs:73-77, 108-111): SSTs with lz4 blocks, and known answers
+    #     for hand-built sequences and for the streams liblz4's safe decoder rejects.
+    sst_fixture("sst_lz4_bench", SsTableBuilder(4096, tag=TAG_LZ4),
+                [(key_of(i), value_of(i)) for i in range(1000)])
+    g = splitmix64(0x5EED0005)
+    kv = [(struct.pack(">Q", i) + rand_bytes(g, 8), rand_bytes(g, 100)) for i in range(34 * 6)]
+    sst_fixture("sst_lz4_4k", SsTableBuilder(4096, tag=TAG_LZ4), kv)
+    pre = lambda n: struct.pack("<I", n)
+    kat = [
+        ("literals_only", pre(5) + bytes([5 << 4]) + b"hello", b"hello"),
+        ("empty_output", pre(0) + b"\x00", b""),
+        ("match_overlap", pre(21) + bytes([4 << 4 | 8]) + b"abcd" + b"\x04\x00"
+         + bytes([5 << 4]) + b"vwxyz", b"abcd" * 4 + b"vwxyz"),
+        ("match_run", pre(30) + bytes([1 << 4 | 15]) + b"z" + b"\x01\x00" + bytes([5])
+         + bytes([5 << 4]) + b"12345", b"z" * 25 + b"12345"),
+        ("literal_ext", pre(300) + bytes([15 << 4]) + bytes([255, 30]) + bytes(range(256))
+         + bytes(44), bytes(range(256)) + bytes(44)),
+        ("offset_zero", pre(21) + bytes([4 << 4 | 8]) + b"abcd" + b"\x00\x00"
+         + bytes([5 << 4]) + b"vwxyz", b"abcd" + bytes(12) + b"vwxyz"),
+        ("short_decode", pre(100) + bytes([5 << 4]) + b"hello", b"hello"),
+        ("err_no_prefix", b"\x05\x00", None),
+        ("err_negative_size", b"\xff\xff\xff\xff\x50hello", None),
+        ("err_empty_stream", pre(5), None),
+        ("err_offset_past", pre(21) + bytes([4 << 4 | 8]) + b"abcd" + b"\x05\x00"
+         + bytes([5 << 4]) + b"vwxyz", None),
+        ("err_literal_past_input", pre(10) + bytes([9 << 4]) + b"abc", None),
+        ("err_output_overrun", pre(3) + bytes([5 << 4]) + b"hello", None),
+        ("err_match_into_last5", pre(12) + bytes([4 << 4 | 4]) + b"abcd" + b"\x04\x00"
+         + bytes([0]), None),
+        ("err_truncated_ml_ext", pre(60) + bytes([4 << 4 | 15]) + b"abcd" + b"\x04\x00"
+         + bytes([255, 255]), None),
+    ]
+    for name, stream, want in kat:
+        assert lz4_block_decompress(stream) == want, name
+    _check_lz4_against_liblz4(kat)
+    with open(os.path.join(HERE, "lz4_kat.json"), "w") as fj:
+        json.dump([{"name": n, "stream": st.hex(), "out": None if w is None else w.hex()}
+                   for n, st, w in kat], fj, indent=0)
+
+    # 11. CRC known answers (pins crc32fast == CRC-32/ISO-HDLC; src/checksum.rs:27-33 string).
     kat = {s.hex(): crc32(s) for s in [b"", b"a", b"123456789", b"12312nskjdhsdi9823r1y3r9",
                                         bytes(range(256)) * 5, b"\x00" * 4150, b"\xff" * 17]}
     with open(os.path.join(HERE, "crc_kat.json"), "w") as fj:
         json.dump(kat, fj, indent=0, sort_keys=True)
+
+
+def _check_lz4_against_liblz4(kat):
+    """Pins the restatement to liblz4 itself (the library the lz4 crate binds) when this image
+    has it: every KAT and the LZ4 fixture blocks decode identically."""
+    import ctypes
+    try:
+        lib = ctypes.CDLL("liblz4.so.1")
+    except OSError:
+        print("liblz4 not loadable: LZ4 fixtures pinned by the restatement only")
+        return
+    lib.LZ4_decompress_safe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.c_int]
+    for name, stream, want in kat:
+        if len(stream) < 4 or struct.unpack("<i", stream[:4])[0] < 0:
+            continue
+        size = struct.unpack("<i", stream[:4])[0]
+        dst = ctypes.create_string_buffer(size + 64)
+        r = lib.LZ4_decompress_safe(stream[4:], dst, len(stream) - 4, size)
+        got = None if r < 0 else dst.raw[:r]
+        assert got == want, (name, got, want)
 
 
 if __name__ == "__main__":

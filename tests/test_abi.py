@@ -125,3 +125,24 @@ def test_host_snappy_encoder_round_trips(config):
     for i in range(len(ext) - 1):
         st, out = O.decompress_block(s2[int(e2[i]):int(e2[i + 1])].tobytes())
         assert st == O.OK and out == src[int(ext[i]):int(ext[i + 1])].tobytes()
+
+
+@pytest.mark.parametrize("config", ["4k", "zipf", "64k"])
+def test_host_lz4_encoder_round_trips(config):
+    """tpz_lz4_encode_blocks (compress::encode with Lz4, compress.rs:73-77) emits size-prefixed
+    LZ4 blocks that the oracle's restatement and liblz4 itself decode back to the Uncompress
+    blocks."""
+    src, ext = synth.make_region(config, 6 if config == "64k" else 60)
+    s2, e2 = synth.lz4_blocks(src, ext)
+    L = O.liblz4()
+    for i in range(len(ext) - 1):
+        blk = s2[int(e2[i]):int(e2[i + 1])].tobytes()
+        want = src[int(ext[i]):int(ext[i + 1])].tobytes()
+        assert blk[-1] == 3 and int.from_bytes(blk[:4], "little") == len(want) - 1
+        st, out = O.decompress_block(blk)
+        assert st == O.OK and out == want
+        if L is not None:
+            import ctypes as C
+            dst = C.create_string_buffer(len(want) + 64)
+            assert L.LZ4_decompress_safe(blk[4:-1], dst, len(blk) - 5, len(want) - 1) == len(want) - 1
+            assert dst.raw[:len(want) - 1] == want[:-1]

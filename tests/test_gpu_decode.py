@@ -33,13 +33,14 @@ def ctx():
 
 
 def gpu_decode(ctx, src, ext):
-    """The device path of Block::decode for a batch: the codec step for snappy blocks
+    """The device path of Block::decode for a batch: the codec step for snappy/lz4 blocks
     (tpz_decompress_blocks), then tpz_decode_blocks; a failed codec step's status wins."""
     src = np.ascontiguousarray(src, np.uint8)
     ext = np.asarray(ext, np.uint64)
     b = DeviceBatch(src, ext)
     codec = None
-    if any(ext[i + 1] > ext[i] and src[int(ext[i + 1]) - 1] == 2 for i in range(len(ext) - 1)):
+    if any(ext[i + 1] > ext[i] and src[int(ext[i + 1]) - 1] in (2, 3)
+           for i in range(len(ext) - 1)):
         b, st = decompress_batch(ctx, b)
         codec = st[:len(ext) - 1].cpu().numpy()
     cols = decode_batch(ctx, b)
@@ -88,7 +89,8 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
 
 
 SSTS = ["sst_100_b128", "sst_b16", "sst_bloom3", "sst_bench_1000", "sst_4k_k16_v100",
-        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k"]
+        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k",
+        "sst_lz4_bench", "sst_lz4_4k"]
 
 
 @pytest.mark.parametrize("name", SSTS)

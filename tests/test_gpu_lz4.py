@@ -1,0 +1,139 @@
+"""Parity of the device codec step for LZ4 blocks (tpz_decompressed_sizes +
+tpz_decompress_blocks, then tpz_decode_blocks) with the CPU oracle.
+
+Reference: compress::decode -> lz4::block::decompress(data, None) (src/block/compress.rs:108-111)
+then Block::decode. The oracle's LZ4 restatement (oracle/tpz_lz4.c) is pinned against liblz4
+1.9.3 by tests/test_lz4_oracle.py. Bar: byte-exact decompressed blocks, statuses equal to the
+oracle's, decoded entries bit-exact (through test_gpu_decode.assert_parity)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import GOLDEN
+from test_gpu_decode import _random_blocks, assert_parity, ctx  # noqa: F401 (fixture)
+from test_gpu_snappy import batch_of, device_codec
+from topazdb_amd import _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_codec(b: bytes):
+    """(status, bytes) of the codec step as the oracle (and the device) define it."""
+    st, out = O.decompress_block(b)
+    if st == O.OK and b and b[-1] == 3 and (len(out) > _lib.MAX_BLOCK_BYTES or len(b) - 1 > 65504):
+        return O.TOO_LARGE, b""
+    return st, out
+
+
+def test_known_answer_streams(ctx):
+    """lz4_kat.json streams as blocks (stream + tag 3): liblz4's output + tag 1, or
+    CODEC_ERROR where lz4::block::decompress returns Err."""
+    kat = json.load(open(os.path.join(GOLDEN, "lz4_kat.json")))
+    blocks = [bytes.fromhex(k["stream"]) + b"\x03" for k in kat]
+    outs, st = device_codec(ctx, blocks)
+    for k, o, s in zip(kat, outs, st):
+        if k["out"] is None:
+            assert s == _lib.BLOCK_CODEC_ERROR, k["name"]
+        else:
+            assert s == _lib.BLOCK_OK and o == bytes.fromhex(k["out"]) + b"\x01", k["name"]
+
+
+def lz4_random_blocks(rng, n, max_target=9000, corrupt_every=0):
+    src, ext = _random_blocks(rng, n, max_target=max_target)
+    blocks = []
+    for i in range(len(ext) - 1):
+        b = src[int(ext[i]):int(ext[i + 1])].tobytes()
+        if i % 5 < 4 and b and b[-1] == 1:
+            b = O.lz4_block(b, 1 if i % 5 == 3 else 0)
+        if corrupt_every and i % corrupt_every == 3:
+            b = bytearray(b)
+            p = int(rng.integers(0, max(len(b) - 1, 1)))
+            kind = i % 3
+            if kind == 0:
+                b[p] ^= 1 << int(rng.integers(0, 8))
+            elif kind == 1:
+                b = b[:p] + b[-1:]
+            else:
+                b[0:4] = int(rng.integers(0, 1 << 31)).to_bytes(4, "little")  # size prefix
+            b = bytes(b)
+        blocks.append(b)
+    return blocks
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_codec_bytes_match_oracle(ctx, seed):
+    rng = np.random.default_rng(seed)
+    blocks = lz4_random_blocks(rng, 300, corrupt_every=5)
+    outs, st = device_codec(ctx, blocks)
+    for i, b in enumerate(blocks):
+        ost, ob = oracle_codec(b)
+        assert st[i] == ost, (i, st[i], ost)
+        if ost == O.OK:
+            assert outs[i] == ob, i
+
+
+def test_fuzzed_streams_match_oracle(ctx):
+    """Random and crafted token streams: the device's acceptance (fast loop / safe loop /
+    shortcut, end-of-buffer rules) and output equal the oracle's, i.e. liblz4's."""
+    rng = np.random.default_rng(7)
+    blocks = []
+    for i in range(3000):
+        if i % 2:
+            body = rng.bytes(int(rng.integers(0, 40)))
+        else:
+            body = bytearray()
+            for _ in range(int(rng.integers(1, 5))):
+                ll, ml = int(rng.integers(0, 16)), int(rng.integers(0, 16))
+                body.append(ll << 4 | ml)
+                if ll == 15:
+                    body += bytes([255] * int(rng.integers(0, 2)) + [int(rng.integers(0, 40))])
+                body += rng.bytes(min(ll, 30))
+                body += int(rng.integers(0, 24)).to_bytes(2, "little")
+                if ml == 15:
+                    body += bytes([int(rng.integers(0, 256))])
+            ll = int(rng.integers(0, 16))
+            body.append(ll << 4)
+            body += rng.bytes(ll)
+        size = int(rng.choice([0, 1, 8, 20, 40, 63, 64, 65, 80, 200, 3 * len(body)]))
+        blocks.append(size.to_bytes(4, "little") + bytes(body) + b"\x03")
+    outs, st = device_codec(ctx, blocks)
+    n_ok = 0
+    for i, b in enumerate(blocks):
+        ost, ob = oracle_codec(b)
+        assert st[i] == ost, (i, b.hex(), st[i], ost)
+        if ost == O.OK:
+            n_ok += 1
+            assert outs[i] == ob, (i, b.hex())
+    assert n_ok > 100           # ~5 % of these streams are valid
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_lz4_blocks_decode(ctx, seed):
+    """Whole path (codec step + decode) against the oracle's Block::decode on every block."""
+    rng = np.random.default_rng(seed)
+    src, ext = batch_of(lz4_random_blocks(rng, 400, corrupt_every=9))
+    assert_parity(ctx, src, ext)
+
+
+def test_large_lz4_blocks(ctx):
+    """64 KiB-config blocks (and long random blocks) take the one-wave kernel; a compressed
+    block past 64 KiB - 31 bytes is TOO_LARGE on both sides."""
+    src, ext = synth.make_region("64k", 40)
+    blocks = [O.lz4_block(src[int(ext[i]):int(ext[i + 1])].tobytes(), i % 2) for i in range(40)]
+    rng = np.random.default_rng(5)
+    blocks += lz4_random_blocks(rng, 40, max_target=60000)
+    raw = rng.bytes(70000)
+    blocks.append(len(raw).to_bytes(4, "little") + O.lz4_compress(raw, 1) + b"\x03")
+    s2, e2 = batch_of(blocks)
+    assert_parity(ctx, s2, e2)
+    _, st = device_codec(ctx, blocks[-1:])
+    assert st[0] == _lib.BLOCK_TOO_LARGE
+
+
+def test_config_batch_lz4(ctx):
+    src, ext = synth.make_region("4k", 5000)
+    s2, e2 = synth.lz4_blocks(src, ext)
+    assert_parity(ctx, s2, e2, expect_all_ok=True)

@@ -22,7 +22,8 @@ from topazdb_amd.table import (Block, BlockError, BlockIterator, FileObject, Ref
 pytestmark = pytest.mark.gpu
 
 SSTS = ["sst_100_b128", "sst_b16", "sst_bloom3", "sst_bench_1000", "sst_4k_k16_v100",
-        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k"]
+        "sst_zipf", "sst_64k_k32_v1k", "sst_snappy_bench", "sst_snappy_4k",
+        "sst_lz4_bench", "sst_lz4_4k"]
 
 
 @pytest.fixture(scope="module")

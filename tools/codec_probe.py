@@ -4,7 +4,7 @@ tpz_decompress_blocks for the shipped build and prints the per-phase wave-cycle 
 stamps build (topazdb_amd/variants/libtpz_gpu_cstamps.so, make -C topazdb_amd/csrc
 codec-variants).
 
-    python3 tools/codec_probe.py [--blocks 262144] [--steps 10] full cstamps
+    python3 tools/codec_probe.py [--blocks 262144] [--steps 10] [--codec lz4] full cstamps
 """
 from __future__ import annotations
 
@@ -47,10 +47,12 @@ def main():
     ap.add_argument("variants", nargs="+")
     ap.add_argument("--blocks", type=int, default=1 << 18)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--codec", default="snappy", choices=["snappy", "lz4"])
     a = ap.parse_args()
 
     src, ext, _, _, _, _ = make_shard("4k", a.blocks, 0)
-    s2, e2 = synth.snappy_blocks(src[:int(ext[a.blocks])], ext[:a.blocks + 1])
+    enc = synth.snappy_blocks if a.codec == "snappy" else synth.lz4_blocks
+    s2, e2 = enc(src[:int(ext[a.blocks])], ext[:a.blocks + 1])
     batch = DeviceBatch(s2, e2)
     nb = batch.n_blocks
     b = _lib.Batch(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes)

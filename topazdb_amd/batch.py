@@ -169,8 +169,8 @@ def verify_files(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | N
 
 def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None):
     """compress::decode's codec step (src/block/compress.rs:95-113) on the GPU: snappy (tag 2)
-    blocks become Uncompress blocks (tpz_decompressed_sizes, a device prefix sum of the sizes,
-    tpz_decompress_blocks). Returns (DeviceBatch of the uncompressed blocks, codec status
+    and lz4 (tag 3) blocks become Uncompress blocks (tpz_decompressed_sizes, a device prefix sum
+    of the sizes, tpz_decompress_blocks). Returns (DeviceBatch of the uncompressed blocks, codec status
     tensor); decode the former with decode_batch and take the codec status for blocks whose codec
     step failed."""
     dev = _dev(ctx.device)

@@ -31,11 +31,15 @@ typedef uint32_t u32;
 typedef uint64_t u64;
 
 constexpr int kWave = 64;
-constexpr int kSmallWaves = 16;
+#ifndef TPZ_CODEC_WAVES
+#define TPZ_CODEC_WAVES 16                           // diagnostic builds vary it
+#endif
+constexpr int kSmallWaves = TPZ_CODEC_WAVES;
 constexpr u32 kSmallIn = 4608, kSmallOut = 5120;     // per-wave windows of the 16-wave kernel
 constexpr u32 kBigIn = 65536, kBigOut = 94208;       // the one-wave kernel
 constexpr u32 kGuard = 16;                           // readable bytes before each input window
 constexpr u32 kInSlack = 16 + 16;                    // staging offset (< 16) + header overread
+constexpr u64 kLz4MaxIn = kBigIn - kInSlack;         // 65504: compressed bytes a window takes
 static_assert(kSmallWaves * (kGuard + kSmallIn + kSmallOut) <= 163840, "small LDS");
 static_assert(kGuard + kBigIn + kBigOut <= 163840, "big LDS");
 
@@ -118,22 +122,6 @@ struct CodecParams {
   u32* defer_list;
   u32* defer_count;
 };
-
-// ------------------------------------------------------------------ sizes
-__global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n_blocks) return;
-  const u64 s = p.ext[i], e = p.ext[i + 1], len = e - s;
-  if (len == 0 || p.src[e - 1] != 2) {   // not snappy: copied unchanged
-    p.size[i] = len;
-    return;
-  }
-  u64 want = 0;
-  const u32 h = snappy_header(p.src + s, len - 1, want);
-  // an invalid preamble leaves an empty range; a declared length no device decode could take
-  // leaves a lone tag byte (the decode reports it; the codec status says why)
-  p.size[i] = h == 0 ? 0 : (want + 1 <= TPZ_MAX_BLOCK_BYTES ? want + 1 : 1);
-}
 
 // ------------------------------------------------------------------ per-block work
 // Copies LDS bytes to global [g, g + n). The bytes sit at win[(g & 15) ..], i.e. LDS and global
@@ -244,10 +232,260 @@ __device__ __forceinline__ bool snappy_decode(const uint8_t* in, u32 n, u32 ip, 
   return d == want;
 }
 
+// ------------------------------------------------------------------ LZ4 (codec 3)
+// lz4::block::decompress(data, None) (src/block/compress.rs:108-111): i32 LE size prefix (Err if
+// the source is shorter than 4 bytes, the size is negative or above LZ4_compressBound's limit
+// 0x7E000000), then LZ4_decompress_safe(src + 4, dst, len - 4, size); the output is the `ret`
+// bytes it decodes (possibly fewer than `size`). The acceptance rules below are liblz4 1.9.3's
+// LZ4_decompress_generic for LZ4_decompress_safe, restated as oracle/tpz_lz4.c does (and pinned
+// against liblz4 by tests/test_lz4_oracle.py): the fast loop while >= 64 output bytes remain,
+// then the safe loop with its two-stage shortcut. A match repeats the bytes `offset` back
+// (periodic when it overlaps); an offset-0 match is zeros. `Src` reads input bytes, `Out`
+// copies (or not: the sizes pass only walks).
+struct Lz4NoOut {
+  __device__ void lit(int64_t, int64_t, int64_t) const {}
+  __device__ void match(int64_t, int64_t, int64_t) const {}
+};
+struct Lz4GlobalSrc {            // per thread, straight from global memory
+  const uint8_t* p;
+  __device__ u32 byte(int64_t i) const { return p[i]; }
+};
+struct Lz4LdsSrc {               // wave-uniform, from the staged bytes
+  const uint8_t* p;
+  __device__ u32 byte(int64_t i) const { return uni(p[i]); }
+};
+
+__device__ __forceinline__ void match_copy_wave(uint8_t* out, u32 d, u32 off, u32 len) {
+  const u32 lane = lane_id();
+  if (off == 0) {
+    for (u32 k = lane; k < len; k += kWave) out[d + k] = 0;
+  } else if (off >= (u32)kWave) {
+    // each round of 64 bytes reads bytes at least 64 back: written by earlier rounds
+    for (u32 k = lane; k < len; k += kWave) out[d + k] = out[d + k - off];
+  } else {
+    // period off: byte k is byte k mod off of the run before d
+    u32 r = lane - (u32)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)off)) * off;
+    const u32 c = (u32)kWave % off;
+    for (u32 k = lane; k < len; k += kWave) {
+      out[d + k] = out[d - off + r];
+      r += c;
+      r = r >= off ? r - off : r;
+    }
+  }
+}
+
+struct Lz4WaveOut {              // wave-wide copies into the LDS output window
+  const uint8_t* in;
+  uint8_t* out;
+  __device__ void lit(int64_t op, int64_t ip, int64_t len) const {
+    literal_copy(in, (u32)ip, out, (u32)op, (u32)len);
+  }
+  __device__ void match(int64_t op, int64_t off, int64_t len) const {
+    match_copy_wave(out, (u32)op, (u32)off, (u32)len);
+  }
+};
+
+template <class Src, class Out>
+__device__ int64_t lz4_walk(const Src& in, int64_t iend, const Out& out, int64_t oend) {
+  if (oend == 0) return (iend == 1 && in.byte(0) == 0) ? 0 : -1;
+  if (iend == 0) return -1;
+  const int64_t shortiend = iend - 16, shortoend = oend - 32;
+  int64_t ip = 0, op = 0, lit = 0, ml = 0, off = 0, match = 0, cpy = 0;
+  u32 token = 0;
+  if (oend >= 64) {
+    for (;;) {                                                // fast loop
+      token = in.byte(ip++);
+      lit = token >> 4;
+      if (lit == 15) {
+        if (ip >= iend - 15) return -1;
+        u32 sv;
+        do {
+          sv = in.byte(ip++);
+          lit += sv;
+          if (ip >= iend - 15) break;
+        } while (sv == 255);
+        cpy = op + lit;
+        if (cpy > oend - 32 || ip + lit > iend - 32) goto safe_literal_copy;
+      } else {
+        cpy = op + lit;
+        if (ip > iend - 17) goto safe_literal_copy;
+      }
+      out.lit(op, ip, lit);
+      ip += lit;
+      op = cpy;
+      off = (int64_t)(in.byte(ip) | in.byte(ip + 1) << 8);
+      ip += 2;
+      match = op - off;
+      ml = token & 15;
+      if (ml == 15) {
+        if (match < 0) return -1;
+        u32 sv;
+        do {
+          sv = in.byte(ip++);
+          ml += sv;
+          if (ip >= iend - 4) return -1;
+        } while (sv == 255);
+        ml += 4;
+        if (op + ml >= oend - 64) goto safe_match_copy;
+      } else {
+        ml += 4;
+        if (op + ml >= oend - 64) goto safe_match_copy;
+      }
+      if (match < 0) return -1;
+      out.match(op, off, ml);
+      op += ml;
+    }
+  }
+  for (;;) {                                                  // safe loop
+    token = in.byte(ip++);
+    lit = token >> 4;
+    if (lit != 15 && ip < shortiend && op <= shortoend) {     // the shortcut
+      out.lit(op, ip, lit);
+      op += lit;
+      ip += lit;
+      ml = token & 15;
+      off = (int64_t)(in.byte(ip) | in.byte(ip + 1) << 8);
+      ip += 2;
+      match = op - off;
+      if (ml != 15 && off >= 8 && match >= 0) {
+        out.match(op, off, ml + 4);
+        op += ml + 4;
+        continue;
+      }
+      goto copy_match;
+    }
+    if (lit == 15) {
+      if (ip >= iend - 15) return -1;
+      u32 sv;
+      do {
+        sv = in.byte(ip++);
+        lit += sv;
+        if (ip >= iend - 15) break;
+      } while (sv == 255);
+    }
+    cpy = op + lit;
+  safe_literal_copy:
+    if (cpy > oend - 12 || ip + lit > iend - 8) {             // must be the last sequence
+      if (ip + lit != iend || cpy > oend) return -1;
+      out.lit(op, ip, lit);
+      op += lit;
+      break;
+    }
+    out.lit(op, ip, lit);
+    ip += lit;
+    op = cpy;
+    off = (int64_t)(in.byte(ip) | in.byte(ip + 1) << 8);
+    ip += 2;
+    match = op - off;
+    ml = token & 15;
+  copy_match:
+    if (ml == 15) {
+      u32 sv;
+      do {
+        sv = in.byte(ip++);
+        ml += sv;
+        if (ip >= iend - 4) return -1;
+      } while (sv == 255);
+    }
+    ml += 4;
+  safe_match_copy:
+    if (match < 0) return -1;
+    cpy = op + ml;
+    if (cpy > oend - 5) return -1;                            // the last 5 bytes are literals
+    out.match(op, off, ml);
+    op = cpy;
+  }
+  return op;
+}
+
+// The size prefix: the i32 LE size, or -1 where lz4::block::decompress returns Err before
+// decoding (source < 4 bytes, negative size, size past LZ4_compressBound's limit).
+__device__ __forceinline__ int64_t lz4_prefix(const uint8_t* s, u64 n) {
+  if (n < 4) return -1;
+  const int32_t v = (int32_t)((u32)s[0] | (u32)s[1] << 8 | (u32)s[2] << 16 | (u32)s[3] << 24);
+  return (v < 0 || v > 0x7E000000) ? -1 : (int64_t)v;
+}
+
+// The whole decode decision of a tag-3 block from global memory (per thread): its decoded
+// length, or -1 (the codec's Err).
+__device__ __forceinline__ int64_t lz4_block_length(const uint8_t* blk, u64 len) {
+  const int64_t size = lz4_prefix(blk, len - 1);
+  if (size < 0) return -1;
+  return lz4_walk(Lz4GlobalSrc{blk + 4}, (int64_t)len - 5, Lz4NoOut{}, size);
+}
+
+// ------------------------------------------------------------------ sizes
+__global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_blocks) return;
+  const u64 s = p.ext[i], e = p.ext[i + 1], len = e - s;
+  const u32 tag = len ? p.src[e - 1] : 0u;
+  if (tag == 3) {
+    // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err, or a
+    // block past the device limits, leaves a lone tag byte
+    const int64_t r = lz4_block_length(p.src + s, len);
+    p.size[i] = (r < 0 || (u64)r + 1 > TPZ_MAX_BLOCK_BYTES || len - 1 > kLz4MaxIn) ? 1 : r + 1;
+    return;
+  }
+  if (tag != 2) {                         // not compressed: copied unchanged
+    p.size[i] = len;
+    return;
+  }
+  u64 want = 0;
+  const u32 h = snappy_header(p.src + s, len - 1, want);
+  // an invalid preamble leaves an empty range; a declared length no device decode could take
+  // leaves a lone tag byte (the decode reports it; the codec status says why)
+  p.size[i] = h == 0 ? 0 : (want + 1 <= TPZ_MAX_BLOCK_BYTES ? want + 1 : 1);
+}
+
 struct BlockMeta {
   u64 s, e, D0, D1;
   u32 tag;
 };
+
+// One LZ4 block (tag 3). Returns false when it does not fit the windows (the caller defers it).
+template <u32 kIn, u32 kOut>
+__device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const BlockMeta& m,
+                                          uint8_t* in_win, uint8_t* out_win, bool last_resort) {
+  const u32 lane = lane_id();
+  const u64 s = m.s, len = m.e - m.s;
+  uint8_t* dst = p.dst + m.D0;
+  const u64 dn = m.D1 - m.D0;
+  const bool fits = len - 1 + kInSlack <= kIn && dn + 16 <= kOut;
+  if (!fits && !last_resort) return false;
+  u32 st = TPZ_BLOCK_CODEC_ERROR;
+  bool ok = false;
+  const u32 a_out = (u32)(reinterpret_cast<uintptr_t>(dst) & 15);
+  uint8_t* out = out_win + a_out;
+  if (!fits || dn < 2) {
+    // an Err, a block past the limits (the sizes pass gave it 1 byte) or an empty output: the
+    // decision again, from global memory
+    const int64_t r = lz4_block_length(p.src + s, len);
+    if (r >= 0) {
+      if (r == 0 && dn == 1 && len - 1 <= kLz4MaxIn) ok = true;
+      else st = TPZ_BLOCK_TOO_LARGE;
+    }
+  } else {
+    stage_aligned(p.src, p.src_bytes, s, (u32)(len - 1), in_win);
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* in = in_win + (u32)(s & 15);
+    const int64_t size = lz4_prefix(p.src + s, len - 1);     // valid: dn >= 2
+    const int64_t r = lz4_walk(Lz4LdsSrc{in + 4}, (int64_t)len - 5, Lz4WaveOut{in + 4, out}, size);
+    __builtin_amdgcn_wave_barrier();
+    ok = r >= 0 && (u64)r + 1 == dn;
+  }
+  if (ok) {
+    if (lane == 0) out[dn - 1] = 1;                            // re-tagged Uncompress
+    __builtin_amdgcn_wave_barrier();
+    store_aligned(out_win, dst, (u32)dn);
+    if (lane == 0) p.status[b] = TPZ_BLOCK_OK;
+  } else if (lane == 0) {
+    if (dn) dst[dn - 1] = 0;                                   // decodes as BAD_TAG
+    p.status[b] = (uint8_t)st;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
 
 // One block. Returns false when it does not fit the windows (the caller defers it).
 template <u32 kIn, u32 kOut>
@@ -258,6 +496,7 @@ __device__ __forceinline__ bool codec_block(const CodecParams& p, u32 b, const B
   const u64 s = m.s, len = m.e - m.s;
   uint8_t* dst = p.dst + m.D0;
   const u64 dn = m.D1 - m.D0;
+  if (len != 0 && m.tag == 3) return lz4_block<kIn, kOut>(p, b, m, in_win, out_win, last_resort);
   if (len == 0 || m.tag != 2) {                               // copied unchanged
     const u64 n = len < dn ? len : dn;
     for (u64 k = lane; k < n; k += kWave) dst[k] = p.src[s + k];

@@ -113,9 +113,80 @@ size_t snappy_encode(const uint8_t* s, size_t n, uint8_t* o) {
   return p;
 }
 
+// LZ4 block encoder (the format LZ4_compress_default writes): greedy matches over a 4-byte
+// hash, offsets < 64 KiB; the last match starts >= 12 bytes before the end and the last 5 bytes
+// are literals, as the format's end rules require. Returns the length.
+size_t lz4_encode(const uint8_t* s, size_t n, uint8_t* o) {
+  size_t p = 0;
+  auto put_len = [&](size_t v) {
+    for (; v >= 255; v -= 255) o[p++] = 255;
+    o[p++] = (uint8_t)v;
+  };
+  auto sequence = [&](size_t lo, size_t hi, size_t off, size_t m) {
+    const size_t ll = hi - lo, mc = m ? m - 4 : 0;
+    o[p++] = (uint8_t)((ll >= 15 ? 15 : ll) << 4 | (m ? (mc >= 15 ? 15 : mc) : 0));
+    if (ll >= 15) put_len(ll - 15);
+    std::memcpy(o + p, s + lo, ll);
+    p += ll;
+    if (!m) return;
+    o[p++] = (uint8_t)off;
+    o[p++] = (uint8_t)(off >> 8);
+    if (mc >= 15) put_len(mc - 15);
+  };
+  constexpr int kBits = 13;
+  thread_local std::vector<int32_t> table(1 << kBits);
+  std::fill(table.begin(), table.end(), -1);
+  const size_t mflimit = n > 12 ? n - 12 : 0, matchlimit = n > 5 ? n - 5 : 0;
+  size_t anchor = 0, i = 0;
+  while (i + 4 <= n && i < mflimit) {
+    uint32_t w;
+    std::memcpy(&w, s + i, 4);
+    const uint32_t h = (w * 2654435761u) >> (32 - kBits);
+    const int32_t c = table[h];
+    table[h] = (int32_t)i;
+    uint32_t cw;
+    if (c < 0 || i - (size_t)c > 65535 || (std::memcpy(&cw, s + c, 4), cw != w)) {
+      i++;
+      continue;
+    }
+    size_t m = 4;
+    while (i + m < matchlimit && s[c + m] == s[i + m]) m++;
+    sequence(anchor, i, i - (size_t)c, m);
+    i += m;
+    anchor = i;
+  }
+  sequence(anchor, n, 0, 0);
+  return p;
+}
+
 }  // namespace
 
 extern "C" {
+
+int tpz_lz4_encode_blocks(const uint8_t* src, const uint64_t* ext, uint64_t n_blocks,
+                          uint8_t* out, uint64_t out_cap, uint64_t* out_ext, uint64_t* out_len) {
+  if (!src || !ext || !out || !out_ext || !out_len) return TPZ_ERR_INVALID_ARG;
+  uint64_t o = 0;
+  for (uint64_t b = 0; b < n_blocks; b++) {
+    const uint8_t* blk = src + ext[b];
+    const uint64_t len = ext[b + 1] - ext[b];
+    out_ext[b] = o;
+    if (len == 0 || blk[len - 1] != 1 || len - 1 > 0x7E000000ull) {  // re-encode Uncompress only
+      if (o + len > out_cap) return TPZ_ERR_NOMEM;
+      std::memcpy(out + o, blk, len);
+      o += len;
+      continue;
+    }
+    if (o + 32 + len + len / 255 > out_cap) return TPZ_ERR_NOMEM;
+    const uint64_t body = len - 1;                          // payload | crc, before the tag
+    for (int k = 0; k < 4; k++) out[o++] = (uint8_t)(body >> (8 * k));  // prepend_size (LE)
+    o += lz4_encode(blk, body, out + o);
+    out[o++] = 3;                                           // compress.rs:75 Lz4 tag
+  }
+  out_ext[n_blocks] = o;
+  *out_len = o;
+  return TPZ_SUCCESS;
+}
 
 int tpz_snappy_encode_blocks(const uint8_t* src, const uint64_t* ext, uint64_t n_blocks,
                              uint8_t* out, uint64_t out_cap, uint64_t* out_ext,

@@ -120,7 +120,7 @@ def snappy_blocks(src: np.ndarray, ext: np.ndarray):
     compress::encode, src/block/compress.rs:66-71): (src, ext)."""
     L = _lib.lib()
     L.tpz_snappy_encode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
-                                           C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
+                                        C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
     nb = len(ext) - 1
     src = np.ascontiguousarray(src, np.uint8)
     ext = np.ascontiguousarray(ext, np.uint64)
@@ -129,6 +129,25 @@ def snappy_blocks(src: np.ndarray, ext: np.ndarray):
     oext = np.empty(nb + 1, np.uint64)
     n = C.c_uint64()
     _lib.check(L.tpz_snappy_encode_blocks(src.ctypes.data, ext.ctypes.data, nb, out.ctypes.data,
-                                          cap, oext.ctypes.data, C.byref(n)),
+                                       cap, oext.ctypes.data, C.byref(n)),
                "tpz_snappy_encode_blocks")
+    return out[:n.value], oext
+
+
+def lz4_blocks(src: np.ndarray, ext: np.ndarray):
+    """Re-encode a region's Uncompress blocks with the Lz4 codec (tpz_lz4_encode_blocks,
+    compress::encode, src/block/compress.rs:73-77): (src, ext)."""
+    L = _lib.lib()
+    L.tpz_lz4_encode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                        C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64)]
+    nb = len(ext) - 1
+    src = np.ascontiguousarray(src, np.uint8)
+    ext = np.ascontiguousarray(ext, np.uint64)
+    cap = 32 * nb + 2 * int(ext[-1]) + 64
+    out = np.empty(cap, np.uint8)
+    oext = np.empty(nb + 1, np.uint64)
+    n = C.c_uint64()
+    _lib.check(L.tpz_lz4_encode_blocks(src.ctypes.data, ext.ctypes.data, nb, out.ctypes.data,
+                                       cap, oext.ctypes.data, C.byref(n)),
+               "tpz_lz4_encode_blocks")
     return out[:n.value], oext

@@ -14,10 +14,9 @@ Same names, argument meaning and error behaviour as the reference:
 Errors: where the reference returns an anyhow::Error, this raises BlockError whose text is the
 reference's message ("checksum: expected E, actual A", "data is empty", "invaild data"); where
 the reference panics (a malformed block, a file shorter than its checksum, seek_to_last on an
-empty block, ...) it raises ReferencePanic. Snappy blocks are decompressed on the device
-first; a stream snap rejects raises BlockError("decompression failed"). LZ4 blocks (not decoded
-on the device yet) raise BlockError("unsupported codec") — there is no CPU
-fallback.
+empty block, ...) it raises ReferencePanic. Snappy and LZ4 blocks are decompressed on the
+device first (tpz_decompress_blocks); a stream the codec rejects raises
+BlockError("decompression failed"). There is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -120,15 +119,16 @@ class Block:
 
 
 def _decode_region(ctx: Context, region: bytes, ext: np.ndarray) -> list:
-    """Decode blocks [ext[i], ext[i+1]) of `region`: snappy blocks first go through the device
-    codec step (compress.rs:104-107), then one tpz_decode_blocks launch decodes the batch.
+    """Decode blocks [ext[i], ext[i+1]) of `region`: snappy and lz4 blocks first go through the
+    device codec step (compress.rs:104-111), then one tpz_decode_blocks launch decodes the batch.
     Returns per block a Block or the exception the reference's Block::decode / iteration would
     raise."""
     src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
     batch = DeviceBatch(src, ext, ctx.device)
     nb = batch.n_blocks
     codec = None
-    if any(int(ext[b + 1]) > int(ext[b]) and region[int(ext[b + 1]) - 1] == 2 for b in range(nb)):
+    if any(int(ext[b + 1]) > int(ext[b]) and region[int(ext[b + 1]) - 1] in (2, 3)
+           for b in range(nb)):
         batch, st = decompress_batch(ctx, batch)
         codec = st[:nb].cpu().numpy()
     cols = decode_batch(ctx, batch)
