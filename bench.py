@@ -249,6 +249,57 @@ def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10
             "roofline_frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def seek_rate(ctx, batch: DeviceBatch, cols: SlottedColumns, config: str, dev,
+              n_q: int = 1 << 20, steps: int = 10) -> dict:
+    """Batched SsTableIterator::seek_to_key (tpz_seek_keys, SURVEY.md §8f row 4) over the
+    decoded shard as one table: half the queries are existing keys (each must land on its own
+    block and entry), half random. Latency-bound binary searches; reported as queries/s."""
+    assert config == "4k"
+    nb = batch.n_blocks
+    klen = 16                                   # the 4k config's fixed 16-B keys
+    ext = batch.ext
+    idx = torch.arange(nb, device=dev, dtype=torch.int64)
+    slot = ((ext[:nb] + 127) & ~127) + 256 * idx
+    cnt = cols.count[:nb].to(torch.int64)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    # the table's first keys: entry 0 of every block
+    off = torch.arange(klen, device=dev)
+    fk = cols.data[(slot[:, None] + off).reshape(-1)]
+    fpos = torch.arange(nb + 1, device=dev, dtype=torch.int64) * klen
+    half = n_q // 2
+    qb = torch.randint(0, nb, (half,), device=dev, generator=g)
+    qe = (torch.rand(half, device=dev, generator=g) * cnt[qb]).to(torch.int64)
+    qk = cols.data[((slot[qb] + klen * qe)[:, None] + off).reshape(-1)]
+    qk = torch.cat([qk, torch.randint(0, 256, ((n_q - half) * klen,), device=dev,
+                                      generator=g, dtype=torch.uint8)])
+    qpos = torch.arange(n_q + 1, device=dev, dtype=torch.int64) * klen
+    table = _lib.Table(fk.data_ptr(), fpos.data_ptr(), ext.data_ptr(), nb, cols.data.data_ptr(),
+                       cols.ends.data_ptr(), cols.count.data_ptr(), cols.status.data_ptr())
+    ob = torch.empty(n_q, dtype=torch.int32, device=dev)
+    oe = torch.empty(n_q, dtype=torch.int32, device=dev)
+    ost = torch.empty(n_q, dtype=torch.uint8, device=dev)
+    ov = torch.empty(n_q, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run():
+        ctx.seek_keys_ptrs(table, qk.data_ptr(), qpos.data_ptr(), n_q, ob.data_ptr(),
+                           oe.data_ptr(), ost.data_ptr(), ov.data_ptr(), stream.cuda_stream)
+    run()
+    torch.cuda.synchronize(dev)
+    assert torch.equal(ob[:half].to(torch.int64), qb) and torch.equal(oe[:half].to(torch.int64), qe)
+    assert bool((ov[:half] == 1).all()) and bool((ost == 0).all()), "seek results"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    return {"queries": n_q, "table_blocks": nb, "ms": round(ms, 4),
+            "mqueries_s": round(n_q / ms / 1e3, 1)}
+
+
 def codec_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, codec: str = "snappy",
                nb: int = 1 << 18, steps: int = 10) -> dict:
     """The same blocks with the Snappy codec (topazdb's default, src/opt.rs:48) or the Lz4 one:
@@ -350,6 +401,7 @@ def main():
     ap.add_argument("--no-file-crc", action="store_true")
     ap.add_argument("--no-snappy", action="store_true")
     ap.add_argument("--no-lz4", action="store_true")
+    ap.add_argument("--no-seek", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -416,6 +468,13 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"file CRC measurement failed: {ex}")
 
+    seek = None
+    if rank == 0 and not args.no_seek and args.config == "4k":
+        try:
+            seek = seek_rate(ctx, batch, cols, args.config, dev)
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"seek measurement failed: {ex}")
+
     snappy = lz4 = None
     if rank == 0 and not args.no_snappy:
         try:
@@ -467,6 +526,7 @@ def main():
             "cpu_baseline": cpu,
             "e2e_h2d_d2h_gib_s": e2e,
             "file_crc": fcrc,
+            "seek": seek,
             "snappy": snappy,
             "lz4": lz4,
         }

@@ -194,6 +194,43 @@ tpz_err tpz_decompressed_sizes(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d
 tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_dst,
                               const uint64_t* d_dst_ext, uint8_t* d_status, void* stream);
 
+/* ---- batched point-get side ----------------------------------------
+ * A table = its block metas' first keys plus the columns tpz_decode_blocks wrote for its
+ * blocks (d_ext: the extents of the batch that decode ran over, i.e. after the codec step).
+ *   tpz_seek_keys: for every query key, SsTableIterator::seek_to_key (src/table/iterator.rs:
+ *     44-72): find_block_idx (src/table.rs:178-182, partition_point(first_key <= key) - 1,
+ *     saturating; the lower-bound bisection), BlockIterator::seek_to_key in that block
+ *     (src/block/iterator.rs:91-109: binary search, an equal key returns at once), then the
+ *     next block's first entry when that iterator is invalid and a next block exists.
+ *     d_block/d_entry = the position, d_valid = is_valid() (iterator.rs:50-52: the current key
+ *     is non-empty), d_status = the status of the last block the seek read (non-OK: the
+ *     reference's read_block_cached Err, or its panic for MALFORMED; a table with no blocks
+ *     gives MALFORMED: block_metas[0] panics).
+ *   tpz_bloom_may_contain: SsTable::may_contain (src/table.rs:114-119) = Bloom::may_contain
+ *     (src/bloom.rs:72-84) of xxh3_64(key) for every key; d_filter = Bloom::encode (the bit
+ *     array, then k). d_out = 1 (may contain), 0 (absent), 2 (the reference panics: an empty
+ *     filter, or no bit array with k > 0).
+ * Keys are packed: key i = d_keys[d_key_pos[i] .. d_key_pos[i+1]). */
+typedef struct {
+  const uint8_t* d_first_keys;
+  const uint64_t* d_first_pos; /* n_blocks + 1 */
+  const uint64_t* d_ext;       /* n_blocks + 1 */
+  uint32_t n_blocks;
+  const uint8_t* d_data;
+  const uint32_t* d_ends;
+  const uint32_t* d_count;
+  const uint8_t* d_status;
+} tpz_table;
+
+tpz_err tpz_seek_keys(tpz_ctx* ctx, const tpz_table* table, const uint8_t* d_keys,
+                      const uint64_t* d_key_pos, uint32_t n_keys, uint32_t* d_block,
+                      uint32_t* d_entry, uint8_t* d_status, uint8_t* d_valid, void* stream);
+tpz_err tpz_bloom_may_contain(tpz_ctx* ctx, const uint8_t* d_filter, uint64_t filter_len,
+                              const uint8_t* d_keys, const uint64_t* d_key_pos, uint32_t n_keys,
+                              uint8_t* d_out, void* stream);
+/* xxh3_64 (seed 0) on the host: the hash the reference's bloom uses (xxhash-rust 0.8.5). */
+uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len);
+
 /* ---- host write side (inputs for benches and the table facade) ---------------------------
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule
  * (src/block/builder.rs:26-41) and Block::encode + Uncompress (src/block.rs:31-44,

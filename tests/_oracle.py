@@ -157,6 +157,9 @@ class SstIter:
         p = fn(self._it, C.byref(n))
         return C.string_at(p, n.value) if n.value else b""
 
+    def block_idx(self) -> int:
+        return int(lib().tpzo_sst_iter_block_idx(self._it))
+
     def key(self) -> bytes:
         return self._get(lib().tpzo_sst_iter_key)
 

@@ -146,3 +146,14 @@ def test_host_lz4_encoder_round_trips(config):
             dst = C.create_string_buffer(len(want) + 64)
             assert L.LZ4_decompress_safe(blk[4:-1], dst, len(blk) - 5, len(want) - 1) == len(want) - 1
             assert dst.raw[:len(want) - 1] == want[:-1]
+
+
+def test_host_xxh3_matches_xxhash():
+    """tpz_host_xxh3_64 (the device's xxh3, compiled for the host) equals xxhash-rust's
+    xxh3_64 as Python's xxhash 3.8.1 computes it, on every length path (0-16, 17-128, 129-240,
+    long inputs with partial and whole 1 KiB blocks)."""
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(21)
+    for n in list(range(0, 260)) + [511, 512, 1023, 1024, 1025, 2048, 2049, 5000, 70000]:
+        b = rng.bytes(n)
+        assert _lib.xxh3_64(b) == xxhash.xxh3_64_intdigest(b), n

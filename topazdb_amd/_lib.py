@@ -39,6 +39,13 @@ class Columns(C.Structure):
 COLUMN_FIELDS = ("data", "ends", "count", "status", "crc")
 
 
+class Table(C.Structure):
+    """tpz_table: block first keys + the columns tpz_decode_blocks wrote for the table."""
+    _fields_ = [("d_first_keys", C.c_void_p), ("d_first_pos", C.c_void_p), ("d_ext", C.c_void_p),
+                ("n_blocks", C.c_uint32), ("d_data", C.c_void_p), ("d_ends", C.c_void_p),
+                ("d_count", C.c_void_p), ("d_status", C.c_void_p)]
+
+
 _lib = None
 
 
@@ -81,6 +88,14 @@ def lib() -> C.CDLL:
         L.tpz_format_block_error.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_char_p,
                                              C.c_size_t]
         L.tpz_last_error.restype = C.c_char_p
+        L.tpz_seek_keys.argtypes = [C.c_void_p, C.POINTER(Table), C.c_void_p, C.c_void_p,
+                                    C.c_uint32] + [C.c_void_p] * 5
+        L.tpz_seek_keys.restype = C.c_int
+        L.tpz_bloom_may_contain.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                            C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.tpz_bloom_may_contain.restype = C.c_int
+        L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
+        L.tpz_host_xxh3_64.restype = C.c_uint64
         for f in ("slot_base", "entry_base", "data_capacity", "entry_capacity"):
             fn = getattr(L, "tpz_layout_" + f)
             fn.argtypes = [C.c_uint64, C.c_uint64]
@@ -184,3 +199,25 @@ class Context:
         check(lib().tpz_verify_files(self.handle, C.byref(b), C.c_void_p(d_crc),
                                      C.c_void_p(d_status), C.c_void_p(stream)),
               "tpz_verify_files")
+
+    def seek_keys_ptrs(self, table: Table, d_keys: int, d_key_pos: int, n_keys: int,
+                       d_block: int, d_entry: int, d_status: int, d_valid: int,
+                       stream: int = 0) -> None:
+        """tpz_seek_keys: SsTableIterator::seek_to_key for every key (table/iterator.rs:44-72)."""
+        check(lib().tpz_seek_keys(self.handle, C.byref(table), C.c_void_p(d_keys),
+                                  C.c_void_p(d_key_pos), n_keys, C.c_void_p(d_block),
+                                  C.c_void_p(d_entry), C.c_void_p(d_status), C.c_void_p(d_valid),
+                                  C.c_void_p(stream)), "tpz_seek_keys")
+
+    def bloom_ptrs(self, d_filter: int, filter_len: int, d_keys: int, d_key_pos: int,
+                   n_keys: int, d_out: int, stream: int = 0) -> None:
+        """tpz_bloom_may_contain: SsTable::may_contain for every key (table.rs:114-119)."""
+        check(lib().tpz_bloom_may_contain(self.handle, C.c_void_p(d_filter), filter_len,
+                                          C.c_void_p(d_keys), C.c_void_p(d_key_pos), n_keys,
+                                          C.c_void_p(d_out), C.c_void_p(stream)),
+              "tpz_bloom_may_contain")
+
+
+def xxh3_64(b: bytes) -> int:
+    """xxh3_64 on the host through the library (tpz_host_xxh3_64)."""
+    return int(lib().tpz_host_xxh3_64(b, len(b)))

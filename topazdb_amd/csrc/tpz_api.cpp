@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "tpz_internal.h"
+#include "tpz_xxh3.h"
 
 namespace {
 
@@ -366,6 +367,40 @@ tpz_err tpz_verify_files(tpz_ctx* c, const tpz_batch* f, uint32_t* d_crc, uint8_
                          void* stream) {
   if (!d_status) return TPZ_ERR_INVALID_ARG;
   return crc_ranges(c, f, 4, d_crc, d_status, stream);
+}
+
+tpz_err tpz_seek_keys(tpz_ctx* c, const tpz_table* t, const uint8_t* d_keys,
+                      const uint64_t* d_key_pos, uint32_t n_keys, uint32_t* d_block,
+                      uint32_t* d_entry, uint8_t* d_status, uint8_t* d_valid, void* stream) {
+  if (!c || !t || !d_key_pos || !d_block || !d_entry || !d_status || !d_valid)
+    return TPZ_ERR_INVALID_ARG;
+  if (n_keys == 0) return TPZ_SUCCESS;
+  if (t->n_blocks && (!t->d_first_keys || !t->d_first_pos || !t->d_ext || !t->d_data ||
+                      !t->d_ends || !t->d_count || !t->d_status))
+    return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz::SeekLaunch a{t->d_first_keys, t->d_first_pos, t->n_blocks, t->d_ext, t->d_data,
+                    t->d_ends, t->d_count, t->d_status, d_keys, d_key_pos, n_keys,
+                    d_block, d_entry, d_status, d_valid};
+  tpz::launch_seek(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filter_len,
+                              const uint8_t* d_keys, const uint64_t* d_key_pos, uint32_t n_keys,
+                              uint8_t* d_out, void* stream) {
+  if (!c || !d_key_pos || !d_out || (filter_len && !d_filter)) return TPZ_ERR_INVALID_ARG;
+  if (n_keys == 0) return TPZ_SUCCESS;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz::BloomLaunch a{d_filter, filter_len, d_keys, d_key_pos, n_keys, d_out};
+  tpz::launch_bloom(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len) {
+  return tpz::xxh3::hash64(h_buf, len);
 }
 
 int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actual, char* buf,

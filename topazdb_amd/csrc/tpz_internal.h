@@ -72,6 +72,35 @@ struct CrcLaunch {
 
 void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream);
 
+struct SeekLaunch {
+  const uint8_t* fk;
+  const uint64_t* fk_pos;
+  uint32_t n_blocks;
+  const uint64_t* ext;
+  const uint8_t* data;
+  const uint32_t* ends;
+  const uint32_t* count;
+  const uint8_t* bstatus;
+  const uint8_t* q;
+  const uint64_t* q_pos;
+  uint32_t n_q;
+  uint32_t* out_block;
+  uint32_t* out_entry;
+  uint8_t* out_status;
+  uint8_t* out_valid;
+};
+void launch_seek(const SeekLaunch& a, hipStream_t stream);
+
+struct BloomLaunch {
+  const uint8_t* filter;
+  uint64_t filter_len;
+  const uint8_t* q;
+  const uint64_t* q_pos;
+  uint32_t n_q;
+  uint8_t* out;
+};
+void launch_bloom(const BloomLaunch& a, hipStream_t stream);
+
 struct CodecLaunch {
   const uint8_t* src;
   const uint64_t* ext;

@@ -1,0 +1,176 @@
+// tpz_seek.hip — gfx950 kernels for the batched point-get side of an SSTable (SURVEY.md §8f
+// row 4), over a table whose blocks tpz_decode_blocks has decoded into the slotted columns.
+//
+//   seek_kernel   SsTableIterator::seek_to_key (src/table/iterator.rs:44-72, 74-79): for every
+//                 query key, find_block_idx (src/table.rs:178-182: partition_point(first_key <=
+//                 key) - 1, saturating), BlockIterator::seek_to_key in that block
+//                 (src/block/iterator.rs:91-109: binary search, an equal key returns at once, else
+//                 the lower bound), and, when the block iterator is invalid and a next block
+//                 exists, seek_to_first of the next block.
+//   bloom_kernel  SsTable::may_contain (src/table.rs:114-119) = Bloom::may_contain
+//                 (src/bloom.rs:72-84) of xxh3_64(key) (xxhash-rust 0.8.5).
+//
+// One thread per query: both are a few binary-search steps of dependent global loads (keys of a
+// few tens of bytes), latency-bound, so the launch simply puts many queries in flight. A query
+// whose block did not decode gets that block's status (the reference's read_block_cached Err, or
+// its panic for MALFORMED); OVERLAP blocks (a device limit) report OVERLAP.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tpz_internal.h"
+#include "tpz_xxh3.h"
+
+namespace tpz {
+
+namespace {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+// memcmp then length, as Rust's Ord for [u8]
+__device__ __forceinline__ int key_cmp(const uint8_t* a, u64 al, const uint8_t* b, u64 bl) {
+  const u64 n = al < bl ? al : bl;
+  for (u64 i = 0; i < n; i++) {
+    const u32 x = a[i], y = b[i];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+struct SeekParams {
+  const uint8_t* fk;        // block first keys, packed
+  const u64* fk_pos;        // n_blocks + 1
+  u32 n_blocks;
+  const u64* ext;           // the data region's block extents (slot bases)
+  const uint8_t* data;      // decoded columns
+  const u32* ends;
+  const u32* count;
+  const uint8_t* bstatus;
+  const uint8_t* q;         // query keys, packed
+  const u64* q_pos;         // n_q + 1
+  u32 n_q;
+  u32* out_block;
+  u32* out_entry;
+  uint8_t* out_status;
+  uint8_t* out_valid;
+};
+
+// Entry j's key in block b: its bytes and length.
+__device__ __forceinline__ const uint8_t* entry_key(const SeekParams& p, u32 b, u32 j, u64& len) {
+  const u64 e0 = p.ext[b];
+  const u64 s = slot_base(e0, b), e = entry_base(e0, b);
+  const u32 lo = j ? p.ends[2 * (e + j - 1)] : 0u, hi = p.ends[2 * (e + j)];
+  len = hi - lo;
+  return p.data + s + lo;
+}
+
+__global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_q) return;
+  const uint8_t* qk = p.q + p.q_pos[i];
+  const u64 ql = p.q_pos[i + 1] - p.q_pos[i];
+  if (p.n_blocks == 0) {                      // block_metas[0]: the reference panics
+    p.out_block[i] = 0;
+    p.out_entry[i] = 0;
+    p.out_status[i] = TPZ_BLOCK_MALFORMED;
+    p.out_valid[i] = 0;
+    return;
+  }
+  // find_block_idx: partition_point(first_key <= key) (the lower-bound bisection), minus one
+  u32 lo = 0, hi = p.n_blocks;
+  while (lo < hi) {
+    const u32 mid = lo + (hi - lo) / 2;
+    const u64 a = p.fk_pos[mid];
+    if (key_cmp(p.fk + a, p.fk_pos[mid + 1] - a, qk, ql) <= 0) lo = mid + 1; else hi = mid;
+  }
+  u32 b = lo ? lo - 1 : 0;
+  u32 st = p.bstatus[b], pos = 0;
+  bool valid = false;
+  if (st == TPZ_BLOCK_OK) {
+    // BlockIterator::seek_to_key
+    const u32 n = p.count[b];
+    u32 l = 0, r = n;
+    pos = n;
+    bool found = false;
+    while (l < r) {
+      const u32 mid = (r - l) / 2 + l;
+      u64 kl;
+      const uint8_t* k = entry_key(p, b, mid, kl);
+      const int c = key_cmp(k, kl, qk, ql);
+      if (c > 0) r = mid;
+      else if (c < 0) l = mid + 1;
+      else { pos = mid; found = true; break; }
+    }
+    if (!found) pos = l;
+    u64 kl = 0;
+    if (pos < n) entry_key(p, b, pos, kl);
+    valid = pos < n && kl > 0;                // is_valid: the current key is non-empty
+    if (!valid && b + 1 < p.n_blocks) {       // the next block, from its first entry
+      b++;
+      st = p.bstatus[b];
+      pos = 0;
+      valid = false;
+      if (st == TPZ_BLOCK_OK && p.count[b] > 0) {
+        entry_key(p, b, 0, kl);
+        valid = kl > 0;
+      }
+    }
+  }
+  p.out_block[i] = b;
+  p.out_entry[i] = pos;
+  p.out_status[i] = (uint8_t)st;
+  p.out_valid[i] = st == TPZ_BLOCK_OK && valid;
+}
+
+struct BloomParams {
+  const uint8_t* filter;    // Bloom::encode: the bit array, then k in the last byte
+  u64 filter_len;
+  const uint8_t* q;
+  const u64* q_pos;
+  u32 n_q;
+  uint8_t* out;
+};
+
+__global__ __launch_bounds__(256) void bloom_kernel(BloomParams p) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_q) return;
+  const u64 a = p.q_pos[i];
+  u64 h = xxh3::hash64(p.q + a, p.q_pos[i + 1] - a);
+  if (p.filter_len == 0) {                    // filter.last().unwrap() panics
+    p.out[i] = 2;
+    return;
+  }
+  const u64 delta = (h >> 34) | (h << 30);
+  const u32 k = p.filter[p.filter_len - 1];
+  const u64 limit = (p.filter_len - 1) * 8;
+  if (limit == 0) {                           // no bit array: `% 0` panics unless k == 0
+    p.out[i] = k ? 2 : 1;
+    return;
+  }
+  uint8_t hit = 1;
+  for (u32 j = 0; j < k; j++) {
+    const u64 bit = h % limit;
+    if (!(p.filter[bit >> 3] & (1u << (bit & 7)))) {
+      hit = 0;
+      break;
+    }
+    h += delta;
+  }
+  p.out[i] = hit;
+}
+
+}  // namespace
+
+void launch_seek(const SeekLaunch& a, hipStream_t stream) {
+  SeekParams p{a.fk, a.fk_pos, a.n_blocks, a.ext, a.data, a.ends, a.count, a.bstatus,
+               a.q, a.q_pos, a.n_q, a.out_block, a.out_entry, a.out_status, a.out_valid};
+  hipLaunchKernelGGL(seek_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
+}
+
+void launch_bloom(const BloomLaunch& a, hipStream_t stream) {
+  BloomParams p{a.filter, a.filter_len, a.q, a.q_pos, a.n_q, a.out};
+  hipLaunchKernelGGL(bloom_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
+}
+
+}  // namespace tpz

@@ -118,38 +118,115 @@ class Block:
         return r
 
 
+def _pack(keys: list[bytes]) -> tuple[np.ndarray, np.ndarray]:
+    pos = np.zeros(len(keys) + 1, np.int64)
+    np.cumsum([len(k) for k in keys], out=pos[1:])
+    buf = np.frombuffer(b"".join(keys) or b"\0", np.uint8)
+    return buf, pos
+
+
+class DeviceTable:
+    """The device side of a decoded SST data region, kept resident for batched point gets
+    (SURVEY.md §8f row 4): the blocks after the device codec step (snappy and lz4 blocks,
+    compress.rs:104-111), their slotted columns (tpz_decode_blocks), the block metas' first keys
+    and the bloom filter. `seek_keys` runs SsTableIterator::seek_to_key for a whole batch of keys
+    (tpz_seek_keys) and `may_contain` SsTable::may_contain (tpz_bloom_may_contain)."""
+
+    def __init__(self, ctx: Context, region: bytes, ext: np.ndarray,
+                 first_keys: list[bytes] | None = None, bloom: bytes | None = None):
+        self.ctx = ctx
+        dev = torch.device("cuda", ctx.device)
+        src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
+        batch = DeviceBatch(src, ext, ctx.device)
+        nb = self.n_blocks = batch.n_blocks
+        self.codec = None
+        if any(int(ext[b + 1]) > int(ext[b]) and region[int(ext[b + 1]) - 1] in (2, 3)
+               for b in range(nb)):
+            batch, st = decompress_batch(ctx, batch)
+            self.codec = st[:nb]
+        self.batch = batch
+        self.cols = decode_batch(ctx, batch)
+        # the status a reader of block i sees: the codec's Err wins over the decode of its stub
+        self.status = self.cols.status[:max(nb, 1)].clone()
+        if self.codec is not None:
+            self.status[:nb] = torch.where(self.codec != BLOCK_OK, self.codec, self.status[:nb])
+        fk, fpos = _pack(first_keys or [])
+        self.first_keys = torch.from_numpy(fk.copy()).to(dev)
+        self.first_pos = torch.from_numpy(fpos).to(dev)
+        self.bloom = None if bloom is None else torch.from_numpy(
+            np.frombuffer(bloom or b"\0", np.uint8).copy()).to(dev)
+        self.bloom_len = 0 if bloom is None else len(bloom)
+
+    def table(self) -> _lib.Table:
+        c = self.cols
+        return _lib.Table(self.first_keys.data_ptr(), self.first_pos.data_ptr(),
+                          self.batch.ext.data_ptr(), self.n_blocks, c.data.data_ptr(),
+                          c.ends.data_ptr(), c.count.data_ptr(), self.status.data_ptr())
+
+    def seek_keys(self, keys: list[bytes]) -> dict:
+        """SsTableIterator::seek_to_key (src/table/iterator.rs:44-72) for every key: the block
+        and entry it lands on, is_valid(), and the status of the last block it read (non-OK =
+        the reference's Err / panic). Numpy arrays, one entry per key."""
+        dev = torch.device("cuda", self.ctx.device)
+        n = len(keys)
+        buf, pos = _pack(keys)
+        q = torch.from_numpy(buf.copy()).to(dev)
+        qp = torch.from_numpy(pos).to(dev)
+        out = {k: torch.empty(max(n, 1), dtype=t, device=dev) for k, t in
+               (("block", torch.int32), ("entry", torch.int32), ("status", torch.uint8),
+                ("valid", torch.uint8))}
+        self.ctx.seek_keys_ptrs(self.table(), q.data_ptr(), qp.data_ptr(), n,
+                                out["block"].data_ptr(), out["entry"].data_ptr(),
+                                out["status"].data_ptr(), out["valid"].data_ptr(),
+                                torch.cuda.current_stream(dev).cuda_stream)
+        return {k: v[:n].cpu().numpy() for k, v in out.items()}
+
+    def may_contain(self, keys: list[bytes]) -> np.ndarray:
+        """SsTable::may_contain (src/table.rs:114-119) for every key: True without a filter."""
+        if self.bloom is None:
+            return np.ones(len(keys), bool)
+        dev = torch.device("cuda", self.ctx.device)
+        buf, pos = _pack(keys)
+        q = torch.from_numpy(buf.copy()).to(dev)
+        qp = torch.from_numpy(pos).to(dev)
+        out = torch.empty(max(len(keys), 1), dtype=torch.uint8, device=dev)
+        self.ctx.bloom_ptrs(self.bloom.data_ptr(), self.bloom_len, q.data_ptr(), qp.data_ptr(),
+                            len(keys), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        r = out[:len(keys)].cpu().numpy()
+        if (r == 2).any():
+            raise ReferencePanic("attempt to calculate the remainder with a divisor of zero")
+        return r.astype(bool)
+
+    def host_blocks(self) -> list:
+        """Per block a Block or the exception the reference's Block::decode would raise."""
+        torch.cuda.synchronize(torch.device("cuda", self.ctx.device))
+        batch, nb = self.batch, self.n_blocks
+        codec = None if self.codec is None else self.codec.cpu().numpy()
+        d = self.cols.dense(batch.ext_host)
+        dext = batch.ext_host.astype(np.int64)
+        out = []
+        for b in range(nb):
+            if codec is not None and codec[b] != BLOCK_OK:
+                out.append(_status_error(int(codec[b]), 0, 0))
+                continue
+            st = int(d.status[b])
+            lo, hi = int(dext[b]), int(dext[b + 1])
+            if st == BLOCK_OK:
+                out.append(Block.from_dense(d, b, hi - lo - 5))
+            else:
+                expected = 0
+                if hi - lo >= 5:
+                    expected = _be32(batch.src[hi - 5:hi - 1].cpu().numpy().tobytes())
+                out.append(_status_error(st, expected, int(d.crc_actual[b])))
+        return out
+
+
 def _decode_region(ctx: Context, region: bytes, ext: np.ndarray) -> list:
     """Decode blocks [ext[i], ext[i+1]) of `region`: snappy and lz4 blocks first go through the
     device codec step (compress.rs:104-111), then one tpz_decode_blocks launch decodes the batch.
     Returns per block a Block or the exception the reference's Block::decode / iteration would
     raise."""
-    src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
-    batch = DeviceBatch(src, ext, ctx.device)
-    nb = batch.n_blocks
-    codec = None
-    if any(int(ext[b + 1]) > int(ext[b]) and region[int(ext[b + 1]) - 1] in (2, 3)
-           for b in range(nb)):
-        batch, st = decompress_batch(ctx, batch)
-        codec = st[:nb].cpu().numpy()
-    cols = decode_batch(ctx, batch)
-    torch.cuda.synchronize(torch.device("cuda", ctx.device))
-    d = cols.dense(batch.ext_host)
-    dext = batch.ext_host.astype(np.int64)
-    out = []
-    for b in range(nb):
-        if codec is not None and codec[b] != BLOCK_OK:
-            out.append(_status_error(int(codec[b]), 0, 0))
-            continue
-        st = int(d.status[b])
-        lo, hi = int(dext[b]), int(dext[b + 1])
-        if st == BLOCK_OK:
-            out.append(Block.from_dense(d, b, hi - lo - 5))
-        else:
-            expected = 0
-            if hi - lo >= 5:
-                expected = _be32(batch.src[hi - 5:hi - 1].cpu().numpy().tobytes())
-            out.append(_status_error(st, expected, int(d.crc_actual[b])))
-    return out
+    return DeviceTable(ctx, region, ext).host_blocks()
 
 
 # ------------------------------------------------------------------------------- iterators
@@ -357,6 +434,7 @@ class SsTable:
     src/table.rs:167-175)."""
 
     def __init__(self, id: int, file: FileObject, metas, meta_off, bloom, blocks):
+        self.device = None
         self.id = id
         self.file = file
         self.block_metas = metas
@@ -395,17 +473,30 @@ class SsTable:
         if len(metas) and (np.diff(ext.astype(np.int64)) < 0).any():
             raise ReferencePanic("range start index out of range")  # read_block's end - offset
         region = file.read(0, meta_offset)
-        blocks = _decode_region(ctx, region, ext) if metas else []
+        dt = None
+        blocks = []
+        if metas:
+            dt = DeviceTable(ctx, region, ext, [m.first_key for m in metas],
+                             None if bloom is None else bloom.filter)
+            blocks = dt.host_blocks()
         t = cls(id, file, metas, meta_offset, bloom, blocks)
+        t.device = dt   # kept resident for batched seeks / bloom probes (seek_keys_gpu)
         t.init_samllest_biggest_key()
         return t
+
+    def seek_keys_gpu(self, keys: list[bytes]) -> dict:
+        """Batched SsTableIterator::seek_to_key on the device (tpz_seek_keys)."""
+        return self.device.seek_keys(keys)
+
+    def may_contain_gpu(self, keys: list[bytes]) -> np.ndarray:
+        """Batched SsTable::may_contain on the device (tpz_bloom_may_contain)."""
+        return self.device.may_contain(keys)
 
     def may_contain(self, key: bytes) -> bool:
         """table.rs:114-119 (xxh3_64 of the key)."""
         if self.bloom is None:
             return True
-        import xxhash
-        return self.bloom.may_contain(xxhash.xxh3_64_intdigest(key))
+        return self.bloom.may_contain(_lib.xxh3_64(key))
 
     def init_samllest_biggest_key(self) -> None:
         if not self.block_metas:
