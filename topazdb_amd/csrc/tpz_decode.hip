@@ -372,12 +372,37 @@ struct Out {
   u32* defer_count;
 };
 
+// Lane 0 stores block b's status, count and crc. Every lane issues the three buffer stores
+// (the others at an offset past the descriptor, which the hardware drops) instead of a
+// lane-0 branch: no exec-skip branch and its scalar bookkeeping per block, and the block's
+// entry-ends stores are written the same way. Measured 2.05 -> 1.96 ms per 2^20 4k blocks
+// (profiles/r1/ablations_vmpad.jsonl, variant vm0 = this build).
+constexpr u32 kOob = 0x7FFFFFF8u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)0x7FFFFFF0, 0x00020000);
+}
 __device__ __forceinline__ void put_meta(const Out& o, u32 b, u32 st, u32 n, u32 crc) {
-  if (lane_id() == 0) {
-    o.status[b] = (uint8_t)st;
-    o.count[b] = n;
-    o.crc[b] = crc;
-  }
+  const bool l0 = lane_id() == 0;
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)st, whole_rsrc(o.status), l0 ? b : kOob, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(n, whole_rsrc(o.count), l0 ? 4 * b : kOob, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(crc, whole_rsrc(o.crc), l0 ? 4 * b : kOob, 0, 0);
+}
+// K VMEM ops that touch nothing (a zero-length descriptor), issued right behind the next
+// block's prefetch loads (diagnostic builds, TPZ_VMPAD=K): they make the compiler's wait for
+// those loads vmcnt(>= K) on every path. The shipped build issues none: the branch-free
+// meta/ends stores alone gave the gain (2.05 -> 1.96 ms per
+// 2^20 blocks) although the wait stays vmcnt(0), and padding on top measured slower
+// (profiles/r1/ablations_vmpad.jsonl).
+#ifndef TPZ_VMPAD
+#define TPZ_VMPAD 0                   // measured: 7/12/20 pads were 0.5-1.5 % slower than none
+#endif
+constexpr int kVmAfter = TPZ_VMPAD;
+template <int K>
+__device__ __forceinline__ void vm_pad(const Out& o) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)o.status, (short)0, 0, 0x00020000);
+#pragma unroll
+  // distinct, non-adjacent offsets: neither merged nor vectorized into fewer instructions
+  for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(0u, r, 256 * i, 0, 0);
 }
 
 // Bytes [lo, hi) of the 4-byte word d (lo, hi in 0..16, relative to the chunk start).
@@ -678,7 +703,10 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         knz_all = __builtin_popcountll(kmask);
       }
       const u32 vs = (ktot + 15) & ~15u;  // value stream start (tpz_value_start)
-      if (slots_fit && i < n_pad) ends_g[i] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(
+          __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
+                             act ? make_uint2(ki, vi) : make_uint2(0, 0)),
+          whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
       if (act && slots_fit) {
         // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
         // after the segment's end (ends beyond the map only occur in OVERLAP blocks)
@@ -879,6 +907,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   };
   u32 k = 0;  // this wave's block counter
   issue(b, 0, s_cur, e_cur);
+  vm_pad<kVmAfter>(p.out);
 
   while (b < p.n_blocks) {
     const u64 s = s_cur, e = e_cur;
@@ -902,6 +931,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       load_group((k >> 6) + 1, gs_nxt, ge_nxt);
     }
     issue(b, k, s_cur, e_cur);       // next block's loads fly while this one decodes
+    vm_pad<kVmAfter>(p.out);
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
     if (fits) {
