@@ -4,6 +4,7 @@
     python3 profiles/summarize.py gpurun_out/prof profiles/r1
 
 writes  profiles/r1/kernel_stats.csv     rocprofv3 --kernel-trace --stats summary (as produced)
+        profiles/r1/kernel_stats_codecs.csv  the same for the codec / seek measurements
         profiles/r1/pmc_summary.json     per-dispatch means of the PMC passes, decode_wave_kernel
         profiles/traffic.json            HBM bytes per launch for bench.py's roofline.traffic:
                                          (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the x2 being the
@@ -37,6 +38,9 @@ def main():
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    codecs = glob.glob(os.path.join(src, "trace_codecs", "**", "*kernel_stats.csv"), recursive=True)
+    if codecs:  # codec step, seek and the decodes of the codec batches (bench.py fields)
+        shutil.copy(codecs[0], os.path.join(dst, "kernel_stats_codecs.csv"))
     means = {}
     disp = 0
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
