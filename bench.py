@@ -455,33 +455,34 @@ def main():
         log(rank, "validation: all blocks OK, every key/value byte and end offset matches")
 
     e2e = None
-    if not args.no_e2e and rank == 0:
+    side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
+    if not args.no_e2e and side:
         try:
             e2e = round(e2e_rate(ctx, src, ext, dev), 2)
         except Exception as ex:  # reported, never the metric
             log(rank, f"e2e measurement failed: {ex}")
 
     fcrc = None
-    if rank == 0 and not args.no_file_crc:
+    if side and not args.no_file_crc:
         try:
             fcrc = file_crc_rate(ctx, batch, src, dev)
         except Exception as ex:  # reported, never the metric
             log(rank, f"file CRC measurement failed: {ex}")
 
     seek = None
-    if rank == 0 and not args.no_seek and args.config == "4k":
+    if side and not args.no_seek and args.config == "4k":
         try:
             seek = seek_rate(ctx, batch, cols, args.config, dev)
         except Exception as ex:  # reported, never the metric
             log(rank, f"seek measurement failed: {ex}")
 
     snappy = lz4 = None
-    if rank == 0 and not args.no_snappy:
+    if side and not args.no_snappy:
         try:
             snappy = codec_rate(ctx, src, ext, dev, "snappy")
         except Exception as ex:  # reported, never the metric
             log(rank, f"snappy measurement failed: {ex}")
-    if rank == 0 and not args.no_lz4:
+    if side and not args.no_lz4:
         try:
             lz4 = codec_rate(ctx, src, ext, dev, "lz4")
         except Exception as ex:  # reported, never the metric
