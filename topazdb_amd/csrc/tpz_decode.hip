@@ -16,10 +16,10 @@
 //    a device worklist by the wave path and decoded by a second kernel, one wave per block with
 //    a 92 KiB LDS window (TPZ_MAX_BLOCK_BYTES: every block a 64 KiB-target BlockBuilder can
 //    emit) and its entry table in a per-workgroup global scratch (no entry-count limit).
-//  CRC-32: payload split into 16-byte chunks aligned to the payload END; lane l folds chunks
-//  l, l+64, ... (Horner with a shift-by-1024 operator), then a lane tree (DPP row shifts, then
-//  readlane across rows) combines with shift-by-16*2^k operators. All operators are
-//  byte-sliced lookup tables in LDS (40 KiB).
+//  CRC-32: the payload is cut into 80-byte runs aligned to its END; lane l folds run l with
+//  five slice-by-16 steps (fused with the copy's windows on the wave path), then a lane tree
+//  (exec-masked shift-by-80*2^k lookups, DPP row shifts, readlane across rows) combines them.
+//  All operators are byte-sliced lookup tables in LDS (41 KiB).
 //  Decode: lanes parse 64 entries at a time (n, offsets, klen, vlen, bounds checks that mirror
 //  the reference's panics), DPP wave prefix sums give packed output positions in the block's
 //  output stream (key bytes, then value bytes from the next 16-byte boundary), and every
@@ -48,7 +48,7 @@ constexpr int kWavesPerWG = 12;
 constexpr int kWavesPerWG = 16;
 #endif
 constexpr int kWGThreads = kWave * kWavesPerWG;
-constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 40 KiB
+constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
 // wave path slot: [guard 96][window 4352][pad 32][entry table 512 x u32][map 288 x u16]
@@ -228,9 +228,8 @@ __device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
 // unchanged), so every LDS read is an aligned ds_read_b128 (80-byte lane stride: conflict-free
 // per 16 lanes); lane l folds run l (counted from the end) with five chained slice-by-16 steps;
 // super-rounds of 64 runs (5120 B, long blocks only) are chained with two shift-by-2560 steps.
-// Run l then sits 80*l bytes before the end: every lane applies shift-by-80*2^k for the set bits
-// k of l (six levels, the same instruction stream in all lanes), and the lanes' values are
-// XOR-ed together with DPP and readlane. Returns R0 (wave-uniform).
+// Run l then sits 80*l bytes before the end; crc_combine merges the lanes' values as a tree
+// (shift-by-80*2^k at level k, DPP, readlane). Returns R0 (wave-uniform).
 __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
   const u32 lane = lane_id();
