@@ -40,6 +40,7 @@ constexpr u32 kBigIn = 65536, kBigOut = 94208;       // the one-wave kernel
 constexpr u32 kGuard = 16;                           // readable bytes before each input window
 constexpr u32 kInSlack = 16 + 16;                    // staging offset (< 16) + header overread
 constexpr u64 kLz4MaxIn = kBigIn - kInSlack;         // 65504: compressed bytes a window takes
+constexpr uint8_t kLeftForWaveKernel = 0xFF;         // status the group pass leaves behind
 static_assert(kSmallWaves * (kGuard + kSmallIn + kSmallOut) <= 163840, "small LDS");
 static_assert(kGuard + kBigIn + kBigOut <= 163840, "big LDS");
 
@@ -135,6 +136,7 @@ struct CodecParams {
   uint8_t* status;
   u32* defer_list;
   u32* defer_count;
+  u32 group_pass;    // snappy_group_kernel ran first (status 0xFF = left for the wave kernel)
 };
 
 // ------------------------------------------------------------------ per-block work
@@ -601,10 +603,13 @@ __global__ __launch_bounds__(kWave * kSmallWaves) void codec_wave_kernel(CodecPa
     mj.D0 = p.dst_ext[bc];
     mj.D1 = p.dst_ext[bc + 1];
     mj.tag = mj.e > mj.s ? p.src[mj.e - 1] : 0u;
+    // blocks the group kernel decoded carry their final status; the rest are marked
+    const u32 left = (!p.group_pass || p.status[bc] == kLeftForWaveKernel) ? 1u : 0u;
     const u32 cnt = uni((p.n_blocks - g + S - 1) / S < (u32)kWave ? (p.n_blocks - g + S - 1) / S
                                                                   : (u32)kWave);
     STAMP(0);
     for (u32 k = 0; k < cnt; k++) {
+      if (!__builtin_amdgcn_readlane(left, k)) continue;
       BlockMeta m;
       m.s = readlane64(mj.s, k);
       m.e = readlane64(mj.e, k);
@@ -621,6 +626,152 @@ __global__ __launch_bounds__(kWave * kSmallWaves) void codec_wave_kernel(CodecPa
 #ifdef TPZ_CODEC_STAMPS
   st_.flush(lane == 0);
 #endif
+}
+
+// ------------------------------------------------------------------ snappy, G blocks per wave
+// The one-block-per-wave element loop is bound by instruction issue (its wave-uniform work runs
+// once per element per block). Here a wave decodes G snappy blocks at once, one per group of
+// W = 64 / G lanes: every group walks its own element chain with per-lane (group-uniform)
+// state, so each header decode, check and copy instruction serves G blocks; the groups diverge
+// only in which copy path a round takes and for how many iterations. Blocks it does not take
+// (other tags, blocks past the windows, an invalid or mismatching preamble) get status 0xFF and
+// are left to codec_wave_kernel, which runs next and skips every other block.
+#ifndef TPZ_CODEC_G
+#define TPZ_CODEC_G 2
+#endif
+constexpr int kGroupBlocks = TPZ_CODEC_G;
+constexpr int kGroupWaves = 16 / TPZ_CODEC_G;
+constexpr u32 kGroupSlot = kGuard + kSmallIn + kSmallOut;
+static_assert(kGroupWaves * kGroupBlocks * kGroupSlot <= 163840, "group LDS");
+
+template <int G>
+__global__ __launch_bounds__(kWave * kGroupWaves) void snappy_group_kernel(CodecParams p) {
+  constexpr u32 W = kWave / G;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kGroupWaves * G * kGroupSlot];
+  const u32 lane = lane_id();
+  const u32 gi = lane / W, sl = lane % W;
+  const u32 wid = uni(threadIdx.x >> 6);
+  uint8_t* in_win = lds + (wid * G + gi) * kGroupSlot + kGuard;
+  uint8_t* out_win = in_win + kSmallIn;
+  const u32 nw = gridDim.x * kGroupWaves, gw = blockIdx.x * kGroupWaves + wid;
+  for (u32 r = 0;; r++) {
+    const u64 b64 = ((u64)r * nw + gw) * G + gi;
+    if (uni((u32)(((u64)r * nw + gw) * G >= p.n_blocks))) break;  // no group has a block
+    const bool valid = b64 < p.n_blocks;
+    const u32 b = valid ? (u32)b64 : 0u;
+    u64 s = 0, e = 0, D0 = 0, D1 = 0;
+    u32 tag = 0;
+    if (valid) {
+      s = p.ext[b];
+      e = p.ext[b + 1];
+      D0 = p.dst_ext[b];
+      D1 = p.dst_ext[b + 1];
+      tag = e > s ? p.src[e - 1] : 0u;
+    }
+    const u64 len = e - s, dn = D1 - D0;
+    bool mine = valid && len > 1 && tag == 2 && len - 1 + kInSlack <= kSmallIn &&
+                dn + 16 <= kSmallOut && dn >= 2;
+    const u32 n = (u32)(len - 1);
+    // stage the compressed bytes at in_win[(s & 15) ..] (16-byte pieces; the piece that
+    // straddles the end of the source buffer is read byte by byte)
+    if (mine) {
+      const u64 ws = s & ~15ull;
+      const u32 nb = (u32)(s + n - ws);
+      for (u32 off = 16 * sl; off < nb; off += 16 * W) {
+        uint4 v;
+        if (ws + off + 16 <= p.src_bytes) {
+          v = *reinterpret_cast<const uint4*>(p.src + ws + off);
+        } else {
+          uint8_t t[16];
+          for (int i = 0; i < 16; i++) t[i] = ws + off + i < p.src_bytes ? p.src[ws + off + i] : 0;
+          v = *reinterpret_cast<const uint4*>(t);
+        }
+        *reinterpret_cast<uint4*>(in_win + off) = v;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* in = in_win + (u32)(s & 15);
+    const u32 a_out = (u32)(reinterpret_cast<uintptr_t>(p.dst + D0) & 15);
+    uint8_t* out = out_win + a_out;
+    // the varint preamble (at most 10 bytes); a mismatch with the sizes pass leaves the block
+    u32 ip = 0, want = 0;
+    if (mine) {
+      u64 v = 0;
+      u32 h = 0;
+      for (u32 i = 0; i < 10 && i < n; i++) {
+        const u32 c = in[i];
+        v |= (u64)(c & 0x7F) << (7 * i);
+        if (!(c & 0x80)) {
+          if (v <= 0xFFFFFFFFull) h = i + 1;
+          break;
+        }
+      }
+      mine = h != 0 && v + 1 == dn;
+      ip = h;
+      want = (u32)v;
+    }
+    if (valid && !mine && sl == 0) p.status[b] = kLeftForWaveKernel;
+    // the element loop: one element per group per round
+    bool ok = mine, run = mine && ip < n;
+    u32 d = 0;
+    while (__ballot(run)) {
+      if (run) {
+        const u32 w0 = lds_u32_lane(in + ip), w1 = lds_u32_lane(in + ip + 4);
+        const u32 tg = w0 & 0xFF, kind = tg & 3, t6 = tg >> 2;
+        const u32 x = (w0 >> 8) | (w1 << 24);
+        const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
+        u32 lx = nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1));
+        lx = lx < 0x7FFFFFFFu ? lx : 0x7FFFFFFFu;
+        const u32 ln = kind == 0 ? lx + 1 : (kind == 1 ? 4 + (t6 & 7) : t6 + 1);
+        const u32 hl = kind == 0 ? 1 + nb : (0x5320u >> (4 * kind)) & 15;
+        const u32 off = kind == 1 ? ((tg >> 5) << 8) | (x & 0xFF) : (kind == 2 ? x & 0xFFFF : x);
+        const u32 next = ip + hl + (kind == 0 ? ln : 0u);
+        if (d + ln > want || next > n || (kind != 0 && off - 1 >= d)) {
+          ok = false;                                   // snap's Err
+        } else if (kind == 0) {
+          // literal: head bytes to the next 4-byte boundary, then whole aligned dwords (the last
+          // may write up to 3 bytes past the literal, which later elements overwrite)
+          const u32 pad0 = (0u - (u32)reinterpret_cast<uintptr_t>(out + d)) & 3u;
+          const u32 pad = pad0 < ln ? pad0 : ln;
+          if (sl < pad) out[d + sl] = in[ip + hl + sl];
+          const u32 nd = (ln - pad + 3) >> 2;
+          u32* o = reinterpret_cast<u32*>(out + d + pad);
+          const uint8_t* i8 = in + ip + hl + pad;
+          for (u32 t = sl; t < nd; t += W) o[t] = lds_u32_lane(i8 + 4 * t);
+        } else {
+          // copy (<= 64 bytes): period `off` when it overlaps
+          for (u32 k = sl; k < ln; k += W) {
+            const u32 q = (u32)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+            out[d + k] = out[d - off + (off >= ln ? k : k - q * off)];
+          }
+        }
+        ip = next;
+        d += ln;
+        run = ok && ip < n;
+      }
+    }
+    ok = ok && d == want;
+    __builtin_amdgcn_wave_barrier();
+    if (mine) {
+      uint8_t* dst = p.dst + D0;
+      if (ok) {
+        if (sl == 0) out[want] = 1;                     // re-tagged Uncompress
+        __builtin_amdgcn_wave_barrier();
+        // store [0, dn): head bytes to the 16-byte boundary, whole pieces, tail bytes
+        const u32 head = (16 - a_out) & 15, h = head < dn ? head : (u32)dn;
+        const u32 body = ((u32)dn - h) & ~15u;
+        for (u32 k = sl; k < h; k += W) dst[k] = out_win[a_out + k];
+        for (u32 k = 16 * sl; k < body; k += 16 * W)
+          *reinterpret_cast<uint4*>(dst + h + k) = *reinterpret_cast<const uint4*>(out_win + a_out + h + k);
+        for (u32 k = h + body + sl; k < dn; k += W) dst[k] = out_win[a_out + k];
+        if (sl == 0) p.status[b] = TPZ_BLOCK_OK;
+      } else if (sl == 0) {
+        dst[dn - 1] = 0;                                // decodes as BAD_TAG
+        p.status[b] = TPZ_BLOCK_CODEC_ERROR;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 __global__ __launch_bounds__(kWave) void codec_big_kernel(CodecParams p) {
@@ -675,6 +826,16 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
   p.status = a.status;
   p.defer_list = a.defer_list;
   p.defer_count = a.defer_count;
+#ifndef TPZ_CODEC_NO_GROUPS
+  {
+    u32 gg = (a.n_blocks + kGroupBlocks * kGroupWaves - 1) / (kGroupBlocks * kGroupWaves);
+    if (gg > a.num_cus) gg = a.num_cus;
+    if (gg == 0) gg = 1;
+    p.group_pass = 1;
+    hipLaunchKernelGGL(snappy_group_kernel<kGroupBlocks>, dim3(gg), dim3(kWave * kGroupWaves), 0,
+                       stream, p);
+  }
+#endif
   u32 grid = (a.n_blocks + kSmallWaves - 1) / kSmallWaves;
   if (grid > a.num_cus) grid = a.num_cus;
   if (grid == 0) grid = 1;
