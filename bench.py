@@ -179,43 +179,77 @@ def cpu_baseline(src, ext, gen, n_ent, threads, target_s=12.0):
 
 # ------------------------------------------------------------------ H2D/D2H-inclusive
 def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
-    """Pinned host blocks -> H2D -> decode -> D2H of all columns, chunked and double-buffered
-    over two streams. Returns GiB/s of encoded input."""
+    """Pinned host blocks -> H2D -> decode -> pack the used entry ends (tpz_pack_ends) -> D2H of
+    the data stream, the dense ends and the per-block metadata, chunked over two streams. A
+    chunk's data and ends go back once its metadata (and so its entry total) is on the host,
+    which the host waits for while the next chunk already runs. Returns GiB/s of encoded input;
+    checks the returned entry totals against the input's."""
     nb = len(ext) - 1
     h_src = torch.from_numpy(src).pin_memory()
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
-    bufs = []
-    for i in range(2):
-        cb = min(chunk_blocks, nb)
-        cap = int(ext[cb] - ext[0]) + 64 if cb < nb else int(ext[-1])
-        cap = max(cap, int(max(ext[min(k + cb, nb)] - ext[k] for k in range(0, nb, cb))))
-        d_src = torch.empty(cap + 64, dtype=torch.uint8, device=dev)
-        d_ext = torch.empty(cb + 1, dtype=torch.int64, device=dev)
+    cb = min(chunk_blocks, nb)
+    cap = max(int(ext[min(k + cb, nb)] - ext[k]) for k in range(0, nb, cb))
+    slots = []
+    for _ in range(2):
         cols = SlottedColumns(cb, cap, dev.index)
-        h_cols = {k: torch.empty(getattr(cols, k).numel(), dtype=getattr(cols, k).dtype).pin_memory()
-                  for k in _lib.COLUMN_FIELDS}
-        bufs.append((d_src, d_ext, cols, h_cols))
+        slots.append({
+            "d_src": torch.empty(cap + 64, dtype=torch.uint8, device=dev),
+            "d_ext": torch.empty(cb + 1, dtype=torch.int64, device=dev),
+            "cols": cols,
+            "h_data": torch.empty(cols.data.numel(), dtype=torch.uint8).pin_memory(),
+            "h_dense": torch.empty(cols.ends.numel(), dtype=torch.int32).pin_memory(),
+            "h_count": torch.empty(cb, dtype=torch.int32).pin_memory(),
+            "h_status": torch.empty(cb, dtype=torch.uint8).pin_memory(),
+            "h_crc": torch.empty(cb, dtype=torch.int32).pin_memory(),
+            "h_total": torch.empty(1, dtype=torch.int64).pin_memory(),
+            "first": torch.zeros(cb + 1, dtype=torch.int64, device=dev),
+            "dense": torch.empty(cols.ends.numel(), dtype=torch.int32, device=dev),
+        })
+    h_ext = torch.from_numpy(ext.astype(np.int64)).pin_memory()
+    entries = [0]
+
+    def finish(job):
+        lo, hi, slot, ev, s, dense = job
+        ev.synchronize()
+        total = int(slot["h_total"][0])
+        entries[0] += total
+        dc = _lib.data_capacity(int(ext[hi] - ext[lo]), hi - lo)
+        with torch.cuda.stream(s):
+            slot["h_data"][:dc].copy_(slot["cols"].data[:dc], non_blocking=True)
+            slot["h_dense"][:2 * total].copy_(dense[:2 * total], non_blocking=True)
+
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for ci, lo in enumerate(range(0, nb, chunk_blocks)):
-        hi = min(nb, lo + chunk_blocks)
-        s = streams[ci & 1]
-        d_src, d_ext, cols, h_cols = bufs[ci & 1]
+    pending = None
+    for ci, lo in enumerate(range(0, nb, cb)):
+        hi = min(nb, lo + cb)
+        s, slot = streams[ci & 1], slots[ci & 1]
+        cols = slot["cols"]
         base, end = int(ext[lo]), int(ext[hi])
-        e = torch.from_numpy((ext[lo:hi + 1] - ext[lo]).astype(np.int64))
         with torch.cuda.stream(s):
-            d_src[:end - base].copy_(h_src[base:end], non_blocking=True)
-            d_ext[:hi - lo + 1].copy_(e, non_blocking=True)
-            ctx.decode_ptrs(d_src.data_ptr(), d_ext.data_ptr(), hi - lo, end - base,
+            slot["d_src"][:end - base].copy_(h_src[base:end], non_blocking=True)
+            slot["d_ext"][:hi - lo + 1].copy_(h_ext[lo:hi + 1], non_blocking=True)
+            slot["d_ext"][:hi - lo + 1] -= base
+            n = hi - lo
+            ctx.decode_ptrs(slot["d_src"].data_ptr(), slot["d_ext"].data_ptr(), n, end - base,
                             cols.ptrs(), s.cuda_stream)
-            dc = _lib.data_capacity(end - base, hi - lo)
-            sc = 2 * _lib.entry_capacity(end - base, hi - lo)
-            for k, n in (("data", dc), ("ends", sc), ("count", hi - lo), ("status", hi - lo),
-                         ("crc", hi - lo)):
-                h_cols[k][:n].copy_(getattr(cols, k)[:n], non_blocking=True)
+            first, dense = slot["first"], slot["dense"]
+            torch.cumsum(cols.count[:n].to(torch.int64), 0, out=first[1:n + 1])
+            _lib._pack_ends(ctx, slot["d_ext"].data_ptr(), n, end - base, cols.ptrs(),
+                            first.data_ptr(), dense.data_ptr(), s.cuda_stream)
+            slot["h_count"][:hi - lo].copy_(cols.count[:hi - lo], non_blocking=True)
+            slot["h_status"][:hi - lo].copy_(cols.status[:hi - lo], non_blocking=True)
+            slot["h_crc"][:hi - lo].copy_(cols.crc[:hi - lo], non_blocking=True)
+            slot["h_total"].copy_(first[hi - lo:hi - lo + 1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(s)
+        if pending is not None:
+            finish(pending)
+        pending = (lo, hi, slot, ev, s, dense)
+    finish(pending)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    return float(ext[-1] - ext[0]) / dt / GIB
+    return float(ext[-1] - ext[0]) / dt / GIB, entries[0]
 
 
 def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10) -> dict:
@@ -458,7 +492,9 @@ def main():
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
     if not args.no_e2e and side:
         try:
-            e2e = round(e2e_rate(ctx, src, ext, dev), 2)
+            e2e_v, e2e_entries = e2e_rate(ctx, src, ext, dev)
+            assert e2e_entries == int(n_ent.sum()), "e2e entry total"
+            e2e = round(e2e_v, 2)
         except Exception as ex:  # reported, never the metric
             log(rank, f"e2e measurement failed: {ex}")
 

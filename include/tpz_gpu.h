@@ -154,6 +154,14 @@ tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
 tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* out,
                           void* stream);
 
+/* Dense entry ends for consumers that copy a batch out (e.g. back to the host): the slotted
+ * ends reserve the worst case (a pair per 6 input bytes, ~1.33x the input) so that blocks need no
+ * prefix pass; this packs the used pairs. d_first = exclusive prefix sums of out->d_count
+ * (n_blocks + 1 entries, from the caller's device scan); block i's count[i] {kend, vend} pairs go
+ * to d_dense[2*d_first[i] .. 2*d_first[i+1]) (zeros for a block whose status is not OK). */
+tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* cols,
+                      const uint64_t* d_first, uint32_t* d_dense, void* stream);
+
 /* ---- whole-range CRC-32 ------------------------------------------------------------------
  * Ranges use the batch type: range i is d_src[d_ext[i] .. d_ext[i+1]) (d_ext non-decreasing,
  * n_blocks = number of ranges, src_bytes = d_ext[n]). Each range may be up to 2^35 bytes.

@@ -94,6 +94,9 @@ def lib() -> C.CDLL:
         L.tpz_bloom_may_contain.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
         L.tpz_bloom_may_contain.restype = C.c_int
+        L.tpz_pack_ends.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
+                                    C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tpz_pack_ends.restype = C.c_int
         L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
         L.tpz_host_xxh3_64.restype = C.c_uint64
         for f in ("slot_base", "entry_base", "data_capacity", "entry_capacity"):
@@ -216,6 +219,14 @@ class Context:
                                           C.c_void_p(d_keys), C.c_void_p(d_key_pos), n_keys,
                                           C.c_void_p(d_out), C.c_void_p(stream)),
               "tpz_bloom_may_contain")
+
+
+def _pack_ends(ctx, d_ext: int, n_blocks: int, src_bytes: int, cols: dict, d_first: int,
+               d_dense: int, stream: int = 0) -> None:
+    b = Batch(None, d_ext, n_blocks, src_bytes)
+    c = Columns(*[cols[f] for f in COLUMN_FIELDS])
+    check(lib().tpz_pack_ends(ctx.handle, C.byref(b), C.byref(c), C.c_void_p(d_first),
+                              C.c_void_p(d_dense), C.c_void_p(stream)), "tpz_pack_ends")
 
 
 def xxh3_64(b: bytes) -> int:

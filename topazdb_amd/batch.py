@@ -144,6 +144,24 @@ def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None =
     return cols
 
 
+def pack_ends(ctx: Context, batch: DeviceBatch, cols: SlottedColumns,
+              stream: torch.cuda.Stream | None = None):
+    """tpz_pack_ends: the used {kend, vend} pairs of every block, dense in block order (for a
+    copy back to the host; the slotted ends reserve the worst case). Returns (first, dense):
+    device int64 exclusive prefix sums of count (n_blocks + 1) and the int32 pairs, capacity
+    2 * tpz_entry_capacity (the used part is 2 * first[n])."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    nb = batch.n_blocks
+    with torch.cuda.stream(s):
+        first = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(cols.count[:nb].to(torch.int64), 0, out=first[1:])
+        dense = torch.empty(cols.ends.numel(), dtype=torch.int32, device=dev)
+    _lib._pack_ends(ctx, batch.ext.data_ptr(), nb, batch.src_bytes, cols.ptrs(), first.data_ptr(),
+                    dense.data_ptr(), s.cuda_stream)
+    return first, dense
+
+
 def crc32_ranges(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None
                  ) -> torch.Tensor:
     """checksum::calculate_checksum (src/checksum.rs:6-10) of every range of `batch` on the GPU

@@ -399,6 +399,19 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filt
   return TPZ_SUCCESS;
 }
 
+tpz_err tpz_pack_ends(tpz_ctx* c, const tpz_batch* b, const tpz_columns* cols,
+                      const uint64_t* d_first, uint32_t* d_dense, void* stream) {
+  if (!c || !b || !cols || !d_first || !d_dense) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks == 0) return TPZ_SUCCESS;
+  if (!b->d_ext || !cols->d_ends || !cols->d_count || !cols->d_status) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz::PackLaunch a{b->d_ext, b->n_blocks, cols->d_ends, cols->d_count, cols->d_status, d_first,
+                    d_dense};
+  tpz::launch_pack_ends(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
 uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len) {
   return tpz::xxh3::hash64(h_buf, len);
 }

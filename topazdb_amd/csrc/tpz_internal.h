@@ -101,6 +101,17 @@ struct BloomLaunch {
 };
 void launch_bloom(const BloomLaunch& a, hipStream_t stream);
 
+struct PackLaunch {
+  const uint64_t* ext;
+  uint32_t n_blocks;
+  const uint32_t* ends;
+  const uint32_t* count;
+  const uint8_t* status;
+  const uint64_t* first;
+  uint32_t* dense;
+};
+void launch_pack_ends(const PackLaunch& a, hipStream_t stream);
+
 struct CodecLaunch {
   const uint8_t* src;
   const uint64_t* ext;

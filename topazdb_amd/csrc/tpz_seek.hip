@@ -160,7 +160,29 @@ __global__ __launch_bounds__(256) void bloom_kernel(BloomParams p) {
   p.out[i] = hit;
 }
 
+// Dense entry ends: block b's count[b] {kend, vend} pairs (status OK; zeros otherwise) moved
+// from its worst-case-sized slot (tpz_entry_base) to dense[2 * first[b] ..]. One wave per block.
+__global__ __launch_bounds__(256) void pack_ends_kernel(const u64* ext, u32 n, const u32* ends,
+                                                        const u32* count, const uint8_t* status,
+                                                        const u64* first, uint2* dense) {
+  const u32 lane = threadIdx.x & 63u;
+  const u32 nw = gridDim.x * (blockDim.x >> 6);
+  for (u32 b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < n; b += nw) {
+    const u64 f = first[b], c = first[b + 1] - f;
+    const bool ok = status[b] == TPZ_BLOCK_OK;
+    const uint2* src = reinterpret_cast<const uint2*>(ends) + entry_base(ext[b], b);
+    for (u64 j = lane; j < c; j += 64) dense[f + j] = ok ? src[j] : make_uint2(0, 0);
+  }
+}
+
 }  // namespace
+
+void launch_pack_ends(const PackLaunch& a, hipStream_t stream) {
+  u32 grid = (a.n_blocks + 3) / 4;
+  if (grid > 65535) grid = 65535;
+  hipLaunchKernelGGL(pack_ends_kernel, dim3(grid), dim3(256), 0, stream, a.ext, a.n_blocks,
+                     a.ends, a.count, a.status, a.first, reinterpret_cast<uint2*>(a.dense));
+}
 
 void launch_seek(const SeekLaunch& a, hipStream_t stream) {
   SeekParams p{a.fk, a.fk_pos, a.n_blocks, a.ext, a.data, a.ends, a.count, a.bstatus,
