@@ -73,7 +73,10 @@ typedef enum {
 /* ---- batch input -------------------------------------------------------------------------
  * Encoded blocks back to back in one device buffer (an SST data region [0, meta_off), or the
  * data regions of many SSTs concatenated). Block i is d_src[d_ext[i] .. d_ext[i+1]); d_ext has
- * n_blocks+1 entries and is non-decreasing. src_bytes = d_ext[n_blocks] (host copy). */
+ * n_blocks+1 entries and is non-decreasing. src_bytes = d_ext[n_blocks] (host copy). Blocks may
+ * start at any byte offset; d_src itself must be 16-byte aligned for tpz_decode_blocks and the
+ * codec step (hipMalloc returns 256-byte aligned memory; TPZ_ERR_INVALID_ARG otherwise). The
+ * CRC entry points take any d_src. */
 typedef struct {
   const uint8_t* d_src;
   const uint64_t* d_ext;

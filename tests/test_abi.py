@@ -180,3 +180,15 @@ def test_c_example_compiles_against_the_header(tmp_path):
     """The ABI is consumable from plain C (what a cgo/Rust/JNI binding sees): the example links
     against libtpz_gpu.so with gcc, no C++ and no torch types."""
     assert os.path.exists(_build_c_example(tmp_path))
+
+
+def test_unaligned_src_is_rejected():
+    """tpz_decode_blocks and the codec step require a 16-byte aligned d_src (include/tpz_gpu.h):
+    an unaligned pointer is TPZ_ERR_INVALID_ARG before any device work (no GPU needed)."""
+    L = _lib.lib()
+    b = _lib.Batch(0x1001, 0x2000, 1, 10)
+    c = _lib.Columns(0x3000, 0x4000, 0x5000, 0x6000, 0x7000)
+    assert L.tpz_decode_blocks(C.c_void_p(0x10), C.byref(b), C.byref(c), None) == \
+        _lib.ERR_INVALID_ARG
+    assert L.tpz_decompressed_sizes(C.c_void_p(0x10), C.byref(b), C.c_void_p(0x8000), None) == \
+        _lib.ERR_INVALID_ARG

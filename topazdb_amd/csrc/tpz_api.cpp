@@ -250,7 +250,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   if (!c || !b || !o) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
   if (!b->d_src || !b->d_ext || !o->d_data || !o->d_ends || !o->d_count || !o->d_status ||
-      !o->d_crc)
+      !o->d_crc || (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
     return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz_workspace* w = nullptr;
@@ -316,7 +316,8 @@ static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint
 tpz_err tpz_decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size, void* stream) {
   if (!c || !b || !d_size) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
-  if (!b->d_src || !b->d_ext) return TPZ_ERR_INVALID_ARG;
+  if (!b->d_src || !b->d_ext || (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
+    return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz::CodecLaunch a{};
   a.src = b->d_src;
@@ -333,7 +334,8 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
                               const uint64_t* d_dst_ext, uint8_t* d_status, void* stream) {
   if (!c || !b || !d_dst || !d_dst_ext || !d_status) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
-  if (!b->d_src || !b->d_ext) return TPZ_ERR_INVALID_ARG;
+  if (!b->d_src || !b->d_ext || (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
+    return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz_workspace* w = nullptr;
   {
