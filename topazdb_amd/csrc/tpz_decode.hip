@@ -64,12 +64,21 @@ static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 8 == 0, "slot alignment");
 constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
-// big path (one wave per block): [guard 96][window 92 KiB][pad 32][map u16]; the entry table
-// is in global scratch
+// big path (one 16-wave workgroup per block): [tables][guard 96][window 92 KiB][pad 32]
+// [map u16][group sums u64][window maxima u32][wave CRCs u32][entry table u64]; blocks whose
+// entry table does not fit the LDS one (2n + 1 > kBigLdsSlots) use global scratch
+constexpr int kBigWaves = 16;
+constexpr int kBigThreads = kBigWaves * kWave;
 constexpr int kBigWinBytes = 94208;
 constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
 constexpr int kBigMapLen = 5904;                    // >= (kBigMaxLen + 2) / 16 + 3
-constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2;
+constexpr int kBigStage = (kBigWinBytes + 16 * kBigThreads - 1) / (16 * kBigThreads);  // 6
+constexpr int kBigMaxGroups = 736;                  // n <= (P - 2) / 2 < 47096 entries / 64
+constexpr int kBigMaxWin = 96;                      // copy windows: npad / 64 <= 92
+constexpr int kBigLdsSlots = 1152;                  // u64 entries of the LDS entry table
+constexpr int kBigSuper = 20;                       // CRC super-rounds: ceil(94208 / 5120) <= 19
+constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2 +
+                        kBigMaxGroups * 8 + kBigMaxWin * 4 + kBigWaves * 4 + kBigLdsSlots * 8;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
 static_assert(kBigMapLen % 8 == 0 && (kWaveMaxLen + 2) / 16 + 3 <= (u32)kWaveMapLen &&
               (kBigMaxLen + 2) / 16 + 3 <= (u32)kBigMapLen, "map sizes");
@@ -184,6 +193,19 @@ __device__ __forceinline__ u32 crc_unshift_small(const u32* tab, u32 r, u32 k) {
   return r;
 }
 
+// a * b mod P in the reflected domain (bit 31 = x^0): R0(M || 0^n) = gf_mul(x^(8n) mod P,
+// R0(M)). Table-free (32 VALU steps): the big path shifts each wave's CRC by its distance to the
+// block end with it, once per wave and block.
+__device__ __forceinline__ u32 gf_mul(u32 a, u32 b) {
+  u32 p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    p ^= (a & (0x80000000u >> i)) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
+  }
+  return p;
+}
+
 // shift_n(A) = R_A(0^n) = XOR_i T_{n-1-i}[byte_i(A)], n = kCrcShiftBytes[J].
 template <int J>
 __device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
@@ -293,6 +315,23 @@ struct ColBig {
   __device__ __forceinline__ u32 end(u32 k) const { return (u32)ld(k); }
   __device__ __forceinline__ void get(u32 k, u32& end, int& delta) const {
     const u64 v = ld(k);
+    end = (u32)v;
+    delta = (int)(u32)(v >> 32);
+  }
+  __device__ __forceinline__ void get2(u32 k, u32& e0, int& d0, u32& e1, int& d1) const {
+    get(k, e0, d0);
+    get(k + 1, e1, d1);
+  }
+};
+// Big path, blocks with 2n + 1 <= kBigLdsSlots: the same {end, delta} entries in LDS.
+struct ColLds {
+  u64* t;
+  __device__ __forceinline__ void put(u32 k, u32 end, int delta) const {
+    t[k] = ((u64)(u32)delta << 32) | end;
+  }
+  __device__ __forceinline__ u32 end(u32 k) const { return (u32)t[k]; }
+  __device__ __forceinline__ void get(u32 k, u32& end, int& delta) const {
+    const u64 v = t[k];
     end = (u32)v;
     delta = (int)(u32)(v >> 32);
   }
@@ -836,6 +875,7 @@ struct Params {
   u32 n_blocks;
   const u32* crc_tables;
   Out out;
+  u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
 };
 
 // ------------------------------------------------------------------ wave path kernel
@@ -952,18 +992,156 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 }
 
 // ------------------------------------------------------------------ big path kernel
-__global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
+// Blocks the wave path defers (len > 4336 B or n > 255 entries) are decoded by one 16-wave
+// workgroup each (one workgroup per CU: the 92 KiB window). The phases run wave-parallel with
+// workgroup barriers between them:
+//   stage   every thread loads 16-B pieces of the block into the window (<= 6 per thread);
+//   parse   pass 1: each wave sums its 64-entry groups (key/value bytes, non-empty counts, bad)
+//           into LDS; pass 2: each wave re-parses its groups with the exclusive prefix of those
+//           sums, writes the entry ends, the entry table and the chunk map (as decode_block);
+//   copy    the maximum of the chunk map per 64-chunk window, then each wave copies its windows
+//           with the carry = the maximum over the windows before it (copy_window);
+//   CRC     wave w folds the 5120-B super-rounds r = w (mod 16) as wave_crc does and shifts each
+//           by its distance to the block end (gf_mul with x^(8*5120 r)); the 16 wave values
+//           XOR into R0 of the payload.
+// Group sums, packed: key bytes [0,17), value bytes [17,34), non-empty keys [34,41), non-empty
+// values [41,48), malformed [48] (key + value bytes <= dl < 2^17).
+__device__ __forceinline__ u32 wave_sum(u32 x) { return readlane(wave_scan_incl(x), 63); }
+__device__ __forceinline__ u32 wave_max(u32 x) { return readlane(wave_scan_max(x), 63); }
+
+struct BigSums {
+  u32 kb = 0, vb = 0, kn = 0, vn = 0;
+  bool bad = false;
+  // add the packed sums of groups [lo, hi) (wave-uniform)
+  __device__ __forceinline__ void add(const u64* gsum, u32 lo, u32 hi) {
+    const u32 lane = lane_id();
+    for (u32 u0 = lo; u0 < hi; u0 += 64) {
+      const u32 u = u0 + lane;
+      const u64 g = u < hi ? gsum[u] : 0ull;
+      kb += wave_sum((u32)g & 0x1FFFFu);
+      vb += wave_sum((u32)(g >> 17) & 0x1FFFFu);
+      const u32 c = wave_sum(((u32)(g >> 34) & 0x7Fu) | (((u32)(g >> 41) & 0x7Fu) << 16));
+      kn += c & 0xFFFFu;
+      vn += c >> 16;
+      bad |= __ballot((g >> 48) & 1ull) != 0;
+    }
+  }
+};
+
+// Entry i's key and value lengths (iterator.rs:74-82); 0/0 and ok = false when malformed.
+__device__ __forceinline__ void parse_entry(const uint8_t* win, u32 a0, u32 db, u32 dl, u32 i,
+                                            u32& off, u32& kl, u32& vl, bool& ok) {
+  off = lds_be16(win, a0 + 2 + 2 * i);
+  ok = off + 2 <= dl;
+  kl = vl = 0;
+  if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }
+  if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; }
+  if (!ok) kl = vl = 0;
+}
+
+// Parse + copy of a big block (n passed the header checks); returns its status so far.
+template <class Col, bool kGlobalCol>
+__device__ __forceinline__ u32 big_parse_copy(uint8_t* win, const Col& col, uint16_t* map,
+                                              u64* gsum, u32* wmax, u32 a0, u32 len, u32 n,
+                                              u32 b, u64 ext_b, const Out& o) {
+  const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
+  const u32 P = len - 5;
+  const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
+  const bool slots_fit = 6u * n <= len;
+  uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
+  const u32 n_pad = (n + 15) & ~15u;
+  const u32 G = (n + 63) >> 6;
+  // pass 1: group sums
+  for (u32 g = wid; g < G; g += kBigWaves) {
+    const u32 i = 64 * g + lane;
+    u32 off = 0, kl = 0, vl = 0;
+    bool ok = true;
+    if (i < n) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
+    const u32 kb = wave_sum(kl), vb = wave_sum(vl);
+    const u32 kn = __builtin_popcountll(__ballot(kl != 0)), vn = __builtin_popcountll(__ballot(vl != 0));
+    const bool bad = __ballot(!ok) != 0;
+    if (lane == 0)
+      gsum[g] = (u64)kb | ((u64)vb << 17) | ((u64)kn << 34) | ((u64)vn << 41) | ((u64)bad << 48);
+  }
+  __syncthreads();
+  BigSums T;
+  T.add(gsum, 0, G);
+  const u32 vs = (T.kb + 15) & ~15u;  // value stream start (tpz_value_start)
+  // pass 2: entry ends, entry table, chunk map
+  BigSums C;
+  u32 done = 0;
+  for (u32 g = wid; g < G; g += kBigWaves) {
+    C.add(gsum, done, g);
+    done = g;
+    const u32 i = 64 * g + lane;
+    const bool act = i < n;
+    u32 off = 0, kl = 0, vl = 0;
+    bool ok = true;
+    if (act) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
+    const u32 ki = wave_scan_incl(kl) + C.kb;
+    const u32 vi = wave_scan_incl(vl) + C.vb;
+    const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
+                           act ? make_uint2(ki, vi) : make_uint2(0, 0)),
+        whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
+    if (act && slots_fit) {
+      if (kl) {
+        const u32 m = C.kn + lanes_below(kmask);
+        col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
+        if (((ki + 15) >> 4) < (u32)kBigMapLen) map[(ki + 15) >> 4] = (uint16_t)(m + 1);
+      }
+      if (vl) {
+        const u32 m = T.kn + C.vn + lanes_below(vmask);
+        const u32 ve = vs + vi;
+        col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
+        if (((ve + 15) >> 4) < (u32)kBigMapLen) map[(ve + 15) >> 4] = (uint16_t)(m + 1);
+      }
+    }
+  }
+  if (kGlobalCol) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+  __syncthreads();
+  if (T.bad) return TPZ_BLOCK_MALFORMED;
+  if (!slots_fit || vs + T.vb > len + 2) return TPZ_BLOCK_OVERLAP;  // the slot holds len + 129 B
+#ifndef TPZ_ABL_NOCOPY
+  const u32 nk = T.kn + T.vn, tot = vs + T.vb;
+  const u32 nch = (tot + 15) >> 4;
+  const u32 npad = (nch + 7) & ~7u;
+  const u32 nw = (npad + 63) >> 6;
+  for (u32 v = wid; v < nw; v += kBigWaves) {
+    const u32 c = 64 * v + lane;
+    const u32 m = wave_max(c < nch ? (u32)map[min(c, (u32)kBigMapLen - 1)] : 0u);
+    if (lane == 0) wmax[v] = m;
+  }
+  __syncthreads();
+  uint8_t* dst = o.data + slot_base(ext_b, b);
+  for (u32 v = wid; v < nw; v += kBigWaves) {
+    u32 m = lane < v ? wmax[lane] : 0u;
+    if (lane + 64 < v) m = max(m, wmax[lane + 64]);
+    copy_window(Src16{win}, col, map, nk, nch, npad, dst, (u32)kBigMapLen, v, wave_max(m));
+  }
+#endif
+  return TPZ_BLOCK_OK;
+}
+
+__global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kBigLds];
   u32* tab = reinterpret_cast<u32*>(lds);
   load_tables(tab, p.crc_tables);
-  const u32 lane = lane_id();
+  const u32 tid = threadIdx.x, wid = uni(tid >> 6), lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
-  if (lane < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[lane] = make_uint4(0, 0, 0, 0);
-  const ColBig col{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots};
   uint16_t* map = reinterpret_cast<uint16_t*>(win + kBigWinBytes + 32);
-  Stamps S;
+  u64* gsum = reinterpret_cast<u64*>(map + kBigMapLen);
+  u32* wmax = reinterpret_cast<u32*>(gsum + kBigMaxGroups);
+  u32* xs = wmax + kBigMaxWin;
+  u64* ltab = reinterpret_cast<u64*>(xs + kBigWaves);
+  if (tid < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[tid] = make_uint4(0, 0, 0, 0);
   const u32 cnt = uni(*p.out.defer_count);
   for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
+    __syncthreads();  // the previous block is done with the window
     const u32 b = uni(p.out.defer_list[it]);
     const u64 s = uni64(p.ext[b]), e = uni64(p.ext[b + 1]);
     const u32 len = (u32)(e - s);
@@ -971,23 +1149,114 @@ __global__ __launch_bounds__(kWave, 1) void decode_big_kernel(Params p) {
     const u32 nbytes = (u32)(e - ws);
     const u64 e16 = (e + 15) & ~(u64)15;
     __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, p.src_bytes < e16 ? p.src_bytes : e16, ws);
-    for (u32 off = 0; off < nbytes; off += 4096) {
-      uint4 t[4];
+    uint4 t[kBigStage];
 #pragma unroll
-      for (int r = 0; r < 4; r++)
-        t[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + r * 1024 + lane * 16, 0, 0));
+    for (int r = 0; r < kBigStage; r++) {
+      const u32 off = (u32)r * 16 * kBigThreads + 16 * tid;
+      t[r] = off < nbytes ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
+                          : make_uint4(0, 0, 0, 0);
+    }
+    {
+      // clear the chunk map up to the largest chunk index a non-OVERLAP block can produce
+      const u32 nz = min((u32)kBigMapLen, ((len >> 4) + 3 + 7) / 8 * 8);
+      for (u32 i = tid; i < nz / 8; i += kBigThreads) reinterpret_cast<uint4*>(map)[i] = make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        fix_tail(t[r], p.src, ws + off + r * 1024 + lane * 16, p.src_bytes);
-        if (r == 0 && off == 0) t[0] = zero_head(t[0], lane == 0 ? (u32)(s & 15u) : 0u);
-        if (off + r * 1024 < nbytes) *reinterpret_cast<uint4*>(win + off + r * 1024 + lane * 16) = t[r];
+    for (int r = 0; r < kBigStage; r++) {
+      const u32 off = (u32)r * 16 * kBigThreads + 16 * tid;
+      if (off < nbytes) {
+        fix_tail(t[r], p.src, ws + off, p.src_bytes);
+        if (off == 0) t[r] = zero_head(t[r], (u32)(s & 15u));
+        *reinterpret_cast<uint4*>(win + off) = t[r];
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    decode_block<ColBig, uint16_t, kBigMapLen, true>(tab, win, col, map, (u32)(s & 15u), len, b,
-                                                     s, p.out, S);
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
+    const u32 a0 = (u32)(s & 15u);
+    const u32 tag = win[(int)(a0 + len) - 1];                                  // compress.rs:99
+    const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));    // block.rs:51
+    const u32 n = lds_be16(win, a0);                                           // block.rs:54
+    u32 st0 = 0;
+    if (len == 0) st0 = TPZ_BLOCK_EMPTY;                                       // compress.rs:96
+    else if (tag == 0 || tag > 3) st0 = TPZ_BLOCK_BAD_TAG;                      // :44-53,102
+    else if (tag != 1) st0 = TPZ_BLOCK_UNSUPPORTED_CODEC;
+    else if (len - 1 < 4) st0 = TPZ_BLOCK_MALFORMED;                            // block.rs:49
+    if (st0) {
+      if (wid == 0) put_meta(p.out, b, st0, 0, 0);
+      continue;
+    }
+    const u32 P = len - 5;
+    u32 st = TPZ_BLOCK_OK, bcnt = n;
+    if (P < 2 || P < 2 + 2 * n) {                                              // block.rs:54-59
+      st = TPZ_BLOCK_MALFORMED;
+    } else if (2 * n + 1 <= (u32)kBigLdsSlots) {
+      st = big_parse_copy<ColLds, false>(win, ColLds{ltab}, map, gsum, wmax, a0, len, n, b, s, p.out);
+    } else {
+      st = big_parse_copy<ColBig, true>(win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
+                                        map, gsum, wmax, a0, len, n, b, s, p.out);
+    }
+    if (st == TPZ_BLOCK_MALFORMED) bcnt = 0;
+    __syncthreads();  // the copy is done reading the window
+    u32 crc;
+    if (P >= 4) {
+      // as decode_block: init folded into the first four payload bytes, the k bytes up to the
+      // next 16-byte boundary zeroed, R0(payload' || 0^k) compared in the shifted domain
+      const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
+      if (wid == 0) {
+        if (lane < 4) win[a0 + lane] ^= 0xFFu;
+        if (lane < k) win[a0 + P + lane] = 0;
+      }
+      __syncthreads();
+      const u32 Pa = P + k;
+      const u32 Sr = (Pa + 5119) / 5120;
+      u32 A = 0;
+      for (u32 r = wid; r < Sr; r += kBigWaves) {
+        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+        const int seg = (int)Pa - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
+        u32 c = 0;
+        if (seg + kCrcLaneBytes > 0) {
+#pragma unroll
+          for (int q = 0; q < kCrcLaneBytes / 16; q++) {
+            const u32x4 w = *reinterpret_cast<const u32x4*>(win + (int)a0 + seg + 16 * q);
+            c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
+          }
+        }
+        A ^= gf_mul(p.xp[r], crc_combine(tab, c));
+      }
+      if (lane == 0) xs[wid] = A;
+      __syncthreads();
+      u32 R = 0;
+#pragma unroll
+      for (int w = 0; w < kBigWaves; w++) R ^= xs[w];
+      crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+    } else {
+      u32 c = 0xFFFFFFFFu;
+      for (u32 i = 0; i < P; i++) {
+        c ^= win[a0 + i];
+        for (int q = 0; q < 8; q++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+      }
+      crc = ~c;
+    }
+    if (crc != stored) {                                                       // checksum.rs:17
+      st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+      bcnt = 0;
+    }
+    if (wid == 0) put_meta(p.out, b, st, bcnt, crc);
   }
+}
+
+// x^(8 * 5120 r) mod P (reflected), r < kBigSuper: bit by bit from x^0 (0x80000000).
+static const u32* big_super_shifts() {
+  static const struct Xp {
+    u32 v[kBigSuper];
+    Xp() {
+      u32 x = 0x80000000u;
+      for (int r = 0; r < kBigSuper; r++) {
+        v[r] = x;
+        for (int i = 0; i < 8 * 5120; i++) x = (x >> 1) ^ ((x & 1u) ? 0xEDB88320u : 0u);
+      }
+    }
+  } xp;
+  return xp.v;
 }
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream) {
@@ -999,11 +1268,13 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.crc_tables = a.crc_tables;
   p.big_scratch = a.big_scratch;
   p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count};
+  const u32* xp = big_super_shifts();
+  for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
-  hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kWave), 0, stream, p);
+  hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p);
 }
 
 }  // namespace tpz
