@@ -1039,92 +1039,170 @@ __device__ __forceinline__ void parse_entry(const uint8_t* win, u32 a0, u32 db, 
   if (!ok) kl = vl = 0;
 }
 
-// Parse + copy of a big block (n passed the header checks); returns its status so far.
+// One big block after the header checks (all threads of the workgroup; n, stored read from the
+// window): parse, then the copy and the CRC in one phase (each wave copies its windows and folds
+// its super-rounds, so one wave's LDS latency hides behind another's work), then the status.
 template <class Col, bool kGlobalCol>
-__device__ __forceinline__ u32 big_parse_copy(uint8_t* win, const Col& col, uint16_t* map,
-                                              u64* gsum, u32* wmax, u32 a0, u32 len, u32 n,
-                                              u32 b, u64 ext_b, const Out& o) {
+__device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8_t* win,
+                                          const Col& col, uint16_t* map, u64* gsum, u32* wmax,
+                                          u32* xs, u32 a0, u32 len, u32 n, u32 stored, u32 b,
+                                          u64 ext_b) {
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
+  const Out& o = p.out;
   const u32 P = len - 5;
-  const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
-  const bool slots_fit = 6u * n <= len;
-  uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
-  const u32 n_pad = (n + 15) & ~15u;
-  const u32 G = (n + 63) >> 6;
-  // pass 1: group sums
-  for (u32 g = wid; g < G; g += kBigWaves) {
-    const u32 i = 64 * g + lane;
-    u32 off = 0, kl = 0, vl = 0;
-    bool ok = true;
-    if (i < n) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
-    const u32 kb = wave_sum(kl), vb = wave_sum(vl);
-    const u32 kn = __builtin_popcountll(__ballot(kl != 0)), vn = __builtin_popcountll(__ballot(vl != 0));
-    const bool bad = __ballot(!ok) != 0;
-    if (lane == 0)
-      gsum[g] = (u64)kb | ((u64)vb << 17) | ((u64)kn << 34) | ((u64)vn << 41) | ((u64)bad << 48);
-  }
-  __syncthreads();
-  BigSums T;
-  T.add(gsum, 0, G);
-  const u32 vs = (T.kb + 15) & ~15u;  // value stream start (tpz_value_start)
-  // pass 2: entry ends, entry table, chunk map
-  BigSums C;
-  u32 done = 0;
-  for (u32 g = wid; g < G; g += kBigWaves) {
-    C.add(gsum, done, g);
-    done = g;
-    const u32 i = 64 * g + lane;
-    const bool act = i < n;
-    u32 off = 0, kl = 0, vl = 0;
-    bool ok = true;
-    if (act) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
-    const u32 ki = wave_scan_incl(kl) + C.kb;
-    const u32 vi = wave_scan_incl(vl) + C.vb;
-    const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
-    __builtin_amdgcn_raw_buffer_store_b64(
-        __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
-                           act ? make_uint2(ki, vi) : make_uint2(0, 0)),
-        whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
-    if (act && slots_fit) {
-      if (kl) {
-        const u32 m = C.kn + lanes_below(kmask);
-        col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
-        if (((ki + 15) >> 4) < (u32)kBigMapLen) map[(ki + 15) >> 4] = (uint16_t)(m + 1);
-      }
-      if (vl) {
-        const u32 m = T.kn + C.vn + lanes_below(vmask);
-        const u32 ve = vs + vi;
-        col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
-        if (((ve + 15) >> 4) < (u32)kBigMapLen) map[(ve + 15) >> 4] = (uint16_t)(m + 1);
+  u32 st = TPZ_BLOCK_OK, bcnt = n;
+  u32 nk = 0, tot = 0;
+  bool copy = false;
+  if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
+    st = TPZ_BLOCK_MALFORMED;
+    bcnt = 0;
+  } else {
+#ifndef TPZ_ABL_NOPARSE
+    const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
+    const bool slots_fit = 6u * n <= len;
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
+    const u32 n_pad = (n + 15) & ~15u;
+    const u32 G = (n + 63) >> 6;
+    // pass 1: group sums
+    for (u32 g = wid; g < G; g += kBigWaves) {
+      const u32 i = 64 * g + lane;
+      u32 off = 0, kl = 0, vl = 0;
+      bool ok = true;
+      if (i < n) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
+      const u32 kb = wave_sum(kl), vb = wave_sum(vl);
+      const u32 kn = __builtin_popcountll(__ballot(kl != 0)), vn = __builtin_popcountll(__ballot(vl != 0));
+      const bool bad = __ballot(!ok) != 0;
+      if (lane == 0)
+        gsum[g] = (u64)kb | ((u64)vb << 17) | ((u64)kn << 34) | ((u64)vn << 41) | ((u64)bad << 48);
+    }
+    __syncthreads();
+    BigSums T;
+    T.add(gsum, 0, G);
+    const u32 vs = (T.kb + 15) & ~15u;  // value stream start (tpz_value_start)
+    // pass 2: entry ends, entry table, chunk map
+    BigSums C;
+    u32 done = 0;
+    for (u32 g = wid; g < G; g += kBigWaves) {
+      C.add(gsum, done, g);
+      done = g;
+      const u32 i = 64 * g + lane;
+      const bool act = i < n;
+      u32 off = 0, kl = 0, vl = 0;
+      bool ok = true;
+      if (act) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
+      const u32 ki = wave_scan_incl(kl) + C.kb;
+      const u32 vi = wave_scan_incl(vl) + C.vb;
+      const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+      __builtin_amdgcn_raw_buffer_store_b64(
+          __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
+                             act ? make_uint2(ki, vi) : make_uint2(0, 0)),
+          whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
+      if (act && slots_fit) {
+        if (kl) {
+          const u32 m = C.kn + lanes_below(kmask);
+          col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
+          if (((ki + 15) >> 4) < (u32)kBigMapLen) map[(ki + 15) >> 4] = (uint16_t)(m + 1);
+        }
+        if (vl) {
+          const u32 m = T.kn + C.vn + lanes_below(vmask);
+          const u32 ve = vs + vi;
+          col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
+          if (((ve + 15) >> 4) < (u32)kBigMapLen) map[(ve + 15) >> 4] = (uint16_t)(m + 1);
+        }
       }
     }
+    if (kGlobalCol) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    __syncthreads();
+    if (T.bad) {
+      st = TPZ_BLOCK_MALFORMED;
+      bcnt = 0;
+    } else if (!slots_fit || vs + T.vb > len + 2) {  // the slot holds len + 129 bytes
+      st = TPZ_BLOCK_OVERLAP;
+    } else {
+      copy = true;
+      nk = T.kn + T.vn;
+      tot = vs + T.vb;
+    }
+#endif
   }
-  if (kGlobalCol) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  }
-  __syncthreads();
-  if (T.bad) return TPZ_BLOCK_MALFORMED;
-  if (!slots_fit || vs + T.vb > len + 2) return TPZ_BLOCK_OVERLAP;  // the slot holds len + 129 B
-#ifndef TPZ_ABL_NOCOPY
-  const u32 nk = T.kn + T.vn, tot = vs + T.vb;
-  const u32 nch = (tot + 15) >> 4;
+#ifdef TPZ_ABL_NOCOPY
+  copy = false;
+#endif
+  const u32 nch = copy ? (tot + 15) >> 4 : 0u;
   const u32 npad = (nch + 7) & ~7u;
   const u32 nw = (npad + 63) >> 6;
+  // the copy's window maxima; the CRC's preparation as decode_block's (init folded into the
+  // first four payload bytes, the k bytes up to the next 16-byte boundary zeroed: the parse is
+  // done with them, and a copy chunk reading past its stream's end may see them, which leaves
+  // only unspecified bytes different)
   for (u32 v = wid; v < nw; v += kBigWaves) {
     const u32 c = 64 * v + lane;
     const u32 m = wave_max(c < nch ? (u32)map[min(c, (u32)kBigMapLen - 1)] : 0u);
     if (lane == 0) wmax[v] = m;
   }
-  __syncthreads();
-  uint8_t* dst = o.data + slot_base(ext_b, b);
-  for (u32 v = wid; v < nw; v += kBigWaves) {
-    u32 m = lane < v ? wmax[lane] : 0u;
-    if (lane + 64 < v) m = max(m, wmax[lane + 64]);
-    copy_window(Src16{win}, col, map, nk, nch, npad, dst, (u32)kBigMapLen, v, wave_max(m));
-  }
+  const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
+#if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
+  const bool crc_wave = false;
+#else
+  const bool crc_wave = P >= 4;
 #endif
-  return TPZ_BLOCK_OK;
+  if (crc_wave && wid == kBigWaves - 1) {
+    if (lane < 4) win[a0 + lane] ^= 0xFFu;
+    if (lane < k) win[a0 + P + lane] = 0;
+  }
+  __syncthreads();
+  // wave w: copy windows v = w (mod 16), CRC super-rounds r = w (mod 16)
+  const u32 Pa = P + k;
+  const u32 Sr = crc_wave ? (Pa + 5119) / 5120 : 0u;
+  uint8_t* dst = o.data + slot_base(ext_b, b);
+  u32 A = 0;
+  for (u32 j = wid; j < nw || j < Sr; j += kBigWaves) {
+    if (j < nw) {
+      u32 m = lane < j ? wmax[lane] : 0u;
+      if (lane + 64 < j) m = max(m, wmax[lane + 64]);
+      copy_window(Src16{win}, col, map, nk, nch, npad, dst, (u32)kBigMapLen, j, wave_max(m));
+    }
+    if (j < Sr) {
+      typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+      const int seg = (int)Pa - 5120 * (int)j - kCrcLaneBytes * (int)(lane + 1);
+      u32 c = 0;
+      if (seg + kCrcLaneBytes > 0) {
+#pragma unroll
+        for (int q = 0; q < kCrcLaneBytes / 16; q++) {
+          const u32x4 w = *reinterpret_cast<const u32x4*>(win + (int)a0 + seg + 16 * q);
+          c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
+        }
+      }
+      A ^= gf_mul(p.xp[j], crc_combine(tab, c));
+    }
+  }
+  if (lane == 0) xs[wid] = A;
+  __syncthreads();
+  u32 crc;
+  if (crc_wave) {
+    u32 R = 0;
+#pragma unroll
+    for (int w = 0; w < kBigWaves; w++) R ^= xs[w];
+    crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+  } else {
+    u32 c = 0xFFFFFFFFu;
+    for (u32 i = 0; i < P; i++) {
+      c ^= win[a0 + i];
+      for (int q = 0; q < 8; q++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    }
+    crc = ~c;
+  }
+#if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
+  crc = stored;
+#endif
+  if (crc != stored) {                                                         // checksum.rs:17
+    st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+    bcnt = 0;
+  }
+  if (wid == 0) put_meta(o, b, st, bcnt, crc);
 }
 
 __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
@@ -1140,22 +1218,50 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
   u64* ltab = reinterpret_cast<u64*>(xs + kBigWaves);
   if (tid < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[tid] = make_uint4(0, 0, 0, 0);
   const u32 cnt = uni(*p.out.defer_count);
-  for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
-    __syncthreads();  // the previous block is done with the window
-    const u32 b = uni(p.out.defer_list[it]);
-    const u64 s = uni64(p.ext[b]), e = uni64(p.ext[b + 1]);
-    const u32 len = (u32)(e - s);
-    const u64 ws = s & ~15ull;
-    const u32 nbytes = (u32)(e - ws);
-    const u64 e16 = (e + 15) & ~(u64)15;
+  if (blockIdx.x >= cnt) return;
+  const u32 grid = gridDim.x;
+  // This workgroup's blocks, 64 at a time: lane l holds the list entry and extent of its block
+  // 64 g + l (list position blockIdx.x + (64 g + l) * grid, clamped to the list).
+  u32 gb;
+  u64 gs, ge;
+  auto load_group = [&](u64 first) {
+    u64 pos = first + (u64)lane * grid;
+    pos = pos < cnt ? pos : cnt - 1;
+    gb = p.out.defer_list[pos];
+    gs = p.ext[gb];
+    ge = p.ext[gb + 1];
+  };
+  auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
+  // The next block's bytes are loaded into registers while this one decodes (16 B x <= 6 per
+  // thread); workgroup barriers only wait for LDS, so the loads stay in flight across them.
+  uint4 t[kBigStage];
+  u32 b_nx = 0;
+  u64 s_nx = 0, e_nx = 0;
+  auto issue = [&](u32 k) {
+    b_nx = readlane(gb, k & 63);
+    s_nx = lane64(gs, k & 63);
+    e_nx = lane64(ge, k & 63);
+    const u64 ws = s_nx & ~15ull;
+    const u32 nbytes = (u32)(e_nx - ws);
+    const u64 e16 = (e_nx + 15) & ~(u64)15;
     __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, p.src_bytes < e16 ? p.src_bytes : e16, ws);
-    uint4 t[kBigStage];
 #pragma unroll
     for (int r = 0; r < kBigStage; r++) {
       const u32 off = (u32)r * 16 * kBigThreads + 16 * tid;
       t[r] = off < nbytes ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0))
                           : make_uint4(0, 0, 0, 0);
     }
+  };
+  load_group(blockIdx.x);
+  issue(0);
+  u32 k = 0;
+  for (u32 it = blockIdx.x; it < cnt; it += grid, k++) {
+    const u32 b = b_nx;
+    const u64 s = s_nx, e = e_nx;
+    const u32 len = (u32)(e - s);
+    const u64 ws = s & ~15ull;
+    const u32 nbytes = (u32)(e - ws);
+    __syncthreads();  // the previous block is done with the window
     {
       // clear the chunk map up to the largest chunk index a non-OVERLAP block can produce
       const u32 nz = min((u32)kBigMapLen, ((len >> 4) + 3 + 7) / 8 * 8);
@@ -1171,7 +1277,15 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
       }
     }
     __syncthreads();
+    if ((u64)it + grid < cnt) {
+      if (((k + 1) & 63) == 0) load_group((u64)it + grid);
+      issue(k + 1);
+    }
     const u32 a0 = (u32)(s & 15u);
+#ifdef TPZ_ABL_LOADONLY
+    if (wid == 0) put_meta(p.out, b, TPZ_BLOCK_OK, win[a0], 0);
+    continue;
+#endif
     const u32 tag = win[(int)(a0 + len) - 1];                                  // compress.rs:99
     const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));    // block.rs:51
     const u32 n = lds_be16(win, a0);                                           // block.rs:54
@@ -1184,63 +1298,11 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
       if (wid == 0) put_meta(p.out, b, st0, 0, 0);
       continue;
     }
-    const u32 P = len - 5;
-    u32 st = TPZ_BLOCK_OK, bcnt = n;
-    if (P < 2 || P < 2 + 2 * n) {                                              // block.rs:54-59
-      st = TPZ_BLOCK_MALFORMED;
-    } else if (2 * n + 1 <= (u32)kBigLdsSlots) {
-      st = big_parse_copy<ColLds, false>(win, ColLds{ltab}, map, gsum, wmax, a0, len, n, b, s, p.out);
-    } else {
-      st = big_parse_copy<ColBig, true>(win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
-                                        map, gsum, wmax, a0, len, n, b, s, p.out);
-    }
-    if (st == TPZ_BLOCK_MALFORMED) bcnt = 0;
-    __syncthreads();  // the copy is done reading the window
-    u32 crc;
-    if (P >= 4) {
-      // as decode_block: init folded into the first four payload bytes, the k bytes up to the
-      // next 16-byte boundary zeroed, R0(payload' || 0^k) compared in the shifted domain
-      const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
-      if (wid == 0) {
-        if (lane < 4) win[a0 + lane] ^= 0xFFu;
-        if (lane < k) win[a0 + P + lane] = 0;
-      }
-      __syncthreads();
-      const u32 Pa = P + k;
-      const u32 Sr = (Pa + 5119) / 5120;
-      u32 A = 0;
-      for (u32 r = wid; r < Sr; r += kBigWaves) {
-        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-        const int seg = (int)Pa - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
-        u32 c = 0;
-        if (seg + kCrcLaneBytes > 0) {
-#pragma unroll
-          for (int q = 0; q < kCrcLaneBytes / 16; q++) {
-            const u32x4 w = *reinterpret_cast<const u32x4*>(win + (int)a0 + seg + 16 * q);
-            c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
-          }
-        }
-        A ^= gf_mul(p.xp[r], crc_combine(tab, c));
-      }
-      if (lane == 0) xs[wid] = A;
-      __syncthreads();
-      u32 R = 0;
-#pragma unroll
-      for (int w = 0; w < kBigWaves; w++) R ^= xs[w];
-      crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
-    } else {
-      u32 c = 0xFFFFFFFFu;
-      for (u32 i = 0; i < P; i++) {
-        c ^= win[a0 + i];
-        for (int q = 0; q < 8; q++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
-      }
-      crc = ~c;
-    }
-    if (crc != stored) {                                                       // checksum.rs:17
-      st = TPZ_BLOCK_CHECKSUM_MISMATCH;
-      bcnt = 0;
-    }
-    if (wid == 0) put_meta(p.out, b, st, bcnt, crc);
+    if (2 * n + 1 <= (u32)kBigLdsSlots)
+      big_block<ColLds, false>(p, tab, win, ColLds{ltab}, map, gsum, wmax, xs, a0, len, n, stored, b, s);
+    else
+      big_block<ColBig, true>(p, tab, win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
+                              map, gsum, wmax, xs, a0, len, n, stored, b, s);
   }
 }
 
