@@ -194,6 +194,37 @@ def test_tiny_entries_many_per_block(ctx):
     assert_parity(ctx, np.frombuffer(bytes(src), np.uint8), ext, expect_all_ok=True)
 
 
+def test_big_path_entry_groups(ctx):
+    """Big-path blocks (one 16-wave workgroup each) with 300..11000 entries: the entry table in
+    LDS (2n + 1 <= 1152) and in global scratch, 1..170 64-entry groups spread over the waves
+    (the cross-wave prefix of the group sums), and malformed offsets in early and late groups
+    of otherwise valid blocks (valid CRC: the status must be MALFORMED)."""
+    src = bytearray()
+    ext = [0]
+    ns = []
+    for t, target in enumerate([2500, 5000, 9000, 30000, 60000]):
+        bb = MG.BlockBuilder(target)
+        i = 0
+        while bb.add(bytes([65 + (i + t) % 26]) * (1 + i % 3), b"" if i % 4 else bytes([i & 255])):
+            i += 1
+        offs, data = bb.build()
+        ns.append(len(offs))
+        variants = [list(offs)]
+        late = list(offs)
+        late[-3] = len(data) + 7           # past the data region, in the last group
+        variants.append(late)
+        early = list(offs)
+        early[min(70, len(offs) - 1)] = len(data) - 1   # key length read past the data
+        variants.append(early)
+        for v in variants:
+            src += MG.encode_block(v, data)
+            ext.append(len(src))
+    assert max(ns) > 64 * 16 and min(ns) > 256 and any(2 * n + 1 <= 1152 for n in ns)
+    g, o = assert_parity(ctx, np.frombuffer(bytes(src), np.uint8), ext)
+    assert (o.status[0::3] == O.OK).all()
+    assert (o.status[1::3] == O.MALFORMED).all() and (o.status[2::3] == O.MALFORMED).all()
+
+
 def test_batch_not_starting_at_zero(ctx):
     """ext[0] > 0: blocks sit at arbitrary byte offsets of the device buffer."""
     src, ext = synth.make_region("4k", 50)

@@ -1039,23 +1039,67 @@ __device__ __forceinline__ void parse_entry(const uint8_t* win, u32 a0, u32 db, 
   if (!ok) kl = vl = 0;
 }
 
+// CRC super-round r of a big block's payload (wave_crc's lane runs), with decode_block's
+// preparation applied in registers instead of in the window (init folded into payload bytes
+// [0, 4), bytes [P, P + k) up to the 16-byte boundary zeroed), so the CRC can run while other
+// waves parse and copy from the same window. Returns Z_{5120 r}(R0 of the round) (uniform).
+__device__ __forceinline__ u32 big_crc_round(const Params& p, const u32* tab, const uint8_t* win,
+                                             u32 a0, u32 P, u32 Pa, u32 r) {
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+  const u32 lane = lane_id();
+  const int seg = (int)Pa - 5120 * (int)r - kCrcLaneBytes * (int)(lane + 1);
+  u32 c = 0;
+  if (seg + kCrcLaneBytes > 0) {
+#pragma unroll
+    for (int q = 0; q < kCrcLaneBytes / 16; q++) {
+      const int base = seg + 16 * q;  // payload-relative offset of the 16 bytes
+      u32x4 w = *reinterpret_cast<const u32x4*>(win + (int)a0 + base);
+      if (base < 4 || base + 16 > (int)P) {   // the first or the last chunk of the payload
+        const int zl = (int)P - base, zh = (int)Pa - base;
+        w.x = (w.x ^ byte_mask(-base, 4 - base, 0)) & ~byte_mask(zl, zh, 0);
+        w.y = (w.y ^ byte_mask(-base, 4 - base, 1)) & ~byte_mask(zl, zh, 1);
+        w.z = (w.z ^ byte_mask(-base, 4 - base, 2)) & ~byte_mask(zl, zh, 2);
+        w.w = (w.w ^ byte_mask(-base, 4 - base, 3)) & ~byte_mask(zl, zh, 3);
+      }
+      c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
+    }
+  }
+  return gf_mul(p.xp[r], crc_combine(tab, c));
+}
+
 // One big block after the header checks (all threads of the workgroup; n, stored read from the
-// window): parse, then the copy and the CRC in one phase (each wave copies its windows and folds
-// its super-rounds, so one wave's LDS latency hides behind another's work), then the status.
+// window). Phase 1: the waves that own 64-entry groups parse (one pass when the block has one
+// group, else group sums -> barrier -> pass 2) while the other waves fold the CRC super-rounds
+// (round r on wave 15 - r mod 16); phase 2: the copy's window maxima; phase 3: the copy; then
+// the wave CRCs are combined and the status stored.
 template <class Col, bool kGlobalCol>
 __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8_t* win,
                                           const Col& col, uint16_t* map, u64* gsum, u32* wmax,
                                           u32* xs, u32 a0, u32 len, u32 n, u32 stored, u32 b,
-                                          u64 ext_b) {
+                                          u64 ext_b, Stamps& S) {
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
   const Out& o = p.out;
   const u32 P = len - 5;
+  const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
+  const u32 Pa = P + k;
+#if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
+  const bool crc_wave = false;
+#else
+  const bool crc_wave = P >= 4;
+#endif
+  const u32 Sr = crc_wave ? (Pa + 5119) / 5120 : 0u;
+  u32 A = 0;
+  for (u32 r = kBigWaves - 1 - wid; r < Sr; r += kBigWaves) A ^= big_crc_round(p, tab, win, a0, P, Pa, r);
+  if (lane == 0) xs[wid] = A;
+  TPZ_STAMP(S, 4);
+
   u32 st = TPZ_BLOCK_OK, bcnt = n;
   u32 nk = 0, tot = 0;
   bool copy = false;
   if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
     st = TPZ_BLOCK_MALFORMED;
     bcnt = 0;
+    __syncthreads();
   } else {
 #ifndef TPZ_ABL_NOPARSE
     const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
@@ -1063,7 +1107,7 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
     const u32 n_pad = (n + 15) & ~15u;
     const u32 G = (n + 63) >> 6;
-    // pass 1: group sums
+    // pass 1: group sums (read back by the same wave when there is one group)
     for (u32 g = wid; g < G; g += kBigWaves) {
       const u32 i = 64 * g + lane;
       u32 off = 0, kl = 0, vl = 0;
@@ -1075,47 +1119,52 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
       if (lane == 0)
         gsum[g] = (u64)kb | ((u64)vb << 17) | ((u64)kn << 34) | ((u64)vn << 41) | ((u64)bad << 48);
     }
+    if (G > 1) __syncthreads();
+    // pass 2: entry ends, entry table, chunk map
+    if (wid < G) {
+      BigSums T;
+      T.add(gsum, 0, G);
+      const u32 vs = (T.kb + 15) & ~15u;  // value stream start (tpz_value_start)
+      BigSums C;
+      u32 done = 0;
+      for (u32 g = wid; g < G; g += kBigWaves) {
+        C.add(gsum, done, g);
+        done = g;
+        const u32 i = 64 * g + lane;
+        const bool act = i < n;
+        u32 off = 0, kl = 0, vl = 0;
+        bool ok = true;
+        if (act) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
+        const u32 ki = wave_scan_incl(kl) + C.kb;
+        const u32 vi = wave_scan_incl(vl) + C.vb;
+        const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
+                               act ? make_uint2(ki, vi) : make_uint2(0, 0)),
+            whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
+        if (act && slots_fit) {
+          if (kl) {
+            const u32 m = C.kn + lanes_below(kmask);
+            col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
+            if (((ki + 15) >> 4) < (u32)kBigMapLen) map[(ki + 15) >> 4] = (uint16_t)(m + 1);
+          }
+          if (vl) {
+            const u32 m = T.kn + C.vn + lanes_below(vmask);
+            const u32 ve = vs + vi;
+            col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
+            if (((ve + 15) >> 4) < (u32)kBigMapLen) map[(ve + 15) >> 4] = (uint16_t)(m + 1);
+          }
+        }
+      }
+      if (kGlobalCol) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      }
+    }
     __syncthreads();
     BigSums T;
     T.add(gsum, 0, G);
-    const u32 vs = (T.kb + 15) & ~15u;  // value stream start (tpz_value_start)
-    // pass 2: entry ends, entry table, chunk map
-    BigSums C;
-    u32 done = 0;
-    for (u32 g = wid; g < G; g += kBigWaves) {
-      C.add(gsum, done, g);
-      done = g;
-      const u32 i = 64 * g + lane;
-      const bool act = i < n;
-      u32 off = 0, kl = 0, vl = 0;
-      bool ok = true;
-      if (act) parse_entry(win, a0, db, dl, i, off, kl, vl, ok);
-      const u32 ki = wave_scan_incl(kl) + C.kb;
-      const u32 vi = wave_scan_incl(vl) + C.vb;
-      const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
-      __builtin_amdgcn_raw_buffer_store_b64(
-          __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
-                             act ? make_uint2(ki, vi) : make_uint2(0, 0)),
-          whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
-      if (act && slots_fit) {
-        if (kl) {
-          const u32 m = C.kn + lanes_below(kmask);
-          col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
-          if (((ki + 15) >> 4) < (u32)kBigMapLen) map[(ki + 15) >> 4] = (uint16_t)(m + 1);
-        }
-        if (vl) {
-          const u32 m = T.kn + C.vn + lanes_below(vmask);
-          const u32 ve = vs + vi;
-          col.put(m, ve, (int)(db + off + 4 + kl) - (int)(ve - vl));
-          if (((ve + 15) >> 4) < (u32)kBigMapLen) map[(ve + 15) >> 4] = (uint16_t)(m + 1);
-        }
-      }
-    }
-    if (kGlobalCol) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    }
-    __syncthreads();
+    const u32 vs = (T.kb + 15) & ~15u;
     if (T.bad) {
       st = TPZ_BLOCK_MALFORMED;
       bcnt = 0;
@@ -1126,83 +1175,57 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
       nk = T.kn + T.vn;
       tot = vs + T.vb;
     }
+#else
+    __syncthreads();
 #endif
   }
+  TPZ_STAMP(S, 1);
 #ifdef TPZ_ABL_NOCOPY
   copy = false;
 #endif
-  const u32 nch = copy ? (tot + 15) >> 4 : 0u;
-  const u32 npad = (nch + 7) & ~7u;
-  const u32 nw = (npad + 63) >> 6;
-  // the copy's window maxima; the CRC's preparation as decode_block's (init folded into the
-  // first four payload bytes, the k bytes up to the next 16-byte boundary zeroed: the parse is
-  // done with them, and a copy chunk reading past its stream's end may see them, which leaves
-  // only unspecified bytes different)
-  for (u32 v = wid; v < nw; v += kBigWaves) {
-    const u32 c = 64 * v + lane;
-    const u32 m = wave_max(c < nch ? (u32)map[min(c, (u32)kBigMapLen - 1)] : 0u);
-    if (lane == 0) wmax[v] = m;
-  }
-  const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
-#if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
-  const bool crc_wave = false;
-#else
-  const bool crc_wave = P >= 4;
-#endif
-  if (crc_wave && wid == kBigWaves - 1) {
-    if (lane < 4) win[a0 + lane] ^= 0xFFu;
-    if (lane < k) win[a0 + P + lane] = 0;
-  }
-  __syncthreads();
-  // wave w: copy windows v = w (mod 16), CRC super-rounds r = w (mod 16)
-  const u32 Pa = P + k;
-  const u32 Sr = crc_wave ? (Pa + 5119) / 5120 : 0u;
-  uint8_t* dst = o.data + slot_base(ext_b, b);
-  u32 A = 0;
-  for (u32 j = wid; j < nw || j < Sr; j += kBigWaves) {
-    if (j < nw) {
+  if (copy) {
+    const u32 nch = (tot + 15) >> 4;
+    const u32 npad = (nch + 7) & ~7u;
+    const u32 nw = (npad + 63) >> 6;
+    for (u32 v = wid; v < nw; v += kBigWaves) {
+      const u32 c = 64 * v + lane;
+      const u32 m = wave_max(c < nch ? (u32)map[min(c, (u32)kBigMapLen - 1)] : 0u);
+      if (lane == 0) wmax[v] = m;
+    }
+    __syncthreads();
+    TPZ_STAMP(S, 2);
+    uint8_t* dst = o.data + slot_base(ext_b, b);
+    for (u32 j = wid; j < nw; j += kBigWaves) {
       u32 m = lane < j ? wmax[lane] : 0u;
       if (lane + 64 < j) m = max(m, wmax[lane + 64]);
       copy_window(Src16{win}, col, map, nk, nch, npad, dst, (u32)kBigMapLen, j, wave_max(m));
     }
-    if (j < Sr) {
-      typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-      const int seg = (int)Pa - 5120 * (int)j - kCrcLaneBytes * (int)(lane + 1);
-      u32 c = 0;
-      if (seg + kCrcLaneBytes > 0) {
+    TPZ_STAMP(S, 3);
+  }
+  if (wid == 0) {
+    u32 crc;
+    if (crc_wave) {
+      u32 R = 0;
 #pragma unroll
-        for (int q = 0; q < kCrcLaneBytes / 16; q++) {
-          const u32x4 w = *reinterpret_cast<const u32x4*>(win + (int)a0 + seg + 16 * q);
-          c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
-        }
+      for (int w = 0; w < kBigWaves; w++) R ^= xs[w];
+      crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+    } else {
+      u32 c = 0xFFFFFFFFu;
+      for (u32 i = 0; i < P; i++) {
+        c ^= win[a0 + i];
+        for (int q = 0; q < 8; q++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
       }
-      A ^= gf_mul(p.xp[j], crc_combine(tab, c));
+      crc = ~c;
     }
-  }
-  if (lane == 0) xs[wid] = A;
-  __syncthreads();
-  u32 crc;
-  if (crc_wave) {
-    u32 R = 0;
-#pragma unroll
-    for (int w = 0; w < kBigWaves; w++) R ^= xs[w];
-    crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
-  } else {
-    u32 c = 0xFFFFFFFFu;
-    for (u32 i = 0; i < P; i++) {
-      c ^= win[a0 + i];
-      for (int q = 0; q < 8; q++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
-    }
-    crc = ~c;
-  }
 #if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
-  crc = stored;
+    crc = stored;
 #endif
-  if (crc != stored) {                                                         // checksum.rs:17
-    st = TPZ_BLOCK_CHECKSUM_MISMATCH;
-    bcnt = 0;
+    if (crc != stored) {                                                       // checksum.rs:17
+      st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+      bcnt = 0;
+    }
+    put_meta(o, b, st, bcnt, crc);
   }
-  if (wid == 0) put_meta(o, b, st, bcnt, crc);
 }
 
 __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
@@ -1254,6 +1277,10 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
   };
   load_group(blockIdx.x);
   issue(0);
+  Stamps S;
+#ifdef TPZ_ABL_STAMPS
+  S.last = stamp_now();
+#endif
   u32 k = 0;
   for (u32 it = blockIdx.x; it < cnt; it += grid, k++) {
     const u32 b = b_nx;
@@ -1277,6 +1304,7 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
       }
     }
     __syncthreads();
+    TPZ_STAMP(S, 0);
     if ((u64)it + grid < cnt) {
       if (((k + 1) & 63) == 0) load_group((u64)it + grid);
       issue(k + 1);
@@ -1299,11 +1327,17 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
       continue;
     }
     if (2 * n + 1 <= (u32)kBigLdsSlots)
-      big_block<ColLds, false>(p, tab, win, ColLds{ltab}, map, gsum, wmax, xs, a0, len, n, stored, b, s);
+      big_block<ColLds, false>(p, tab, win, ColLds{ltab}, map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
     else
       big_block<ColBig, true>(p, tab, win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
-                              map, gsum, wmax, xs, a0, len, n, stored, b, s);
+                              map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
+    TPZ_STAMP(S, 5);
   }
+#ifdef TPZ_ABL_STAMPS
+  const u32 gw = blockIdx.x * kBigWaves + wid;
+  if (lane == 0 && gw < (u32)kStampWaves)
+    for (int q = 0; q < 6; q++) g_stamps[gw * 8 + q] = S.t[q];
+#endif
 }
 
 // x^(8 * 5120 r) mod P (reflected), r < kBigSuper: bit by bit from x^0 (0x80000000).
