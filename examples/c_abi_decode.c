@@ -90,6 +90,12 @@ int main(int argc, char** argv) {
   CHECK_HIP(hipMalloc((void**)&cols.d_count, nb * sizeof(uint32_t)));
   CHECK_HIP(hipMalloc((void**)&cols.d_status, nb));
   CHECK_HIP(hipMalloc((void**)&cols.d_crc, nb * sizeof(uint32_t)));
+  /* BlockBuilder output never spills (include/tpz_gpu.h): no arena, but the per-block offsets
+   * and the used-bytes word are always given */
+  cols.d_spill = NULL;
+  cols.spill_cap = 0;
+  CHECK_HIP(hipMalloc((void**)&cols.d_spill_off, nb * sizeof(uint64_t)));
+  CHECK_HIP(hipMalloc((void**)&cols.d_spill_used, sizeof(uint64_t)));
   const tpz_batch batch = {d_src, d_ext, (uint32_t)nb, len};
   CHECK_TPZ(tpz_decode_blocks(ctx, &batch, &cols, stream));
 

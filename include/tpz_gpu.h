@@ -55,20 +55,23 @@ typedef enum {
   TPZ_BLOCK_MALFORMED = 5,         /* CRC-valid, but the reference panics on it: payload too
                                       short for n/offsets (block.rs:49-59) or an entry out of
                                       range (iterator.rs:74-82)                              */
-  TPZ_BLOCK_OVERLAP = 6,           /* CRC-valid and decodable by the reference, but entries
-                                      overlap so the decoded bytes exceed the block's slot:
-                                      6*n > len or value_start(K) + V > len + 2 (K, V = the
-                                      block's key and value bytes).
-                                      topazdb's BlockBuilder never writes such a block.      */
-  TPZ_BLOCK_TOO_LARGE = 7,         /* len > TPZ_MAX_BLOCK_BYTES (larger than any block a
-                                      block_size <= 64 KiB BlockBuilder emits); for a snappy
-                                      or lz4 block: compressed > 64 KiB - 31 or uncompressed >
-                                      TPZ_MAX_BLOCK_BYTES - 1                                */
+  TPZ_BLOCK_OK_SPILLED = 6,        /* Ok(Block); all entries decoded, into the spill arena
+                                      (tpz_columns.d_spill) instead of the block's slot: the
+                                      decoded bytes do not fit the slot (entries that overlap or
+                                      repeat, which iterator.rs:63-83 accepts: 6*n > len or
+                                      value_start(K) + V > len + 2), or the block is longer than
+                                      TPZ_LDS_BLOCK_BYTES. Same answer as TPZ_BLOCK_OK.        */
+  TPZ_BLOCK_SPILL_FULL = 7,        /* Ok(Block) in the reference, but the caller's spill arena
+                                      was too small for this block's record:
+                                      d_spill_off[i] = the bytes it needs. Decode again with
+                                      spill_cap >= *d_spill_used.                               */
   TPZ_BLOCK_CODEC_ERROR = 8        /* Err of the codec: snap's decompress_vec rejects the
                                       stream (compress.rs:104-107)                           */
 } tpz_block_status;
 
-#define TPZ_MAX_BLOCK_BYTES 94192u
+/* The largest block the LDS decode paths stage whole (every block a block_size <= 64 KiB
+ * BlockBuilder emits fits); longer blocks are decoded by the spill path, straight from HBM. */
+#define TPZ_LDS_BLOCK_BYTES 94192u
 
 /* ---- batch input -------------------------------------------------------------------------
  * Encoded blocks back to back in one device buffer (an SST data region [0, meta_off), or the
@@ -100,19 +103,47 @@ typedef struct {
  *           vs = tpz_value_start(K):
  *             key_j   = data[s +      (j ? ends[2(e+j-1)]   : 0) .. s +      ends[2(e+j)]]
  *             value_j = data[s + vs + (j ? ends[2(e+j-1)+1] : 0) .. s + vs + ends[2(e+j)+1]]
- *   count[i]  : entries in block i (n) for OK and OVERLAP, else 0
+ *   count[i]  : entries in block i (n) for OK, OK_SPILLED and SPILL_FULL, else 0
  *   status[i] : tpz_block_status
- *   crc[i]    : CRC-32 the device computed over the payload (valid for OK, MALFORMED,
- *               OVERLAP, CHECKSUM_MISMATCH; the stored one is the payload's trailing u32)
+ *   crc[i]    : CRC-32 the device computed over the payload (valid for OK, OK_SPILLED,
+ *               SPILL_FULL, MALFORMED, CHECKSUM_MISMATCH; the stored one is the payload's
+ *               trailing u32)
  * Bytes of a slot beyond the block's own data are unspecified. A slot spans at most
- * len + 129 bytes (len = the block's encoded length), which never reaches the next slot. */
+ * len + 129 bytes (len = the block's encoded length), which never reaches the next slot.
+ *
+ * Spill arena. A block whose decoded bytes do not fit its slot (the reference iterator accepts
+ * offsets that overlap or repeat, so n entries may materialise up to n * 65535 key and value
+ * bytes each), or one longer than TPZ_LDS_BLOCK_BYTES, is decoded into the caller's spill arena
+ * and reported TPZ_BLOCK_OK_SPILLED. Its record starts at r = d_spill_off[i] (128-aligned):
+ *   u32 ends[2*count[i]] at d_spill[r ..]         {kend, vend} pairs, exactly as in the slot
+ *   stream at d_spill[r + tpz_spill_stream(count[i]) ..]: keys, then values from
+ *                                                 tpz_value_start(K), as in the slot
+ * (K and V each fit in 32 bits: at most 65535 entries of at most 65535 bytes.) Records are
+ * placed by an atomic cursor; *d_spill_used = the bytes every spilled block of the call asked
+ * for (the library zeroes it first). A record that does not fit spill_cap leaves the block
+ * TPZ_BLOCK_SPILL_FULL with d_spill_off[i] = its size: decode the batch again with
+ * spill_cap >= *d_spill_used. Batches written by topazdb's BlockBuilder with block_size <= 64 KiB
+ * never spill; d_spill may then be NULL with spill_cap 0. */
 typedef struct {
-  uint8_t* d_data;   /* capacity tpz_data_capacity(src_bytes, n_blocks) bytes        */
-  uint32_t* d_ends;  /* capacity 2 * tpz_entry_capacity(src_bytes, n_blocks) u32      */
-  uint32_t* d_count; /* n_blocks */
-  uint8_t* d_status; /* n_blocks */
-  uint32_t* d_crc;   /* n_blocks */
+  uint8_t* d_data;          /* capacity tpz_data_capacity(src_bytes, n_blocks) bytes        */
+  uint32_t* d_ends;         /* capacity 2 * tpz_entry_capacity(src_bytes, n_blocks) u32      */
+  uint32_t* d_count;        /* n_blocks */
+  uint8_t* d_status;        /* n_blocks */
+  uint32_t* d_crc;          /* n_blocks */
+  uint8_t* d_spill;         /* spill arena (see above), spill_cap bytes; may be NULL if 0   */
+  uint64_t spill_cap;
+  uint64_t* d_spill_off;    /* n_blocks: written for OK_SPILLED and SPILL_FULL blocks only   */
+  uint64_t* d_spill_used;   /* one u64                                                      */
 } tpz_columns;
+
+/* Offset of a spilled record's stream from the record start: its 2*n u32 ends, 128-aligned. */
+static inline uint64_t tpz_spill_stream(uint64_t n) {
+  return (8u * n + 127u) & ~(uint64_t)127u;
+}
+/* Bytes of a spilled record with n entries, K key and V value bytes (128-aligned). */
+static inline uint64_t tpz_spill_record_bytes(uint64_t n, uint64_t k, uint64_t v) {
+  return tpz_spill_stream(n) + ((((k + 15u) & ~(uint64_t)15u) + v + 127u) & ~(uint64_t)127u);
+}
 
 static inline uint64_t tpz_slot_base(uint64_t ext_i, uint64_t i) {
   return ((ext_i + 127u) & ~(uint64_t)127u) + 256u * i;
@@ -136,6 +167,7 @@ uint64_t tpz_layout_value_start(uint64_t key_bytes);
 uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i);
 uint64_t tpz_layout_data_capacity(uint64_t src_bytes, uint64_t n_blocks);
 uint64_t tpz_layout_entry_capacity(uint64_t src_bytes, uint64_t n_blocks);
+uint64_t tpz_layout_spill_stream(uint64_t n);
 
 /* ---- context ------------------------------------------------------------------------------ */
 typedef struct tpz_ctx tpz_ctx;
@@ -161,7 +193,8 @@ tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_column
  * ends reserve the worst case (a pair per 6 input bytes, ~1.33x the input) so that blocks need no
  * prefix pass; this packs the used pairs. d_first = exclusive prefix sums of out->d_count
  * (n_blocks + 1 entries, from the caller's device scan); block i's count[i] {kend, vend} pairs go
- * to d_dense[2*d_first[i] .. 2*d_first[i+1]) (zeros for a block whose status is not OK). */
+ * to d_dense[2*d_first[i] .. 2*d_first[i+1]) (for OK_SPILLED blocks from their spill records;
+ * zeros for a block whose status is neither OK nor OK_SPILLED). */
 tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* cols,
                       const uint64_t* d_first, uint32_t* d_dense, void* stream);
 
@@ -186,16 +219,16 @@ tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
  * Snappy (tag 2) and LZ4 (tag 3) blocks are decompressed on the device into their Uncompress
  * (tag 1) form, so tpz_decode_blocks then verifies and decodes them like any block:
  *   1. tpz_decompressed_sizes: d_size[i] = the length block i has once decompressed and
- *      re-tagged: for tag 2 the snappy preamble's length + 1 (0 if the preamble is invalid, 1
- *      if the length exceeds TPZ_MAX_BLOCK_BYTES - 1); for tag 3 the length LZ4_decompress_safe
- *      decodes + 1 (lz4::block::decompress keeps only the decoded bytes, which may be fewer than
- *      the size prefix; 1 for an Err or a block past the device limits); the block's own
- *      length for any other block.
+ *      re-tagged: for tag 2 the snappy preamble's length + 1 (0 if the preamble is invalid);
+ *      for tag 3 the length LZ4_decompress_safe decodes + 1 (lz4::block::decompress keeps only
+ *      the decoded bytes, which may be fewer than the size prefix; 1 for an Err); the block's
+ *      own length for any other block. No size limit: blocks past the LDS windows are
+ *      decompressed straight from HBM to HBM.
  *   2. the caller forms d_dst_ext = exclusive prefix sums of d_size (n_blocks + 1 entries) and
  *      allocates d_dst (d_dst_ext[n] bytes).
  *   3. tpz_decompress_blocks writes block i's uncompressed form to d_dst[d_dst_ext[i] ..
  *      d_dst_ext[i+1]) (other tags are copied unchanged) and d_status[i] = TPZ_BLOCK_OK,
- *      TPZ_BLOCK_CODEC_ERROR (the codec's Err) or TPZ_BLOCK_TOO_LARGE. A failed block's range
+ *      or TPZ_BLOCK_CODEC_ERROR (the codec's Err). A failed block's range
  *      ends in tag 0, so decoding it reports BAD_TAG; its d_status is the reference's outcome.
  *   4. tpz_decode_blocks over (d_dst, d_dst_ext).
  * LZ4 acceptance is liblz4 1.9.3's LZ4_decompress_safe (the library the reference's lz4 crate
@@ -216,7 +249,8 @@ tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_d
  *     d_block/d_entry = the position, d_valid = is_valid() (iterator.rs:50-52: the current key
  *     is non-empty), d_status = the status of the last block the seek read (non-OK: the
  *     reference's read_block_cached Err, or its panic for MALFORMED; a table with no blocks
- *     gives MALFORMED: block_metas[0] panics).
+ *     gives MALFORMED: block_metas[0] panics; OK_SPILLED blocks are read from their spill
+ *     records and report OK).
  *   tpz_bloom_may_contain: SsTable::may_contain (src/table.rs:114-119) = Bloom::may_contain
  *     (src/bloom.rs:72-84) of xxh3_64(key) for every key; d_filter = Bloom::encode (the bit
  *     array, then k). d_out = 1 (may contain), 0 (absent), 2 (the reference panics: an empty
@@ -231,6 +265,8 @@ typedef struct {
   const uint32_t* d_ends;
   const uint32_t* d_count;
   const uint8_t* d_status;
+  const uint8_t* d_spill;      /* the decode's spill arena and record offsets (OK_SPILLED) */
+  const uint64_t* d_spill_off;
 } tpz_table;
 
 tpz_err tpz_seek_keys(tpz_ctx* ctx, const tpz_table* table, const uint8_t* d_keys,
@@ -273,7 +309,8 @@ uint32_t tpz_host_crc32(const uint8_t* h_buf, uint64_t len);
 /* ---- errors ------------------------------------------------------------------------------ */
 /* Writes the reference's error text for a block outcome into buf (NUL-terminated):
  * "data is empty", "invaild data", "checksum: expected E, actual A" (decimal, as Rust's {}),
- * "unsupported codec", "malformed block", "overlapping entries", "block too large", "" for OK.
+ * "unsupported codec", "malformed block", "spill arena too small", "decompression failed",
+ * "" for OK and OK_SPILLED.
  * Returns the text length. */
 int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actual, char* buf,
                            size_t cap);

@@ -139,8 +139,6 @@ static int codec_step(const uint8_t* b, size_t len, uint8_t** buf, const uint8_t
     if (tpzo_lz4_prefixed_size(b, len - 1, &size) != 0) return TPZO_CODEC;
     const int64_t r = tpzo_lz4_decompress_safe(b + 4, (int64_t)len - 5, NULL, size);
     if (r < 0) return TPZO_CODEC;
-    /* the device's limits (TPZ_MAX_BLOCK_BYTES; a 64 KiB staging window less 32 bytes) */
-    if (r + 1 > 94192 || len - 1 > 65504) return TPZO_TOO_LARGE;
     *buf = (uint8_t*)malloc((size_t)r + 1);
     tpzo_lz4_decompress_safe(b + 4, (int64_t)len - 5, *buf, size);
     (*buf)[r] = 1;
@@ -151,11 +149,9 @@ static int codec_step(const uint8_t* b, size_t len, uint8_t** buf, const uint8_t
   if (len == 0 || b[len - 1] != 2) return 0;
   uint64_t want = 0;
   if (tpzo_snappy_uncompressed_len(b, len - 1, &want) != 0) return TPZO_CODEC;
-  /* the device's limits (TPZ_MAX_BLOCK_BYTES; a 64 KiB staging window less 32 bytes of slack) */
-  if (want + 1 > 94192 || len - 1 > 65504) return TPZO_TOO_LARGE;
   *buf = (uint8_t*)malloc(want + 1);
   uint64_t got = 0;
-  if (tpzo_snappy_decompress(b, len - 1, *buf, want, &got) != 0) return TPZO_CODEC;
+  if (!*buf || tpzo_snappy_decompress(b, len - 1, *buf, want, &got) != 0) return TPZO_CODEC;
   (*buf)[got] = 1;
   *out = *buf;
   *out_len = got + 1;
@@ -202,10 +198,9 @@ static int entry_at(const blockview* v, uint32_t i, const uint8_t** k, uint32_t*
   return 1;
 }
 
-/* Decode a block and validate every entry the way an iteration over all indices would.
- * Sets TPZO_MALFORMED on any panicking entry, TPZO_OVERLAP when the decoded bytes cannot fit
- * the device slot contract (include/tpz_gpu.h: 6*n <= len and value_start(K) + V <= len + 2,
- * K/V = key/value bytes, value_start = K rounded up to 16). */
+/* Decode a block and validate every entry the way an iteration over all indices would
+ * (iterator.rs:63-83 reads entry i at offsets[i] with no ordering or disjointness check: entries
+ * may overlap or repeat). Sets TPZO_MALFORMED on any panicking entry. */
 static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt, uint64_t* vt) {
   block_decode(b, len, v);
   *kt = *vt = 0;
@@ -217,7 +212,6 @@ static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt,
     *kt += kl;
     *vt += vl;
   }
-  if (6ull * v->n > len || ((*kt + 15) & ~15ull) + *vt > len + 2) v->status = TPZO_OVERLAP;
 }
 
 void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
@@ -231,7 +225,7 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
     size_t blen;
     if (codec_step(src + ext[i], ext[i + 1] - ext[i], &buf, &blk, &blen) == 0) {
       block_full(blk, blen, &v, &kt, &vt);
-      if (v.status == TPZO_OK || v.status == TPZO_OVERLAP) { ne += v.n; kb += kt; vb += vt; }
+      if (v.status == TPZO_OK) { ne += v.n; kb += kt; vb += vt; }
     }
     free(buf);
   }
@@ -262,7 +256,7 @@ int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
     crc_actual[i] = v.crc_actual;
     crc_expected[i] = v.crc_expected;
     count[i] = 0;
-    if (v.status != TPZO_OK && v.status != TPZO_OVERLAP) { free(buf); continue; }
+    if (v.status != TPZO_OK) { free(buf); continue; }
     count[i] = v.n;
     for (uint32_t j = 0; j < v.n; j++, e++) {
       const uint8_t *k, *val;

@@ -30,8 +30,8 @@ enum {
   TPZO_UNSUPPORTED = 3, /* no longer produced: lz4 (tag 3) is decoded (tpz_lz4.c) */
   TPZO_CHECKSUM = 4,    /* Err("checksum: ...")      src/checksum.rs:12-21       */
   TPZO_MALFORMED = 5,   /* the reference panics      src/block.rs:49-59, iterator.rs:74-82 */
-  TPZO_OVERLAP = 6,     /* decodes in the reference; exceeds the device's per-block slot */
-  TPZO_TOO_LARGE = 7,   /* a snappy/lz4 block past the device limits (94192 B out, 64 KiB - 31 in) */
+  /* 6 (OK_SPILLED) and 7 (SPILL_FULL) are device-side placements of an Ok block (the spill
+   * arena of include/tpz_gpu.h); the reference, and so this oracle, reports them TPZO_OK. */
   TPZO_CODEC = 8        /* the codec returns Err: snap's decompress_vec (compress.rs:104-107),
                            lz4::block::decompress (compress.rs:108-111)                     */
 };
@@ -49,7 +49,7 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
 /* Block::decode (src/block.rs:46-65, snappy blocks decompressed first as compress.rs:104-107)
  * + BlockIterator::seek_to for every index (src/block/iterator.rs:63-83) over blocks
  * [ext[i], ext[i+1]). Dense outputs in block order:
- * entries are emitted for TPZO_OK and TPZO_OVERLAP blocks. crc_actual is the CRC the reference
+ * entries are emitted for TPZO_OK blocks. crc_actual is the CRC the reference
  * computes over the payload (0 when it never gets that far). Returns 0. */
 int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint8_t* status, uint32_t* crc_actual, uint32_t* crc_expected,

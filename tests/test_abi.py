@@ -63,9 +63,17 @@ def test_slots_never_overlap():
     assert _lib.entry_base(int(ext[-1]), n) <= _lib.entry_capacity(int(ext[-1]), n)
 
 
+def test_spill_layout_helpers():
+    """include/tpz_gpu.h's spill record layout: 2n u32 ends, then the stream 128-aligned."""
+    L = _lib.lib()
+    for n in [0, 1, 15, 16, 17, 255, 65535]:
+        assert L.tpz_layout_spill_stream(n) == _lib.spill_stream(n) == (8 * n + 127) // 128 * 128
+
+
 def test_error_strings_match_reference():
     """src/checksum.rs:17-20, src/block/compress.rs:97,102."""
     assert _lib.format_block_error(_lib.BLOCK_OK) == ""
+    assert _lib.format_block_error(_lib.BLOCK_OK_SPILLED) == ""   # Ok(Block), in the spill arena
     assert _lib.format_block_error(_lib.BLOCK_EMPTY) == "data is empty"
     assert _lib.format_block_error(_lib.BLOCK_BAD_TAG) == "invaild data"
     assert (_lib.format_block_error(_lib.BLOCK_CHECKSUM_MISMATCH, 123, 4294967295)
@@ -187,7 +195,7 @@ def test_unaligned_src_is_rejected():
     an unaligned pointer is TPZ_ERR_INVALID_ARG before any device work (no GPU needed)."""
     L = _lib.lib()
     b = _lib.Batch(0x1001, 0x2000, 1, 10)
-    c = _lib.Columns(0x3000, 0x4000, 0x5000, 0x6000, 0x7000)
+    c = _lib.Columns(0x3000, 0x4000, 0x5000, 0x6000, 0x7000, None, 0, 0x9000, 0xA000)
     assert L.tpz_decode_blocks(C.c_void_p(0x10), C.byref(b), C.byref(c), None) == \
         _lib.ERR_INVALID_ARG
     assert L.tpz_decompressed_sizes(C.c_void_p(0x10), C.byref(b), C.c_void_p(0x8000), None) == \

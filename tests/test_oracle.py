@@ -183,10 +183,10 @@ def test_edge_blocks():
     d = O.decode_batch(src, np.array(exp["ext"], np.uint64))
     for b, eb in enumerate(exp["blocks"]):
         assert d.status[b] == eb["status"], eb["name"]
-        if eb["status"] in (O.CHECKSUM, O.OK, O.OVERLAP):
+        if eb["status"] in (O.CHECKSUM, O.OK):
             assert d.crc_actual[b] == eb["crc_actual"], eb["name"]
             assert d.crc_expected[b] == eb["crc_expected"], eb["name"]
-        if eb["status"] in (O.OK, O.OVERLAP):
+        if eb["status"] == O.OK:
             check_ents(eb["entries"], d.entries(b))
 
 

@@ -8,5 +8,5 @@ Layout:
   topazdb_amd/table.py         FileObject / SsTable / Block / iterators over the device path
 """
 from ._lib import (BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_CODEC_ERROR,  # noqa
-                   BLOCK_EMPTY, BLOCK_MALFORMED, BLOCK_OK, BLOCK_OVERLAP, BLOCK_TOO_LARGE,
+                   BLOCK_EMPTY, BLOCK_MALFORMED, BLOCK_OK, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL,
                    BLOCK_UNSUPPORTED_CODEC, Context, TpzError, format_block_error)

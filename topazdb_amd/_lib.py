@@ -19,8 +19,8 @@ HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
- BLOCK_MALFORMED, BLOCK_OVERLAP, BLOCK_TOO_LARGE, BLOCK_CODEC_ERROR) = range(9)
-MAX_BLOCK_BYTES = 94192
+ BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR) = range(9)
+LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks take the spill path
 
 
 class TpzError(RuntimeError):
@@ -34,16 +34,20 @@ class Batch(C.Structure):
 
 class Columns(C.Structure):
     _fields_ = [("d_data", C.c_void_p), ("d_ends", C.c_void_p), ("d_count", C.c_void_p),
-                ("d_status", C.c_void_p), ("d_crc", C.c_void_p)]
+                ("d_status", C.c_void_p), ("d_crc", C.c_void_p), ("d_spill", C.c_void_p),
+                ("spill_cap", C.c_uint64), ("d_spill_off", C.c_void_p),
+                ("d_spill_used", C.c_void_p)]
 
-COLUMN_FIELDS = ("data", "ends", "count", "status", "crc")
+COLUMN_FIELDS = ("data", "ends", "count", "status", "crc", "spill", "spill_cap", "spill_off",
+                 "spill_used")
 
 
 class Table(C.Structure):
     """tpz_table: block first keys + the columns tpz_decode_blocks wrote for the table."""
     _fields_ = [("d_first_keys", C.c_void_p), ("d_first_pos", C.c_void_p), ("d_ext", C.c_void_p),
                 ("n_blocks", C.c_uint32), ("d_data", C.c_void_p), ("d_ends", C.c_void_p),
-                ("d_count", C.c_void_p), ("d_status", C.c_void_p)]
+                ("d_count", C.c_void_p), ("d_status", C.c_void_p), ("d_spill", C.c_void_p),
+                ("d_spill_off", C.c_void_p)]
 
 
 _lib = None
@@ -99,6 +103,8 @@ def lib() -> C.CDLL:
         L.tpz_pack_ends.restype = C.c_int
         L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
         L.tpz_host_xxh3_64.restype = C.c_uint64
+        L.tpz_layout_spill_stream.argtypes = [C.c_uint64]
+        L.tpz_layout_spill_stream.restype = C.c_uint64
         for f in ("slot_base", "entry_base", "data_capacity", "entry_capacity"):
             fn = getattr(L, "tpz_layout_" + f)
             fn.argtypes = [C.c_uint64, C.c_uint64]
@@ -131,6 +137,16 @@ def value_start(key_bytes):
 
 def entry_base(ext_i, i):
     return 16 * (ext_i // 96 + i)
+
+
+def spill_stream(n):
+    """tpz_spill_stream: a spill record's stream starts after its 2n u32 ends, 128-aligned."""
+    return (8 * n + 127) & ~127
+
+
+def block_decoded(status) -> bool:
+    """Ok(Block) in the reference: TPZ_BLOCK_OK, or OK_SPILLED (decoded into the spill arena)."""
+    return status == BLOCK_OK or status == BLOCK_OK_SPILLED
 
 
 def data_capacity(src_bytes: int, n_blocks: int) -> int:

@@ -48,22 +48,50 @@ class DeviceBatch:
 
 
 class SlottedColumns:
-    """Device output buffers in the slotted layout of include/tpz_gpu.h (tpz_columns)."""
+    """Device output buffers in the slotted layout of include/tpz_gpu.h (tpz_columns), plus the
+    spill arena for blocks whose decoded entries do not fit their slot (TPZ_BLOCK_OK_SPILLED)."""
 
-    def __init__(self, n_blocks: int, src_bytes: int, device: int = 0):
+    def __init__(self, n_blocks: int, src_bytes: int, device: int = 0, spill_cap: int = 0):
         dev = _dev(device)
         cap = _lib.data_capacity(src_bytes, n_blocks)
         ecap = _lib.entry_capacity(src_bytes, n_blocks)
         nb = max(n_blocks, 1)
+        self.device = device
         self.data = torch.empty(cap, dtype=torch.uint8, device=dev)   # keys | gap | values
         self.ends = torch.empty(2 * ecap, dtype=torch.int32, device=dev)  # {kend, vend} pairs
         self.count = torch.empty(nb, dtype=torch.int32, device=dev)
         self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
         self.crc = torch.empty(nb, dtype=torch.int32, device=dev)
+        self.spill_off = torch.empty(nb, dtype=torch.int64, device=dev)
+        self.spill_used = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.set_spill_cap(spill_cap)
         self.n_blocks = n_blocks
+        self._decoded = None   # (ctx, batch, stream) of the last decode_batch into these columns
+
+    def set_spill_cap(self, spill_cap: int) -> None:
+        self.spill_cap = int(spill_cap)
+        self.spill = (torch.empty(self.spill_cap, dtype=torch.uint8, device=_dev(self.device))
+                      if self.spill_cap else None)
 
     def ptrs(self) -> dict:
-        return {k: getattr(self, k).data_ptr() for k in _lib.COLUMN_FIELDS}
+        p = {k: getattr(self, k).data_ptr() for k in ("data", "ends", "count", "status", "crc",
+                                                     "spill_off", "spill_used")}
+        p["spill"] = self.spill.data_ptr() if self.spill is not None else None
+        p["spill_cap"] = self.spill_cap
+        return p
+
+    def complete(self) -> "SlottedColumns":
+        """Waits for the decode; if its spill arena was too small (TPZ_BLOCK_SPILL_FULL blocks),
+        grows the arena to what the spilled blocks asked for and decodes the batch again."""
+        torch.cuda.synchronize(_dev(self.device))
+        if self._decoded is not None:
+            used = int(self.spill_used.cpu()[0])
+            if used > self.spill_cap:
+                ctx, batch, stream = self._decoded
+                self.set_spill_cap(used)
+                decode_batch(ctx, batch, self, stream)
+                torch.cuda.synchronize(_dev(self.device))
+        return self
 
     def meta_host(self):
         nb = self.n_blocks
@@ -71,36 +99,76 @@ class SlottedColumns:
                 self.count[:nb].cpu().numpy().view(np.uint32))
 
     def dense(self, ext_host: np.ndarray) -> "DenseDecode":
-        """Gather every OK block's entries into dense arrays (block order)."""
+        """Gather every decoded block's entries into dense arrays (block order); statuses are
+        the reference's (OK_SPILLED reads as OK; raw_status keeps the device's)."""
+        self.complete()
         status, crc, count = self.meta_host()
         nb = self.n_blocks
         ext = np.asarray(ext_host[:nb], np.int64)
         bid = np.arange(nb, dtype=np.int64)
-        n_ok = np.where(status == BLOCK_OK, count, 0).astype(np.int64)
+        spilled = status == _lib.BLOCK_OK_SPILLED
+        okm = (status == BLOCK_OK) | spilled
+        n_ok = np.where(okm, count, 0).astype(np.int64)
         ebase = np.zeros(nb + 1, np.int64)
         np.cumsum(n_ok, out=ebase[1:])
         total = int(ebase[-1])
         eblk = np.repeat(bid, n_ok)
         j = np.arange(total, dtype=np.int64) - ebase[eblk]
-        sb = _lib.entry_base(ext, bid)
-        base = _lib.slot_base(ext, bid)
-        slot = sb[eblk] + j
+        data = self.data.cpu().numpy()
         ends = self.ends.cpu().numpy().view(np.uint32)
         kend_d, vend_d = ends[0::2], ends[1::2]
-        # the block's key bytes = kend of its last entry; its values start 16-aligned after them
-        ktot = np.where(n_ok > 0, kend_d[sb + np.maximum(n_ok - 1, 0)].astype(np.int64), 0)
-        vbase = base + _lib.value_start(ktot)
-        ke = kend_d[slot].astype(np.int64)
-        ve = vend_d[slot].astype(np.int64)
-        first = j == 0
-        ks = np.where(first, 0, kend_d[np.maximum(slot - 1, 0)].astype(np.int64))
-        vs = np.where(first, 0, vend_d[np.maximum(slot - 1, 0)].astype(np.int64))
+        # every entry's key/value end, previous end and stream base in one virtual buffer:
+        # [slotted data | spill arena]
+        sb = _lib.entry_base(ext, bid)
+        slot = sb[eblk] + j
+        nbad = np.zeros(total, bool)
+        ke = np.zeros(total, np.int64)
+        ve = np.zeros(total, np.int64)
+        ks = np.zeros(total, np.int64)
+        vs = np.zeros(total, np.int64)
+        base = np.zeros(total, np.int64)
+        vbase = np.zeros(total, np.int64)
+        slotm = ~spilled[eblk]
+        if slotm.any():
+            s_slot = slot[slotm]
+            first = j[slotm] == 0
+            ke[slotm] = kend_d[s_slot]
+            ve[slotm] = vend_d[s_slot]
+            ks[slotm] = np.where(first, 0, kend_d[np.maximum(s_slot - 1, 0)])
+            vs[slotm] = np.where(first, 0, vend_d[np.maximum(s_slot - 1, 0)])
+            # the block's key bytes = kend of its last entry; its values start 16-aligned after
+            b_ok = okm & ~spilled
+            ktot = np.where(b_ok & (n_ok > 0), kend_d[sb + np.maximum(n_ok - 1, 0)].astype(np.int64), 0)
+            sbase = _lib.slot_base(ext, bid)
+            base[slotm] = sbase[eblk[slotm]]
+            vbase[slotm] = (sbase + _lib.value_start(ktot))[eblk[slotm]]
+        buf = data
+        if spilled.any():
+            sp = self.spill.cpu().numpy()
+            offs = self.spill_off[:nb].cpu().numpy()
+            buf = np.concatenate([data, sp])
+            for b in np.nonzero(spilled)[0]:
+                n = int(count[b])
+                if n == 0:
+                    continue
+                r = int(offs[b])
+                e2 = sp[r:r + 8 * n].view(np.uint32).astype(np.int64)
+                kk, vv = e2[0::2], e2[1::2]
+                sl = slice(int(ebase[b]), int(ebase[b + 1]))
+                ke[sl], ve[sl] = kk, vv
+                ks[sl] = np.concatenate([[0], kk[:-1]])
+                vs[sl] = np.concatenate([[0], vv[:-1]])
+                st0 = len(data) + r + _lib.spill_stream(n)
+                base[sl] = st0
+                vbase[sl] = st0 + _lib.value_start(int(kk[-1]))
         klen, vlen = ke - ks, ve - vs
-        data = self.data.cpu().numpy()
-        keys = _gather(data, base[eblk] + ks, klen)
-        vals = _gather(data, vbase[eblk] + vs, vlen)
-        return DenseDecode(status, crc, np.where(status == BLOCK_OK, count, 0).astype(np.uint32),
-                           count, klen.astype(np.uint32), vlen.astype(np.uint32), keys, vals)
+        keys = _gather(buf, base + ks, klen)
+        vals = _gather(buf, vbase + vs, vlen)
+        ref_status = np.where(spilled, BLOCK_OK, status).astype(np.uint8)
+        d = DenseDecode(ref_status, crc, np.where(okm, count, 0).astype(np.uint32),
+                        count, klen.astype(np.uint32), vlen.astype(np.uint32), keys, vals)
+        d.raw_status = status
+        return d
 
 
 def _gather(buf: np.ndarray, starts: np.ndarray, lens: np.ndarray) -> np.ndarray:
@@ -135,12 +203,15 @@ class DenseDecode:
 
 
 def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None = None,
-                 stream: torch.cuda.Stream | None = None) -> SlottedColumns:
+                 stream: torch.cuda.Stream | None = None, spill_cap: int = 0) -> SlottedColumns:
+    """tpz_decode_blocks (asynchronous). Blocks that spill into a too-small arena are finished by
+    cols.complete() (dense() calls it): it grows the arena and decodes again."""
     if cols is None:
-        cols = SlottedColumns(batch.n_blocks, batch.src_bytes, ctx.device)
+        cols = SlottedColumns(batch.n_blocks, batch.src_bytes, ctx.device, spill_cap)
     s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
     ctx.decode_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes,
                     cols.ptrs(), s.cuda_stream)
+    cols._decoded = (ctx, batch, stream)
     return cols
 
 

@@ -113,11 +113,12 @@ std::vector<uint32_t> build_rep_tables(const std::vector<uint32_t>& range) {
 
 }  // namespace
 
-// Device workspace of one stream: the big-path worklist (counter + list), the big path's
+// Device workspace of one stream: the big-path and spill-path worklists, the big path's
 // per-workgroup entry tables and the range-CRC accumulators. Decodes on different streams run
 // concurrently, so each stream has its own; calls on one stream are ordered by the stream.
 struct tpz_workspace {
-  uint32_t* d_defer = nullptr;  // [0] = counter, [1..] = list
+  uint32_t* d_defer = nullptr;  // [0] big/codec counter, [1] spill counter, [2, 2 + cap) big or
+                                // codec list, [2 + cap, 2 + 2 cap) spill list
   uint32_t defer_cap = 0;
   uint64_t* d_big_scratch = nullptr;
   uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
@@ -167,7 +168,7 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
     TPZ_HIP(hipMalloc(&w.d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t)));
   if (!w.d_defer || w.defer_cap < max_blocks) {
     uint32_t* d = nullptr;
-    TPZ_HIP(hipMalloc(&d, ((size_t)max_blocks + 1) * 4));
+    TPZ_HIP(hipMalloc(&d, (2 * (size_t)max_blocks + 2) * 4));
     if (w.d_defer) {
       // an earlier decode on this stream may still be reading the old list
       (void)hipStreamSynchronize((hipStream_t)stream);
@@ -189,6 +190,7 @@ uint64_t tpz_layout_value_start(uint64_t key_bytes) { return tpz_value_start(key
 uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i) { return tpz_entry_base(ext_i, i); }
 uint64_t tpz_layout_data_capacity(uint64_t s, uint64_t n) { return tpz_data_capacity(s, n); }
 uint64_t tpz_layout_entry_capacity(uint64_t s, uint64_t n) { return tpz_entry_capacity(s, n); }
+uint64_t tpz_layout_spill_stream(uint64_t n) { return tpz_spill_stream(n); }
 
 const char* tpz_last_error(void) { return g_last_error.c_str(); }
 
@@ -248,9 +250,16 @@ tpz_err tpz_ctx_reserve(tpz_ctx* c, uint32_t max_blocks, void* stream) {
 
 tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, void* stream) {
   if (!c || !b || !o) return TPZ_ERR_INVALID_ARG;
-  if (b->n_blocks == 0) return TPZ_SUCCESS;
+  if (b->n_blocks == 0) {
+    if (o->d_spill_used) {
+      TPZ_HIP(hipSetDevice(c->device));
+      TPZ_HIP(hipMemsetAsync(o->d_spill_used, 0, 8, (hipStream_t)stream));
+    }
+    return TPZ_SUCCESS;
+  }
   if (!b->d_src || !b->d_ext || !o->d_data || !o->d_ends || !o->d_count || !o->d_status ||
-      !o->d_crc || (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
+      !o->d_crc || !o->d_spill_off || !o->d_spill_used || (o->spill_cap && !o->d_spill) ||
+      (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
     return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz_workspace* w = nullptr;
@@ -260,7 +269,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
     if (r != TPZ_SUCCESS) return r;
   }
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 4, s));
+  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 8, s));   // both worklist counters
   tpz::LaunchArgs a{};
   a.src = b->d_src;
   a.ext = b->d_ext;
@@ -273,7 +282,13 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.status = o->d_status;
   a.crc = o->d_crc;
   a.defer_count = w->d_defer;
-  a.defer_list = w->d_defer + 1;
+  a.defer_list = w->d_defer + 2;
+  a.spill_count = w->d_defer + 1;
+  a.spill_list = w->d_defer + 2 + w->defer_cap;
+  a.spill = o->d_spill;
+  a.spill_cap = o->d_spill ? o->spill_cap : 0;
+  a.spill_off = o->d_spill_off;
+  a.spill_used = o->d_spill_used;   // zeroed by the first kernel
   a.num_cus = c->num_cus;
   a.big_scratch = w->d_big_scratch;
   a.big_grid = c->num_cus;
@@ -354,7 +369,7 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
   a.dst_ext = d_dst_ext;
   a.status = d_status;
   a.defer_count = w->d_defer;
-  a.defer_list = w->d_defer + 1;
+  a.defer_list = w->d_defer + 2;
   a.num_cus = c->num_cus;
   tpz::launch_decompress(a, s);
   TPZ_HIP(hipGetLastError());
@@ -382,8 +397,8 @@ tpz_err tpz_seek_keys(tpz_ctx* c, const tpz_table* t, const uint8_t* d_keys,
     return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz::SeekLaunch a{t->d_first_keys, t->d_first_pos, t->n_blocks, t->d_ext, t->d_data,
-                    t->d_ends, t->d_count, t->d_status, d_keys, d_key_pos, n_keys,
-                    d_block, d_entry, d_status, d_valid};
+                    t->d_ends, t->d_count, t->d_status, t->d_spill, t->d_spill_off, d_keys,
+                    d_key_pos, n_keys, d_block, d_entry, d_status, d_valid};
   tpz::launch_seek(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
@@ -407,8 +422,8 @@ tpz_err tpz_pack_ends(tpz_ctx* c, const tpz_batch* b, const tpz_columns* cols,
   if (b->n_blocks == 0) return TPZ_SUCCESS;
   if (!b->d_ext || !cols->d_ends || !cols->d_count || !cols->d_status) return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
-  tpz::PackLaunch a{b->d_ext, b->n_blocks, cols->d_ends, cols->d_count, cols->d_status, d_first,
-                    d_dense};
+  tpz::PackLaunch a{b->d_ext, b->n_blocks, cols->d_ends, cols->d_count, cols->d_status,
+                    cols->d_spill, cols->d_spill_off, d_first, d_dense};
   tpz::launch_pack_ends(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
@@ -430,8 +445,8 @@ int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actua
       std::snprintf(tmp, sizeof tmp, "checksum: expected %u, actual %u", crc_expected, crc_actual);
       break;
     case TPZ_BLOCK_MALFORMED: std::snprintf(tmp, sizeof tmp, "malformed block"); break;
-    case TPZ_BLOCK_OVERLAP: std::snprintf(tmp, sizeof tmp, "overlapping entries"); break;
-    case TPZ_BLOCK_TOO_LARGE: std::snprintf(tmp, sizeof tmp, "block too large"); break;
+    case TPZ_BLOCK_OK_SPILLED: tmp[0] = 0; break;   // Ok(Block), decoded into the spill arena
+    case TPZ_BLOCK_SPILL_FULL: std::snprintf(tmp, sizeof tmp, "spill arena too small"); break;
     case TPZ_BLOCK_CODEC_ERROR: std::snprintf(tmp, sizeof tmp, "decompression failed"); break;
     default: std::snprintf(tmp, sizeof tmp, "unknown status %d", status); break;
   }

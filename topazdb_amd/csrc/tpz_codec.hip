@@ -16,7 +16,8 @@
 // d - offset + k mod offset, which precedes the copy). The output is assembled in LDS and stored
 // with 16-byte stores (byte stores at the two edge pieces, which neighbouring blocks share).
 // Blocks larger than a 16-wave workgroup's slots go to a one-wave-per-workgroup kernel with
-// 64 KiB input / 94 KiB output windows.
+// 64 KiB input / 94 KiB output windows; blocks past those windows (no size limit: snap and lz4
+// decode any length) are decompressed by that wave straight from HBM to HBM.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,7 +40,7 @@ constexpr u32 kSmallIn = 4608, kSmallOut = 5120;     // per-wave windows of the 
 constexpr u32 kBigIn = 65536, kBigOut = 94208;       // the one-wave kernel
 constexpr u32 kGuard = 16;                           // readable bytes before each input window
 constexpr u32 kInSlack = 16 + 16;                    // staging offset (< 16) + header overread
-constexpr u64 kLz4MaxIn = kBigIn - kInSlack;         // 65504: compressed bytes a window takes
+constexpr u64 kMaxInWindow = kBigIn - kInSlack;      // 65504: compressed bytes a window takes
 constexpr uint8_t kLeftForWaveKernel = 0xFF;         // status the group pass leaves behind
 static_assert(kSmallWaves * (kGuard + kSmallIn + kSmallOut) <= 163840, "small LDS");
 static_assert(kGuard + kBigIn + kBigOut <= 163840, "big LDS");
@@ -425,6 +426,91 @@ __device__ __forceinline__ int64_t lz4_prefix(const uint8_t* s, u64 n) {
   return (v < 0 || v > 0x7E000000) ? -1 : (int64_t)v;
 }
 
+// ------------------------------------------------------------------ HBM-to-HBM path
+// Blocks past the LDS windows: the wave reads the compressed bytes and writes the output in
+// global memory. A back-reference (a snappy copy, an LZ4 match) reads output bytes this wave
+// stored earlier: their stores are drained first (s_waitcnt vmcnt(0)) and the reads are volatile
+// (L2-served), so no stale L1 line can be returned.
+__device__ __forceinline__ u32 out_byte(const uint8_t* p) {
+  return *reinterpret_cast<const volatile uint8_t*>(p);
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// out[0 .. n) = in[0 .. n) by the wave (four bytes in flight per lane).
+__device__ __forceinline__ void wave_copy_g(uint8_t* out, const uint8_t* in, u64 n) {
+  u64 k = lane_id();
+  for (; k + 192 < n; k += 256) {
+    const uint8_t a = in[k], b = in[k + 64], c = in[k + 128], d = in[k + 192];
+    out[k] = a;
+    out[k + 64] = b;
+    out[k + 128] = c;
+    out[k + 192] = d;
+  }
+  for (; k < n; k += kWave) out[k] = in[k];
+}
+
+// out[d .. d + len) repeats the bytes `off` back (off <= d; 0 = zeros, the LZ4 offset-0 case):
+// byte d + k is byte d - off + (k mod off).
+__device__ __forceinline__ void match_copy_g(uint8_t* out, u64 d, u64 off, u64 len) {
+  const u32 lane = lane_id();
+  drain_stores();
+  if (off == 0) {
+    for (u64 k = lane; k < len; k += kWave) out[d + k] = 0;
+    return;
+  }
+  for (u64 k0 = 0; k0 < len; k0 += kWave) {
+    const u64 k = k0 + lane;
+    u32 v = 0;
+    if (k < len) v = out_byte(out + d - off + (k < off ? k : k % off));
+    if (k < len) out[d + k] = (uint8_t)v;
+  }
+}
+
+// snap's decompress_vec over global memory (the LDS path's checks, 64-bit lengths).
+__device__ bool snappy_decode_global(const uint8_t* in, u64 n, u64 ip, uint8_t* out, u64 want) {
+  u64 d = 0;
+  while (ip < n) {
+    u32 h[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) h[q] = ip + q < n ? uni(in[ip + q]) : 0u;
+    const u32 tag = h[0], kind = tag & 3, t6 = tag >> 2;
+    const u32 x = h[1] | h[2] << 8 | h[3] << 16 | h[4] << 24;
+    u64 len, off = 0, hl;
+    if (kind == 0) {
+      const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
+      const u64 lx = nb == 0 ? t6 : (nb == 4 ? (u64)x : (u64)(x & ((1u << (8 * nb)) - 1)));
+      len = lx + 1;
+      hl = 1 + nb;
+    } else {
+      len = kind == 1 ? 4 + (t6 & 7) : t6 + 1;
+      hl = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+      off = kind == 1 ? (((tag >> 5) << 8) | (x & 0xFF)) : (kind == 2 ? (x & 0xFFFF) : x);
+    }
+    const u64 next = ip + hl + (kind == 0 ? len : 0);
+    if (d + len > want || next > n || (kind != 0 && (off == 0 || off > d))) return false;
+    if (kind == 0) wave_copy_g(out + d, in + ip + hl, len);
+    else match_copy_g(out, d, off, len);
+    ip = next;
+    d += len;
+  }
+  return d == want;
+}
+
+struct Lz4GlobalUniSrc {         // wave-uniform, from global memory
+  const uint8_t* p;
+  __device__ u32 byte(int64_t i) const { return uni(p[i]); }
+};
+struct Lz4GlobalOut {            // wave-wide copies into global memory
+  const uint8_t* in;
+  uint8_t* out;
+  __device__ void lit(int64_t op, int64_t ip, int64_t len) const {
+    wave_copy_g(out + op, in + ip, (u64)len);
+  }
+  __device__ void match(int64_t op, int64_t off, int64_t len) const {
+    match_copy_g(out, (u64)op, (u64)off, (u64)len);
+  }
+};
+
 // The whole decode decision of a tag-3 block from global memory (per thread): its decoded
 // length, or -1 (the codec's Err).
 __device__ __forceinline__ int64_t lz4_block_length(const uint8_t* blk, u64 len) {
@@ -440,10 +526,10 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
   const u64 s = p.ext[i], e = p.ext[i + 1], len = e - s;
   const u32 tag = len ? p.src[e - 1] : 0u;
   if (tag == 3) {
-    // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err, or a
-    // block past the device limits, leaves a lone tag byte
+    // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err
+    // leaves a lone tag byte
     const int64_t r = lz4_block_length(p.src + s, len);
-    p.size[i] = (r < 0 || (u64)r + 1 > TPZ_MAX_BLOCK_BYTES || len - 1 > kLz4MaxIn) ? 1 : r + 1;
+    p.size[i] = r < 0 ? 1 : (u64)r + 1;
     return;
   }
   if (tag != 2) {                         // not compressed: copied unchanged
@@ -452,9 +538,8 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
   }
   u64 want = 0;
   const u32 h = snappy_header(p.src + s, len - 1, want);
-  // an invalid preamble leaves an empty range; a declared length no device decode could take
-  // leaves a lone tag byte (the decode reports it; the codec status says why)
-  p.size[i] = h == 0 ? 0 : (want + 1 <= TPZ_MAX_BLOCK_BYTES ? want + 1 : 1);
+  // an invalid preamble leaves an empty range (the decode reports it; the codec status says why)
+  p.size[i] = h == 0 ? 0 : want + 1;
 }
 
 struct BlockMeta {
@@ -462,7 +547,8 @@ struct BlockMeta {
   u32 tag;
 };
 
-// One LZ4 block (tag 3). Returns false when it does not fit the windows (the caller defers it).
+// One LZ4 block (tag 3). Returns false when it does not fit the windows and this is not the
+// last resort (the caller defers it); the last resort decodes past the windows from HBM.
 template <u32 kIn, u32 kOut>
 __device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const BlockMeta& m,
                                           uint8_t* in_win, uint8_t* out_win, bool last_resort) {
@@ -476,14 +562,18 @@ __device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const Blo
   bool ok = false;
   const u32 a_out = (u32)(reinterpret_cast<uintptr_t>(dst) & 15);
   uint8_t* out = out_win + a_out;
-  if (!fits || dn < 2) {
-    // an Err, a block past the limits (the sizes pass gave it 1 byte) or an empty output: the
-    // decision again, from global memory
+  bool direct = false;          // the output went straight to dst
+  if (dn < 2) {
+    // an Err (the sizes pass gave it 1 byte) or an empty output: the decision again, from
+    // global memory
     const int64_t r = lz4_block_length(p.src + s, len);
-    if (r >= 0) {
-      if (r == 0 && dn == 1 && len - 1 <= kLz4MaxIn) ok = true;
-      else st = TPZ_BLOCK_TOO_LARGE;
-    }
+    ok = r == 0 && dn == 1;
+  } else if (!fits) {
+    const int64_t size = lz4_prefix(p.src + s, len - 1);     // valid: dn >= 2
+    const int64_t r = lz4_walk(Lz4GlobalUniSrc{p.src + s + 4}, (int64_t)len - 5,
+                               Lz4GlobalOut{p.src + s + 4, dst}, size);
+    ok = r >= 0 && (u64)r + 1 == dn;
+    direct = true;
   } else {
     stage_aligned(p.src, p.src_bytes, s, (u32)(len - 1), in_win);
     __builtin_amdgcn_wave_barrier();
@@ -493,7 +583,12 @@ __device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const Blo
     __builtin_amdgcn_wave_barrier();
     ok = r >= 0 && (u64)r + 1 == dn;
   }
-  if (ok) {
+  if (ok && direct) {
+    if (lane == 0) {
+      dst[dn - 1] = 1;                                         // re-tagged Uncompress
+      p.status[b] = TPZ_BLOCK_OK;
+    }
+  } else if (ok) {
     if (lane == 0) out[dn - 1] = 1;                            // re-tagged Uncompress
     __builtin_amdgcn_wave_barrier();
     store_aligned(out_win, dst, (u32)dn);
@@ -550,10 +645,17 @@ __device__ __forceinline__ bool codec_block(const CodecParams& p, u32 b, const B
     }
   } else {
     if (!last_resort) return false;
+    // past the LDS windows: straight from HBM to HBM
     h = snappy_header(p.src + s, len - 1, want);
-    if (h != 0) st = TPZ_BLOCK_TOO_LARGE;
+    const bool ok2 = h != 0 && want + 1 == dn &&
+                     snappy_decode_global(p.src + s, len - 1, h, dst, want);
+    if (lane == 0) {
+      if (dn) dst[dn - 1] = ok2 ? 1 : 0;                       // re-tagged, or BAD_TAG
+      p.status[b] = ok2 ? (uint8_t)TPZ_BLOCK_OK : (uint8_t)TPZ_BLOCK_CODEC_ERROR;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
   }
-  if (h != 0 && want + 1 > TPZ_MAX_BLOCK_BYTES) st = TPZ_BLOCK_TOO_LARGE;  // sizes gave 1 byte
   if (fits && h != 0 && want + 1 == dn) {
     STAMP(2);
     ok = snappy_decode(in, (u32)(len - 1), h, out, (u32)want STAMPS_PASS);

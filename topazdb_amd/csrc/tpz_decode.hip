@@ -12,10 +12,14 @@
 //    workgroup, one workgroup per CU, persistent over the batch. The NEXT block's bytes are
 //    prefetched into VGPRs (5 x dwordx4 per lane = 5 KiB per wave) while the current block is
 //    processed out of the wave's LDS slot, so HBM reads stay in flight during the decode.
-//  * big path   — blocks that do not fit a wave slot (len > 5104 B or n > 256) are appended to
-//    a device worklist by the wave path and decoded by a second kernel, one wave per block with
-//    a 92 KiB LDS window (TPZ_MAX_BLOCK_BYTES: every block a 64 KiB-target BlockBuilder can
-//    emit) and its entry table in a per-workgroup global scratch (no entry-count limit).
+//  * big path   — blocks that do not fit a wave slot (len > 4336 B or n > 255) are appended to
+//    a device worklist by the wave path and decoded by a second kernel, one 16-wave workgroup
+//    per block with a 92 KiB LDS window (TPZ_LDS_BLOCK_BYTES: every block a 64 KiB-target
+//    BlockBuilder can emit).
+//  * spill path — blocks longer than TPZ_LDS_BLOCK_BYTES, and blocks whose entries overlap or
+//    repeat so that their decoded bytes do not fit the slot (the reference iterator accepts any
+//    offsets, src/block/iterator.rs:63-83), are appended to the spill worklist by either path and
+//    decoded by tpz_spill.hip into the caller's spill arena.
 //  CRC-32: the payload is cut into 80-byte runs aligned to its END; lane l folds run l with
 //  five slice-by-16 steps (fused with the copy's windows on the wave path), then a lane tree
 //  (exec-masked shift-by-80*2^k lookups, DPP row shifts, readlane across rows) combines them.
@@ -70,19 +74,21 @@ static_assert(kWaveLds <= 163840, "wave path LDS");
 constexpr int kBigWaves = 16;
 constexpr int kBigThreads = kBigWaves * kWave;
 constexpr int kBigWinBytes = 94208;
-constexpr u32 kBigMaxLen = TPZ_MAX_BLOCK_BYTES;     // 94192 (a0 + len <= window)
+constexpr u32 kBigMaxLen = TPZ_LDS_BLOCK_BYTES;     // 94192 (a0 + len <= window)
 constexpr int kBigMapLen = 5904;                    // >= (kBigMaxLen + 2) / 16 + 3
 constexpr int kBigStage = (kBigWinBytes + 16 * kBigThreads - 1) / (16 * kBigThreads);  // 6
 constexpr int kBigMaxGroups = 736;                  // n <= (P - 2) / 2 < 47096 entries / 64
 constexpr int kBigMaxWin = 96;                      // copy windows: npad / 64 <= 92
-constexpr int kBigLdsSlots = 1152;                  // u64 entries of the LDS entry table
+constexpr int kBigLdsSlots = 960;                   // u64 entries of the LDS entry table
 constexpr int kBigSuper = 20;                       // CRC super-rounds: ceil(94208 / 5120) <= 19
 constexpr int kBigLds = kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2 +
-                        kBigMaxGroups * 8 + kBigMaxWin * 4 + kBigWaves * 4 + kBigLdsSlots * 8;
+                        kBigMaxGroups * 10 + kBigMaxWin * 4 + kBigWaves * 4 + kBigLdsSlots * 8;
 static_assert(kBigMaxLen + 16 <= kBigWinBytes, "big window");
 static_assert(kBigMapLen % 8 == 0 && (kWaveMaxLen + 2) / 16 + 3 <= (u32)kWaveMapLen &&
               (kBigMaxLen + 2) / 16 + 3 <= (u32)kBigMapLen, "map sizes");
 static_assert(kBigLds <= 163840, "big path LDS");
+static_assert((kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2 + kBigMaxWin * 4 +
+               kBigWaves * 4) % 8 == 0, "big path entry table alignment");
 
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -374,7 +380,7 @@ __device__ __forceinline__ u32 lanes_below(u64 mask) {
 // LDS, 1 issue the next block's loads, 2 header + parse, 3 copy, 4 CRC, 5 status write + loop.
 #ifdef TPZ_ABL_STAMPS
 constexpr int kStampWaves = 256 * kWavesPerWG;
-__device__ u64 g_stamps[kStampWaves * 8];
+__device__ u64 g_stamps[2 * kStampWaves * 8];   // wave kernel, then the big kernel
 struct Stamps {
   u64 t[6] = {0, 0, 0, 0, 0, 0};
   u64 last = 0;
@@ -408,7 +414,14 @@ struct Out {
   u32* crc;
   u32* defer_list;
   u32* defer_count;
+  u32* spill_list;
+  u32* spill_count;
 };
+
+// Lane 0 appends block b to a worklist (the big path's or the spill path's).
+__device__ __forceinline__ void defer_to(u32* list, u32* count, u32 b) {
+  if (lane_id() == 0) list[atomicAdd(count, 1u)] = b;
+}
 
 // Lane 0 stores block b's status, count and crc. Every lane issues the three buffer stores
 // (the others at an offset past the descriptor, which the hardware drops) instead of a
@@ -682,7 +695,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     st = TPZ_BLOCK_MALFORMED;
     cnt = 0;
   } else if (!BIG && n > kWaveMaxN) {
-    if (lane == 0) o.defer_list[atomicAdd(o.defer_count, 1u)] = b;
+    defer_to(o.defer_list, o.defer_count, b);
     return;
   } else {
 #ifndef TPZ_ABL_NOPARSE
@@ -692,8 +705,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
     const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
     {
-      // clear the chunk map up to the largest chunk index a non-OVERLAP block can produce
-      // (stream <= len + 2 bytes)
+      // clear the chunk map up to the largest chunk index a block that fits its slot can
+      // produce (stream <= len + 2 bytes; the others go to the spill path)
       constexpr u32 per = 16 / sizeof(MapT);
       const u32 nz = min((u32)kMapLen, ((len >> 4) + 3 + per - 1) / per * per);
       for (u32 i = lane; i < nz / per; i += 64)
@@ -747,7 +760,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
           whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
       if (act && slots_fit) {
         // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
-        // after the segment's end (ends beyond the map only occur in OVERLAP blocks)
+        // after the segment's end (ends beyond the map only occur in blocks that spill)
         if (kl) {
           const u32 m = knz + lanes_below(kmask);
           col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
@@ -772,7 +785,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       st = TPZ_BLOCK_MALFORMED;
       cnt = 0;
     } else if (!slots_fit || vs + vc > len + 2) {   // the slot holds len + 129 bytes
-      st = TPZ_BLOCK_OVERLAP;
+      // entries overlap or repeat: the spill path decodes the block (CRC included)
+      defer_to(o.spill_list, o.spill_count, b);
+      return;
     } else {
       if (BIG) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -869,6 +884,7 @@ __device__ __forceinline__ void fix_tail(uint4& v, const uint8_t* src, u64 piece
 
 struct Params {
   u64* big_scratch;  // gridDim(big) x 2 x kBigMaxSlots u64
+  u64* spill_used;   // the spill arena cursor, zeroed here for the spill kernel
   const uint8_t* src;
   const u64* ext;
   u64 src_bytes;
@@ -882,6 +898,7 @@ struct Params {
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill kernel runs after
   load_tables(tab, p.crc_tables);
 
   const u32 wid = uni(threadIdx.x >> 6);
@@ -977,9 +994,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
                                                            len64, bcur, s, p.out, S);
     } else if (len64 > kBigMaxLen) {
-      put_meta(p.out, bcur, TPZ_BLOCK_TOO_LARGE, 0, 0);
-    } else if (lane == 0) {
-      p.out.defer_list[atomicAdd(p.out.defer_count, 1u)] = bcur;
+      defer_to(p.out.spill_list, p.out.spill_count, bcur);
+    } else {
+      defer_to(p.out.defer_list, p.out.defer_count, bcur);
     }
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
@@ -1004,26 +1021,34 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 //   CRC     wave w folds the 5120-B super-rounds r = w (mod 16) as wave_crc does and shifts each
 //           by its distance to the block end (gf_mul with x^(8*5120 r)); the 16 wave values
 //           XOR into R0 of the payload.
-// Group sums, packed: key bytes [0,17), value bytes [17,34), non-empty keys [34,41), non-empty
-// values [41,48), malformed [48] (key + value bytes <= dl < 2^17).
+// Group sums in LDS: key bytes and value bytes as full u32 (entries may overlap or repeat, so a
+// group's sums are bounded by 64 x 65535, not by the block length; a block's by 47096 x 65535 <
+// 2^32), and cnt = non-empty keys [0,7) | non-empty values [7,14) | malformed [14].
 __device__ __forceinline__ u32 wave_sum(u32 x) { return readlane(wave_scan_incl(x), 63); }
 __device__ __forceinline__ u32 wave_max(u32 x) { return readlane(wave_scan_max(x), 63); }
+
+struct GroupSums {
+  u32* kb;
+  u32* vb;
+  uint16_t* cnt;
+};
 
 struct BigSums {
   u32 kb = 0, vb = 0, kn = 0, vn = 0;
   bool bad = false;
-  // add the packed sums of groups [lo, hi) (wave-uniform)
-  __device__ __forceinline__ void add(const u64* gsum, u32 lo, u32 hi) {
+  // add the sums of groups [lo, hi) (wave-uniform)
+  __device__ __forceinline__ void add(const GroupSums& gs, u32 lo, u32 hi) {
     const u32 lane = lane_id();
     for (u32 u0 = lo; u0 < hi; u0 += 64) {
       const u32 u = u0 + lane;
-      const u64 g = u < hi ? gsum[u] : 0ull;
-      kb += wave_sum((u32)g & 0x1FFFFu);
-      vb += wave_sum((u32)(g >> 17) & 0x1FFFFu);
-      const u32 c = wave_sum(((u32)(g >> 34) & 0x7Fu) | (((u32)(g >> 41) & 0x7Fu) << 16));
+      const bool in = u < hi;
+      kb += wave_sum(in ? gs.kb[u] : 0u);
+      vb += wave_sum(in ? gs.vb[u] : 0u);
+      const u32 g = in ? (u32)gs.cnt[u] : 0u;
+      const u32 c = wave_sum((g & 0x7Fu) | (((g >> 7) & 0x7Fu) << 16));
       kn += c & 0xFFFFu;
       vn += c >> 16;
-      bad |= __ballot((g >> 48) & 1ull) != 0;
+      bad |= __ballot((g >> 14) & 1u) != 0;
     }
   }
 };
@@ -1068,13 +1093,14 @@ __device__ __forceinline__ u32 big_crc_round(const Params& p, const u32* tab, co
 }
 
 // One big block after the header checks (all threads of the workgroup; n, stored read from the
-// window). Phase 1: the waves that own 64-entry groups parse (one pass when the block has one
-// group, else group sums -> barrier -> pass 2) while the other waves fold the CRC super-rounds
+// window). Phase 1: the waves that own 64-entry groups parse in two passes (group sums, then
+// the ends and tables; with one group the same wave reads its own sums back, so no barrier sits
+// between the passes) while the other waves fold the CRC super-rounds
 // (round r on wave 15 - r mod 16); phase 2: the copy's window maxima; phase 3: the copy; then
 // the wave CRCs are combined and the status stored.
 template <class Col, bool kGlobalCol>
 __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8_t* win,
-                                          const Col& col, uint16_t* map, u64* gsum, u32* wmax,
+                                          const Col& col, uint16_t* map, const GroupSums& gsum, u32* wmax,
                                           u32* xs, u32 a0, u32 len, u32 n, u32 stored, u32 b,
                                           u64 ext_b, Stamps& S) {
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
@@ -1095,7 +1121,7 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
 
   u32 st = TPZ_BLOCK_OK, bcnt = n;
   u32 nk = 0, tot = 0;
-  bool copy = false;
+  bool copy = false, spill = false;
   if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
     st = TPZ_BLOCK_MALFORMED;
     bcnt = 0;
@@ -1116,8 +1142,11 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
       const u32 kb = wave_sum(kl), vb = wave_sum(vl);
       const u32 kn = __builtin_popcountll(__ballot(kl != 0)), vn = __builtin_popcountll(__ballot(vl != 0));
       const bool bad = __ballot(!ok) != 0;
-      if (lane == 0)
-        gsum[g] = (u64)kb | ((u64)vb << 17) | ((u64)kn << 34) | ((u64)vn << 41) | ((u64)bad << 48);
+      if (lane == 0) {
+        gsum.kb[g] = kb;
+        gsum.vb[g] = vb;
+        gsum.cnt[g] = (uint16_t)(kn | (vn << 7) | ((u32)bad << 14));
+      }
     }
     if (G > 1) __syncthreads();
     // pass 2: entry ends, entry table, chunk map
@@ -1168,8 +1197,8 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     if (T.bad) {
       st = TPZ_BLOCK_MALFORMED;
       bcnt = 0;
-    } else if (!slots_fit || vs + T.vb > len + 2) {  // the slot holds len + 129 bytes
-      st = TPZ_BLOCK_OVERLAP;
+    } else if (!slots_fit || (u64)vs + T.vb > (u64)len + 2) {  // the slot holds len + 129 B
+      spill = true;   // entries overlap or repeat: the spill path decodes the block
     } else {
       copy = true;
       nk = T.kn + T.vn;
@@ -1202,7 +1231,9 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     }
     TPZ_STAMP(S, 3);
   }
-  if (wid == 0) {
+  if (wid == 0 && spill) {
+    defer_to(o.spill_list, o.spill_count, b);
+  } else if (wid == 0) {
     u32 crc;
     if (crc_wave) {
       u32 R = 0;
@@ -1229,19 +1260,22 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
 }
 
 __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
+  const u32 cnt = uni(*p.out.defer_count);
+  if (blockIdx.x >= cnt) return;   // an empty worklist costs one load, not a table upload
   __shared__ __attribute__((aligned(16))) uint8_t lds[kBigLds];
   u32* tab = reinterpret_cast<u32*>(lds);
   load_tables(tab, p.crc_tables);
   const u32 tid = threadIdx.x, wid = uni(tid >> 6), lane = lane_id();
   uint8_t* win = lds + kTableBytes + kGuard;
   uint16_t* map = reinterpret_cast<uint16_t*>(win + kBigWinBytes + 32);
-  u64* gsum = reinterpret_cast<u64*>(map + kBigMapLen);
-  u32* wmax = reinterpret_cast<u32*>(gsum + kBigMaxGroups);
+  u32* wmax = reinterpret_cast<u32*>(map + kBigMapLen);
   u32* xs = wmax + kBigMaxWin;
-  u64* ltab = reinterpret_cast<u64*>(xs + kBigWaves);
+  u64* ltab = reinterpret_cast<u64*>(xs + kBigWaves);        // 8-aligned: see static_assert
+  GroupSums gsum;
+  gsum.kb = reinterpret_cast<u32*>(ltab + kBigLdsSlots);
+  gsum.vb = gsum.kb + kBigMaxGroups;
+  gsum.cnt = reinterpret_cast<uint16_t*>(gsum.vb + kBigMaxGroups);
   if (tid < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[tid] = make_uint4(0, 0, 0, 0);
-  const u32 cnt = uni(*p.out.defer_count);
-  if (blockIdx.x >= cnt) return;
   const u32 grid = gridDim.x;
   // This workgroup's blocks, 64 at a time: lane l holds the list entry and extent of its block
   // 64 g + l (list position blockIdx.x + (64 g + l) * grid, clamped to the list).
@@ -1290,7 +1324,7 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
     const u32 nbytes = (u32)(e - ws);
     __syncthreads();  // the previous block is done with the window
     {
-      // clear the chunk map up to the largest chunk index a non-OVERLAP block can produce
+      // clear the chunk map up to the largest chunk index a slot-fitting block can produce
       const u32 nz = min((u32)kBigMapLen, ((len >> 4) + 3 + 7) / 8 * 8);
       for (u32 i = tid; i < nz / 8; i += kBigThreads) reinterpret_cast<uint4*>(map)[i] = make_uint4(0, 0, 0, 0);
     }
@@ -1336,7 +1370,7 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kBigWaves + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
-    for (int q = 0; q < 6; q++) g_stamps[gw * 8 + q] = S.t[q];
+    for (int q = 0; q < 6; q++) g_stamps[(kStampWaves + gw) * 8 + q] = S.t[q];
 #endif
 }
 
@@ -1363,7 +1397,9 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
   p.big_scratch = a.big_scratch;
-  p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count};
+  p.spill_used = a.spill_used;
+  p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count,
+              a.spill_list, a.spill_count};
   const u32* xp = big_super_shifts();
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
@@ -1371,6 +1407,9 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
   hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p);
+  SpillLaunch sp{a.src, a.ext, a.src_bytes, a.crc_tables, a.spill_list, a.spill_count, a.spill,
+                 a.spill_cap, a.spill_off, a.spill_used, a.count, a.status, a.crc, a.num_cus};
+  launch_spill(sp, stream);
 }
 
 }  // namespace tpz
@@ -1378,7 +1417,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
 #ifdef TPZ_ABL_STAMPS
 // Diagnostic build only: copies the per-wave phase sums (8 u64 per wave, 6 used) to the host.
 extern "C" int tpz_debug_stamps(unsigned long long* host, int n_waves) {
-  if (n_waves > tpz::kStampWaves) n_waves = tpz::kStampWaves;
+  if (n_waves > 2 * tpz::kStampWaves) n_waves = 2 * tpz::kStampWaves;  // wave, then big kernel
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tpz::g_stamps), (size_t)n_waves * 8 * 8);
 }
 #endif

@@ -19,7 +19,7 @@ constexpr int kCrcLaneBytes = 80;
 constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
 // Big path entry-table capacity per block and column: slots are only written when 6n <= len
 // (the unified key+value table holds 2 x this).
-constexpr uint32_t kBigMaxSlots = TPZ_MAX_BLOCK_BYTES / 6 + 16;
+constexpr uint32_t kBigMaxSlots = TPZ_LDS_BLOCK_BYTES / 6 + 16;
 
 // Range CRC (tpz_crc.hip): shift-by-16*2^j operators j = 0..kRangeShiftOps-1 in the global
 // range tables (ranges up to 16 * 2^kRangeShiftOps bytes), and the 32-fold replicated
@@ -34,6 +34,16 @@ __host__ __device__ inline uint64_t slot_base(uint64_t ext_i, uint64_t i) {
 }
 __host__ __device__ inline uint64_t entry_base(uint64_t ext_i, uint64_t i) {
   return 16u * (ext_i / 96u + i);
+}
+__host__ __device__ inline uint64_t value_start(uint64_t key_bytes) {
+  return (key_bytes + 15u) & ~(uint64_t)15u;
+}
+// Spill records (include/tpz_gpu.h): u32 ends[2n], then the stream from spill_stream(n).
+__host__ __device__ inline uint64_t spill_stream(uint64_t n) {
+  return (8u * n + 127u) & ~(uint64_t)127u;
+}
+__host__ __device__ inline uint64_t spill_record_bytes(uint64_t n, uint64_t k, uint64_t v) {
+  return spill_stream(n) + ((value_start(k) + v + 127u) & ~(uint64_t)127u);
 }
 
 struct LaunchArgs {
@@ -52,9 +62,34 @@ struct LaunchArgs {
   uint32_t num_cus;
   uint64_t* big_scratch;  // big_grid x 2 x kBigMaxSlots
   uint32_t big_grid;
+  uint32_t* spill_list;   // workspace: n_blocks entries (blocks for the spill path)
+  uint32_t* spill_count;  // workspace: one u32, zeroed before the launch
+  uint8_t* spill;         // the caller's spill arena (tpz_columns)
+  uint64_t spill_cap;
+  uint64_t* spill_off;
+  uint64_t* spill_used;   // zeroed before the launch
 };
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
+
+// The spill path (tpz_spill.hip): blocks the LDS paths hand over, decoded into the arena.
+struct SpillLaunch {
+  const uint8_t* src;
+  const uint64_t* ext;
+  uint64_t src_bytes;
+  const uint32_t* crc_tables;
+  const uint32_t* list;
+  const uint32_t* list_count;
+  uint8_t* spill;
+  uint64_t spill_cap;
+  uint64_t* spill_off;
+  uint64_t* spill_used;
+  uint32_t* count;
+  uint8_t* status;
+  uint32_t* crc;
+  uint32_t grid;
+};
+void launch_spill(const SpillLaunch& a, hipStream_t stream);
 
 struct CrcLaunch {
   const uint8_t* src;
@@ -81,6 +116,8 @@ struct SeekLaunch {
   const uint32_t* ends;
   const uint32_t* count;
   const uint8_t* bstatus;
+  const uint8_t* spill;
+  const uint64_t* spill_off;
   const uint8_t* q;
   const uint64_t* q_pos;
   uint32_t n_q;
@@ -107,6 +144,8 @@ struct PackLaunch {
   const uint32_t* ends;
   const uint32_t* count;
   const uint8_t* status;
+  const uint8_t* spill;
+  const uint64_t* spill_off;
   const uint64_t* first;
   uint32_t* dense;
 };

@@ -13,7 +13,7 @@
 // One thread per query: both are a few binary-search steps of dependent global loads (keys of a
 // few tens of bytes), latency-bound, so the launch simply puts many queries in flight. A query
 // whose block did not decode gets that block's status (the reference's read_block_cached Err, or
-// its panic for MALFORMED); OVERLAP blocks (a device limit) report OVERLAP.
+// its panic for MALFORMED); OK_SPILLED blocks are read from their spill records and report OK.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -47,6 +47,8 @@ struct SeekParams {
   const u32* ends;
   const u32* count;
   const uint8_t* bstatus;
+  const uint8_t* spill;     // spill arena + record offsets (OK_SPILLED blocks)
+  const u64* spill_off;
   const uint8_t* q;         // query keys, packed
   const u64* q_pos;         // n_q + 1
   u32 n_q;
@@ -56,13 +58,27 @@ struct SeekParams {
   uint8_t* out_valid;
 };
 
-// Entry j's key in block b: its bytes and length.
-__device__ __forceinline__ const uint8_t* entry_key(const SeekParams& p, u32 b, u32 j, u64& len) {
+// A decoded block's ends and stream: its slot, or its spill record (include/tpz_gpu.h).
+struct BlockView {
+  const u32* ends;
+  const uint8_t* stream;
+};
+__device__ __forceinline__ BlockView block_view(const SeekParams& p, u32 b, u32 st) {
+  if (st == TPZ_BLOCK_OK_SPILLED) {
+    const uint8_t* r = p.spill + p.spill_off[b];
+    return BlockView{reinterpret_cast<const u32*>(r), r + spill_stream(p.count[b])};
+  }
   const u64 e0 = p.ext[b];
-  const u64 s = slot_base(e0, b), e = entry_base(e0, b);
-  const u32 lo = j ? p.ends[2 * (e + j - 1)] : 0u, hi = p.ends[2 * (e + j)];
+  return BlockView{p.ends + 2 * entry_base(e0, b), p.data + slot_base(e0, b)};
+}
+// Entry j's key: its bytes and length.
+__device__ __forceinline__ const uint8_t* entry_key(const BlockView& v, u32 j, u64& len) {
+  const u32 lo = j ? v.ends[2 * (j - 1)] : 0u, hi = v.ends[2 * j];
   len = hi - lo;
-  return p.data + s + lo;
+  return v.stream + lo;
+}
+__device__ __forceinline__ bool decoded(u32 st) {
+  return st == TPZ_BLOCK_OK || st == TPZ_BLOCK_OK_SPILLED;
 }
 
 __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
@@ -87,8 +103,9 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
   u32 b = lo ? lo - 1 : 0;
   u32 st = p.bstatus[b], pos = 0;
   bool valid = false;
-  if (st == TPZ_BLOCK_OK) {
+  if (decoded(st)) {
     // BlockIterator::seek_to_key
+    const BlockView v = block_view(p, b, st);
     const u32 n = p.count[b];
     u32 l = 0, r = n;
     pos = n;
@@ -96,7 +113,7 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
     while (l < r) {
       const u32 mid = (r - l) / 2 + l;
       u64 kl;
-      const uint8_t* k = entry_key(p, b, mid, kl);
+      const uint8_t* k = entry_key(v, mid, kl);
       const int c = key_cmp(k, kl, qk, ql);
       if (c > 0) r = mid;
       else if (c < 0) l = mid + 1;
@@ -104,23 +121,23 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
     }
     if (!found) pos = l;
     u64 kl = 0;
-    if (pos < n) entry_key(p, b, pos, kl);
+    if (pos < n) entry_key(v, pos, kl);
     valid = pos < n && kl > 0;                // is_valid: the current key is non-empty
     if (!valid && b + 1 < p.n_blocks) {       // the next block, from its first entry
       b++;
       st = p.bstatus[b];
       pos = 0;
       valid = false;
-      if (st == TPZ_BLOCK_OK && p.count[b] > 0) {
-        entry_key(p, b, 0, kl);
+      if (decoded(st) && p.count[b] > 0) {
+        entry_key(block_view(p, b, st), 0, kl);
         valid = kl > 0;
       }
     }
   }
   p.out_block[i] = b;
   p.out_entry[i] = pos;
-  p.out_status[i] = (uint8_t)st;
-  p.out_valid[i] = st == TPZ_BLOCK_OK && valid;
+  p.out_status[i] = decoded(st) ? (uint8_t)TPZ_BLOCK_OK : (uint8_t)st;
+  p.out_valid[i] = decoded(st) && valid;
 }
 
 struct BloomParams {
@@ -160,17 +177,19 @@ __global__ __launch_bounds__(256) void bloom_kernel(BloomParams p) {
   p.out[i] = hit;
 }
 
-// Dense entry ends: block b's count[b] {kend, vend} pairs (status OK; zeros otherwise) moved
-// from its worst-case-sized slot (tpz_entry_base) to dense[2 * first[b] ..]. One wave per block.
-__global__ __launch_bounds__(256) void pack_ends_kernel(const u64* ext, u32 n, const u32* ends,
-                                                        const u32* count, const uint8_t* status,
-                                                        const u64* first, uint2* dense) {
+// Dense entry ends: block b's count[b] {kend, vend} pairs (status OK: from its worst-case-sized
+// slot, tpz_entry_base; OK_SPILLED: from its spill record; zeros otherwise) moved to
+// dense[2 * first[b] ..]. One wave per block.
+__global__ __launch_bounds__(256) void pack_ends_kernel(PackLaunch a, uint2* dense) {
   const u32 lane = threadIdx.x & 63u;
   const u32 nw = gridDim.x * (blockDim.x >> 6);
-  for (u32 b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < n; b += nw) {
-    const u64 f = first[b], c = first[b + 1] - f;
-    const bool ok = status[b] == TPZ_BLOCK_OK;
-    const uint2* src = reinterpret_cast<const uint2*>(ends) + entry_base(ext[b], b);
+  for (u32 b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < a.n_blocks; b += nw) {
+    const u64 f = a.first[b], c = a.first[b + 1] - f;
+    const u32 st = a.status[b];
+    const bool ok = st == TPZ_BLOCK_OK || st == TPZ_BLOCK_OK_SPILLED;
+    const uint2* src = st == TPZ_BLOCK_OK_SPILLED
+                           ? reinterpret_cast<const uint2*>(a.spill + a.spill_off[b])
+                           : reinterpret_cast<const uint2*>(a.ends) + entry_base(a.ext[b], b);
     for (u64 j = lane; j < c; j += 64) dense[f + j] = ok ? src[j] : make_uint2(0, 0);
   }
 }
@@ -180,13 +199,14 @@ __global__ __launch_bounds__(256) void pack_ends_kernel(const u64* ext, u32 n, c
 void launch_pack_ends(const PackLaunch& a, hipStream_t stream) {
   u32 grid = (a.n_blocks + 3) / 4;
   if (grid > 65535) grid = 65535;
-  hipLaunchKernelGGL(pack_ends_kernel, dim3(grid), dim3(256), 0, stream, a.ext, a.n_blocks,
-                     a.ends, a.count, a.status, a.first, reinterpret_cast<uint2*>(a.dense));
+  hipLaunchKernelGGL(pack_ends_kernel, dim3(grid), dim3(256), 0, stream, a,
+                     reinterpret_cast<uint2*>(a.dense));
 }
 
 void launch_seek(const SeekLaunch& a, hipStream_t stream) {
   SeekParams p{a.fk, a.fk_pos, a.n_blocks, a.ext, a.data, a.ends, a.count, a.bstatus,
-               a.q, a.q_pos, a.n_q, a.out_block, a.out_entry, a.out_status, a.out_valid};
+               a.spill, a.spill_off, a.q, a.q_pos, a.n_q, a.out_block, a.out_entry,
+               a.out_status, a.out_valid};
   hipLaunchKernelGGL(seek_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
 }
 

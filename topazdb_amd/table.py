@@ -145,7 +145,8 @@ class DeviceTable:
             batch, st = decompress_batch(ctx, batch)
             self.codec = st[:nb]
         self.batch = batch
-        self.cols = decode_batch(ctx, batch)
+        # complete(): blocks that spilled into a too-small arena are decoded again with room
+        self.cols = decode_batch(ctx, batch).complete()
         # the status a reader of block i sees: the codec's Err wins over the decode of its stub
         self.status = self.cols.status[:max(nb, 1)].clone()
         if self.codec is not None:
@@ -161,7 +162,9 @@ class DeviceTable:
         c = self.cols
         return _lib.Table(self.first_keys.data_ptr(), self.first_pos.data_ptr(),
                           self.batch.ext.data_ptr(), self.n_blocks, c.data.data_ptr(),
-                          c.ends.data_ptr(), c.count.data_ptr(), self.status.data_ptr())
+                          c.ends.data_ptr(), c.count.data_ptr(), self.status.data_ptr(),
+                          c.spill.data_ptr() if c.spill is not None else None,
+                          c.spill_off.data_ptr())
 
     def seek_keys(self, keys: list[bytes]) -> dict:
         """SsTableIterator::seek_to_key (src/table/iterator.rs:44-72) for every key: the block
