@@ -178,78 +178,124 @@ def cpu_baseline(src, ext, gen, n_ent, threads, target_s=12.0):
 
 
 # ------------------------------------------------------------------ H2D/D2H-inclusive
-def e2e_rate(ctx, src, ext, dev, chunk_blocks=65536):
-    """Pinned host blocks -> H2D -> decode -> pack the used entry ends (tpz_pack_ends) -> D2H of
-    the data stream, the dense ends and the per-block metadata, chunked over two streams. A
-    chunk's data and ends go back once its metadata (and so its entry total) is on the host,
-    which the host waits for while the next chunk already runs. Returns GiB/s of encoded input;
-    checks the returned entry totals against the input's."""
+def parse_cpulist(text: str) -> list[int]:
+    """Linux cpulist ("0-3,8,10-11") -> CPU ids."""
+    cpus = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.extend(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def gpu_local_cpus(device: int) -> list[int]:
+    """Host CPUs on the NUMA node of HIP device `device` (its PCI function's local_cpulist), so
+    that the rank's pinned buffers are first-touched on the node its PCIe link hangs off."""
+    try:
+        import ctypes as C
+        hip = C.CDLL("libamdhip64.so")
+        buf = C.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return []
+        bus = buf.value.decode().lower()
+        with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+            return parse_cpulist(f.read())
+    except Exception:
+        return []
+
+
+def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps: int = 2,
+             chunk_blocks: int = 0) -> dict:
+    """Host memory -> HBM -> host memory through the library's own pipeline
+    (tpz_decode_blocks_host: chunked H2D, decode, packed ends, D2H on two streams), from and to
+    pinned host buffers allocated on the GPU's NUMA node. Beside it, the copy-only ceiling of the
+    same transfers: the input's H2D and a D2H of the same bytes the pipeline returns, issued
+    together on two streams (duplex PCIe). GiB/s of encoded input; every returned status and
+    the entry total are checked."""
     nb = len(ext) - 1
-    h_src = torch.from_numpy(src).pin_memory()
-    streams = [torch.cuda.Stream(dev) for _ in range(2)]
-    cb = min(chunk_blocks, nb)
-    cap = max(int(ext[min(k + cb, nb)] - ext[k]) for k in range(0, nb, cb))
-    slots = []
+    cpus = gpu_local_cpus(dev.index)
+    old = os.sched_getaffinity(0)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    try:
+        h_src = torch.from_numpy(src).pin_memory()
+        dcap = _lib.data_capacity(int(ext[-1]), nb)
+        h_data = torch.empty(dcap, dtype=torch.uint8).pin_memory()
+        ends_cap = 2 * int(n_ent.sum()) + 64
+        h_ends = torch.empty(ends_cap, dtype=torch.int32).pin_memory()
+    finally:
+        os.sched_setaffinity(0, old)
+    h_ext = np.ascontiguousarray(ext, np.uint64)
+    first = np.zeros(nb + 1, np.uint64)
+    count = np.zeros(nb, np.uint32)
+    status = np.zeros(nb, np.uint8)
+    crc = np.zeros(nb, np.uint32)
+    spill_off = np.zeros(nb, np.uint64)
+    spill_used = np.zeros(1, np.uint64)
+    cols = _lib.HostColumns(h_data.data_ptr(), h_ends.data_ptr(), ends_cap, first.ctypes.data,
+                            count.ctypes.data, status.ctypes.data, crc.ctypes.data, None, 0,
+                            spill_off.ctypes.data, spill_used.ctypes.data)
+
+    def run():
+        rc = ctx.decode_host_ptrs(h_src.data_ptr(), h_ext.ctypes.data, nb, cols, chunk_blocks)
+        assert rc == _lib.SUCCESS, "tpz_decode_blocks_host"
+    run()                                               # warm: allocations, registrations
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    assert (status == 0).all() and int(first[-1]) == int(n_ent.sum()), "e2e outputs"
+    dt = min(ts)
+    # copy-only ceiling: the same H2D and D2H volumes, both directions at once
+    down = int(_lib.slot_base(int(ext[-1]), nb) - _lib.slot_base(int(ext[0]), 0)) + 8 * int(first[-1])
+    d_src = torch.empty(int(ext[-1]), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(down, dtype=torch.uint8, device=dev)
+    h_out = h_data if down <= dcap else torch.empty(down, dtype=torch.uint8).pin_memory()
+    s_up, s_dn = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    cts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_up):
+            d_src.copy_(h_src[:int(ext[-1])], non_blocking=True)
+        with torch.cuda.stream(s_dn):
+            h_out[:down].copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        cts.append(time.perf_counter() - t0)
+    ct = min(cts[1:])
+    in_bytes = float(ext[-1] - ext[0])
+    return {"gib_s": round(in_bytes / dt / GIB, 2), "s": round(dt, 4),
+            "copy_only_gib_s": round(in_bytes / ct / GIB, 2), "copy_only_s": round(ct, 4),
+            "frac_of_copy_only": round(ct / dt, 3), "h2d_bytes": int(in_bytes), "d2h_bytes": down,
+            "numa_cpus": len(cpus), "path": "tpz_decode_blocks_host (C ABI)"}
+
+
+def copy_ceiling(batch: DeviceBatch, cols: SlottedColumns, alg_bytes: int, dev,
+                 steps: int = 10) -> dict:
+    """This box's achievable HBM rate for the decode's traffic mix: a device-to-device copy of
+    the shard's input bytes into the output buffer (hipMemcpyAsync D2D through torch), so it reads
+    and writes the same byte count the decode does, timed on the same stream right after it.
+    On MI355X an HBM-resident copy reaches ~4.9-5.5 TB/s (tools/ubench_bw.hip;
+    profiles/r2/bw_ceiling.jsonl), well under the 8.0 TB/s spec peak: the decode's own roofline
+    fraction is reported against both."""
+    n = batch.src_bytes
+    src = batch.src[:n]
+    dst = cols.data[:n]
+    stream = torch.cuda.current_stream(dev)
     for _ in range(2):
-        cols = SlottedColumns(cb, cap, dev.index)
-        slots.append({
-            "d_src": torch.empty(cap + 64, dtype=torch.uint8, device=dev),
-            "d_ext": torch.empty(cb + 1, dtype=torch.int64, device=dev),
-            "cols": cols,
-            "h_data": torch.empty(cols.data.numel(), dtype=torch.uint8).pin_memory(),
-            "h_dense": torch.empty(cols.ends.numel(), dtype=torch.int32).pin_memory(),
-            "h_count": torch.empty(cb, dtype=torch.int32).pin_memory(),
-            "h_status": torch.empty(cb, dtype=torch.uint8).pin_memory(),
-            "h_crc": torch.empty(cb, dtype=torch.int32).pin_memory(),
-            "h_total": torch.empty(1, dtype=torch.int64).pin_memory(),
-            "first": torch.zeros(cb + 1, dtype=torch.int64, device=dev),
-            "dense": torch.empty(cols.ends.numel(), dtype=torch.int32, device=dev),
-        })
-    h_ext = torch.from_numpy(ext.astype(np.int64)).pin_memory()
-    entries = [0]
-
-    def finish(job):
-        lo, hi, slot, ev, s, dense = job
-        ev.synchronize()
-        total = int(slot["h_total"][0])
-        entries[0] += total
-        dc = _lib.data_capacity(int(ext[hi] - ext[lo]), hi - lo)
-        with torch.cuda.stream(s):
-            slot["h_data"][:dc].copy_(slot["cols"].data[:dc], non_blocking=True)
-            slot["h_dense"][:2 * total].copy_(dense[:2 * total], non_blocking=True)
-
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        dst.copy_(src)
+    e1.record(stream)
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    pending = None
-    for ci, lo in enumerate(range(0, nb, cb)):
-        hi = min(nb, lo + cb)
-        s, slot = streams[ci & 1], slots[ci & 1]
-        cols = slot["cols"]
-        base, end = int(ext[lo]), int(ext[hi])
-        with torch.cuda.stream(s):
-            slot["d_src"][:end - base].copy_(h_src[base:end], non_blocking=True)
-            slot["d_ext"][:hi - lo + 1].copy_(h_ext[lo:hi + 1], non_blocking=True)
-            slot["d_ext"][:hi - lo + 1] -= base
-            n = hi - lo
-            ctx.decode_ptrs(slot["d_src"].data_ptr(), slot["d_ext"].data_ptr(), n, end - base,
-                            cols.ptrs(), s.cuda_stream)
-            first, dense = slot["first"], slot["dense"]
-            torch.cumsum(cols.count[:n].to(torch.int64), 0, out=first[1:n + 1])
-            _lib._pack_ends(ctx, slot["d_ext"].data_ptr(), n, end - base, cols.ptrs(),
-                            first.data_ptr(), dense.data_ptr(), s.cuda_stream)
-            slot["h_count"][:hi - lo].copy_(cols.count[:hi - lo], non_blocking=True)
-            slot["h_status"][:hi - lo].copy_(cols.status[:hi - lo], non_blocking=True)
-            slot["h_crc"][:hi - lo].copy_(cols.crc[:hi - lo], non_blocking=True)
-            slot["h_total"].copy_(first[hi - lo:hi - lo + 1], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(s)
-        if pending is not None:
-            finish(pending)
-        pending = (lo, hi, slot, ev, s, dense)
-    finish(pending)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    return float(ext[-1] - ext[0]) / dt / GIB, entries[0]
+    ms = e0.elapsed_time(e1) / steps
+    gbs = 2.0 * n / (ms * 1e-3) / 1e9
+    return {"d2d_copy_gb_s": round(gbs, 1), "d2d_copy_ms": round(ms, 4),
+            "decode_ms_at_copy_rate": round(alg_bytes / (gbs * 1e9) * 1e3, 4)}
 
 
 def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10) -> dict:
@@ -409,6 +455,93 @@ def make_shard(config: str, nb: int, rank: int):
     return src, ext, gen, n_ent, int(gen[1][etot]), int(gen[3][etot])
 
 
+def replicate_plan(src_bytes: int, nb: int, target_bytes: int) -> tuple[int, int]:
+    """BASELINE.json configs[4] (12.5 GiB of 4 KiB blocks per GPU) from one generated shard:
+    (full copies, blocks of the partial last copy). The shard's byte size must be a multiple
+    of 384 = lcm(128, 96), so every copy's slots and entry slots are the first copy's shifted
+    by a constant (tpz_slot_base / tpz_entry_base); the partial copy is a multiple of 128
+    blocks."""
+    assert src_bytes % 384 == 0, "shard size must be a multiple of 384 bytes"
+    full = max(1, target_bytes // src_bytes)
+    rem = target_bytes - full * src_bytes
+    part = (rem * nb // src_bytes) // 128 * 128 if rem > 0 else 0
+    return int(full), int(part)
+
+
+def replicate_on_device(src: np.ndarray, ext: np.ndarray, full: int, part: int, dev):
+    """The device batch of `full` copies of the shard plus the first `part` blocks once more,
+    back to back (extents shifted per copy). Returns (DeviceBatch, host extents)."""
+    S = int(ext[-1])
+    nb = len(ext) - 1
+    total = full * S + (int(ext[part]) if part else 0)
+    d_src = torch.empty(total, dtype=torch.uint8, device=dev)
+    first = torch.from_numpy(src).to(dev)
+    for c in range(full):
+        d_src[c * S:(c + 1) * S].copy_(first)
+    if part:
+        d_src[full * S:].copy_(first[:int(ext[part])])
+    del first
+    ext_all = replicated_extents(ext, full, part)
+    return DeviceBatch(d_src, ext_all, dev.index), ext_all
+
+
+def replicated_extents(ext: np.ndarray, full: int, part: int) -> np.ndarray:
+    """Extents of `full` back-to-back copies of a shard plus its first `part` blocks."""
+    S = int(ext[-1])
+    exts = [ext[:-1].astype(np.int64) + c * S for c in range(full)]
+    exts.append(ext[:part + 1].astype(np.int64) + full * S)
+    return np.concatenate(exts).astype(np.uint64)
+
+
+def combine_e2e(dist, r, world: int, device):
+    """Whole-job H2D/D2H-inclusive rate from every rank's e2e_rate result (None if it failed):
+    each rank joins the MAX reduction of the times (a failure counts as infinite), and the rate
+    is every rank's input bytes over the slowest rank's time."""
+    t_max, ct_max = max_over_ranks(dist, [r["s"], r["copy_only_s"]] if r else
+                                   [float("inf"), float("inf")], device)
+    if not r or t_max == float("inf"):
+        return None
+    e2e = dict(r)
+    e2e["gib_s"] = round(job_rate(r["h2d_bytes"], world, 1, t_max), 2)
+    e2e["copy_only_gib_s"] = round(job_rate(r["h2d_bytes"], world, 1, ct_max), 2)
+    e2e["frac_of_copy_only"] = round(ct_max / t_max, 3)
+    e2e["ranks"] = world
+    return e2e
+
+
+def validate_replicas(cols: SlottedColumns, ext: np.ndarray, nb: int, full: int, part: int,
+                      dev, sample: float = 0.01) -> None:
+    """Copies 1.. of the shard decode to the first copy's bytes, shifted: every block's status,
+    count and CRC, and the data slots and entry ends of a 1 % sample of blocks (SURVEY.md §8d
+    config 5: sampled validation)."""
+    S = int(ext[-1])
+    g = torch.Generator()
+    g.manual_seed(5)
+    st, cnt, crc = cols.status, cols.count, cols.crc
+    ext64 = ext[:nb].astype(np.int64)
+    for c in range(1, full + (1 if part else 0)):
+        m = nb if c < full else part
+        lo = c * nb
+        assert torch.equal(st[lo:lo + m], st[:m]) and torch.equal(cnt[lo:lo + m], cnt[:m]) and \
+            torch.equal(crc[lo:lo + m], crc[:m]), f"replica {c} metadata"
+        pick = torch.randperm(m, generator=g)[:max(1, int(m * sample))].numpy()
+        for b in pick[:64]:
+            b = int(b)
+            sb0 = int(_lib.slot_base(int(ext64[b]), b))
+            sb1 = int(_lib.slot_base(int(ext64[b]) + c * S, b + lo))
+            n = int(cnt[b])
+            e0 = int(_lib.entry_base(int(ext64[b]), b))
+            e1 = int(_lib.entry_base(int(ext64[b]) + c * S, b + lo))
+            ends0 = cols.ends[2 * e0:2 * (e0 + n)]
+            assert torch.equal(cols.ends[2 * e1:2 * (e1 + n)], ends0), f"replica {c} ends"
+            if n:
+                K = int(ends0[-2])
+                ln = int(_lib.value_start(K)) + int(ends0[-1])
+                assert torch.equal(cols.data[sb1:sb1 + ln][:K], cols.data[sb0:sb0 + ln][:K]) and \
+                    torch.equal(cols.data[sb1 + ln - int(ends0[-1]):sb1 + ln],
+                                cols.data[sb0 + ln - int(ends0[-1]):sb0 + ln]), f"replica {c} data"
+
+
 def max_over_ranks(dist, vals, device) -> list[float]:
     """MAX over ranks of the per-rank timings (the only collective; not on the data path)."""
     t = torch.tensor(vals, dtype=torch.float64, device=device)
@@ -428,7 +561,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="4k", choices=sorted(synth.CONFIGS))
-    ap.add_argument("--blocks", type=int, default=None, help="blocks per GPU")
+    ap.add_argument("--blocks", type=int, default=None, help="blocks generated per GPU")
+    ap.add_argument("--gib-per-gpu", type=float, default=None,
+                    help="decode this many GiB per GPU by replicating the generated shard on the "
+                         "device (default: 12.5 with --gpus > 1, BASELINE.json configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -455,10 +591,21 @@ def main():
     log(rank, f"generated {nb} blocks ({src.nbytes / GIB:.2f} GiB) in {time.time() - t0:.1f} s")
 
     ctx = _lib.Context(local)
-    batch = DeviceBatch(src, ext, local)
-    cols = SlottedColumns(nb, batch.src_bytes, local)
+    gib = args.gib_per_gpu
+    if gib is None and world > 1 and args.config == "4k":
+        gib = 12.5                          # BASELINE.json configs[4]: 100 GiB over 8 GPUs
+    full, part = (1, 0) if not gib else replicate_plan(int(ext[-1]), nb, int(gib * GIB))
+    if full == 1 and part == 0:
+        batch = DeviceBatch(src, ext, local)
+        ext_run = ext
+    else:
+        batch, ext_run = replicate_on_device(src, ext, full, part, dev)
+        log(rank, f"device batch: {full} copies + {part} blocks = {batch.n_blocks} blocks "
+                  f"({batch.src_bytes / GIB:.2f} GiB) per GPU")
+    nb_run = batch.n_blocks
+    cols = SlottedColumns(nb_run, batch.src_bytes, local)
     stream = torch.cuda.current_stream(dev)
-    ctx.reserve(nb, stream.cuda_stream)
+    ctx.reserve(nb_run, stream.cuda_stream)
 
     for _ in range(args.warmup):
         decode_batch(ctx, batch, cols, stream)
@@ -479,24 +626,34 @@ def main():
     wall = time.perf_counter() - t_start
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     wall_max, ev_ms_max = max_over_ranks(dist, [wall, ev_ms], dev)
-    in_bytes = float(ext[-1] - ext[0])
+    in_bytes = float(batch.src_bytes)
     value = job_rate(in_bytes, world, args.steps, wall_max)
-    alg = algorithmic_bytes(ext, n_ent, kbytes, vbytes)
+    copies = full + (part / nb if part else 0.0)
+    alg = int(algorithmic_bytes(ext, n_ent, kbytes, vbytes) * copies) if part == 0 else \
+        algorithmic_bytes(ext, n_ent, kbytes, vbytes) * full + \
+        algorithmic_bytes(ext[:part + 1], n_ent[:part], int(gen[1][int(n_ent[:part].sum())]),
+                          int(gen[3][int(n_ent[:part].sum())]))
     achieved = alg / (ev_ms_max * 1e-3) / 1e9
 
     if not args.no_validate:
         validate(cols, ext, n_ent, gen, dev)
-        log(rank, "validation: all blocks OK, every key/value byte and end offset matches")
+        if full > 1 or part:
+            validate_replicas(cols, ext, nb, full, part, dev)
+        log(rank, "validation: all blocks OK, every key/value byte and end offset matches"
+            + (" (replicas: metadata of every block, 1 % sample of slots)" if full > 1 or part else ""))
+
 
     e2e = None
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
-    if not args.no_e2e and side:
+    if not args.no_e2e:
+        # every rank (BASELINE.json configs[4]: the H2D/D2H-inclusive rate at N GPUs, all ranks
+        # sharing the host's links and memory): per-rank times, max over ranks, all bytes
+        r = None
         try:
-            e2e_v, e2e_entries = e2e_rate(ctx, src, ext, dev)
-            assert e2e_entries == int(n_ent.sum()), "e2e entry total"
-            e2e = round(e2e_v, 2)
+            r = e2e_rate(ctx, src, ext, n_ent, dev)
         except Exception as ex:  # reported, never the metric
             log(rank, f"e2e measurement failed: {ex}")
+        e2e = combine_e2e(dist, r, world, dev)   # every rank joins, failed or not
 
     fcrc = None
     if side and not args.no_file_crc:
@@ -529,6 +686,12 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(src, ext, gen, n_ent, threads)
 
+    ceiling = None
+    try:   # last: the copy overwrites the decoded columns
+        ceiling = copy_ceiling(batch, cols, alg, dev)   # rank 0's box is reported
+    except Exception as ex:  # reported, never the metric
+        log(rank, f"copy ceiling measurement failed: {ex}")
+
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -552,16 +715,22 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"{args.config}: {nb} blocks/GPU x {int(np.median(np.diff(ext)))} B "
-                                   f"median, {n_ent.mean():.1f} entries/block, tag 1 (Uncompress)",
-                       "blocks_per_gpu": nb, "input_bytes_per_gpu": int(in_bytes),
+            "config": {"workload": f"{args.config}: {nb_run} blocks/GPU x {int(np.median(np.diff(ext)))} B "
+                                   f"median, {n_ent.mean():.1f} entries/block, tag 1 (Uncompress)"
+                                   + (f"; {batch.src_bytes / GIB:.2f} GiB/GPU = {full} copies + "
+                                      f"{part} blocks of a {nb}-block generated shard"
+                                      if full > 1 or part else ""),
+                       "blocks_per_gpu": nb_run, "input_bytes_per_gpu": int(in_bytes),
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_launch": alg,
-                         "kernel_ms": round(ev_ms_max, 4)},
+                         "kernel_ms": round(ev_ms_max, 4),
+                         "copy_ceiling": ceiling,
+                         "frac_of_copy_ceiling": (round(achieved / ceiling["d2d_copy_gb_s"], 4)
+                                                  if ceiling else None)},
             "cpu_baseline": cpu,
-            "e2e_h2d_d2h_gib_s": e2e,
+            "e2e_h2d_d2h": e2e,
             "file_crc": fcrc,
             "seek": seek,
             "snappy": snappy,

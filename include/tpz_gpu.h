@@ -5,6 +5,9 @@
  * plain Rust API); each entry point below replaces the reference items it names, and
  * INTEGRATION.md shows the `extern "C"` binding a topazdb maintainer adds on the Rust side.
  *
+ *   tpz_decode_blocks_host  the same from host memory: H2D, decode and D2H pipelined in the
+ *                           library (SsTable::read_block + FileObject::read, table.rs:154-164,
+ *                           file_object.rs:23-27)
  *   tpz_decode_blocks       SsTable::read_block (src/table.rs:154-164) batched over many
  *                           blocks -> Block::decode (src/block.rs:46-65) -> compress::decode
  *                           tag dispatch (src/block/compress.rs:95-113) -> checksum::
@@ -197,6 +200,45 @@ tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_column
  * zeros for a block whose status is neither OK nor OK_SPILLED). */
 tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* cols,
                       const uint64_t* d_first, uint32_t* d_dense, void* stream);
+
+/* ---- the host pipeline -------------------------------------------------------------------
+ * SsTable::read_block for a whole run of blocks that sit in HOST memory (src/table.rs:154-164;
+ * the bytes FileObject::read's pread returns, src/table/file_object.rs:23-27): the library
+ * copies the blocks to the device in chunks, decodes them (tpz_decode_blocks), packs the used
+ * entry ends (tpz_pack_ends) and copies every output back, with chunk k+1's upload and decode
+ * overlapping chunk k's downloads on two streams. Synchronous: returns when every output is in
+ * host memory. The caller's buffers are page-locked for the duration of the call when they are
+ * not already (hipHostRegister); pinned buffers (hipHostMalloc) avoid that cost.
+ *
+ * Block i = h_src[h_ext[i] .. h_ext[i+1]) (h_ext non-decreasing, any alignment). Outputs:
+ *   h_data    tpz_data_capacity(h_ext[n], n) bytes: the slotted stream layout of tpz_columns,
+ *             exactly as tpz_decode_blocks writes it for this batch (slot bases from h_ext)
+ *   h_ends    every decoded block's {kend, vend} pairs, dense in block order: block i's at
+ *             h_ends[2*h_first[i] ..]; ends_cap = its capacity in u32
+ *   h_first   n + 1 entries: h_first[i] = pairs before block i (OK and OK_SPILLED blocks only)
+ *   h_count, h_status, h_crc    n each, as tpz_columns
+ *   h_spill, spill_cap, h_spill_off, h_spill_used   as tpz_columns, in host memory: spilled
+ *             blocks' records (the library's device arenas grow as needed)
+ * Returns TPZ_ERR_NOMEM when ends_cap or spill_cap is too small: h_first[n] and *h_spill_used
+ * then hold the sizes needed (the call can be repeated with larger buffers). chunk_blocks = 0
+ * picks the default (65,536 blocks per chunk). */
+typedef struct {
+  uint8_t* h_data;
+  uint32_t* h_ends;
+  uint64_t ends_cap;
+  uint64_t* h_first;
+  uint32_t* h_count;
+  uint8_t* h_status;
+  uint32_t* h_crc;
+  uint8_t* h_spill;
+  uint64_t spill_cap;
+  uint64_t* h_spill_off;
+  uint64_t* h_spill_used;
+} tpz_host_columns;
+
+tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext,
+                               uint32_t n_blocks, const tpz_host_columns* out,
+                               uint32_t chunk_blocks);
 
 /* ---- whole-range CRC-32 ------------------------------------------------------------------
  * Ranges use the batch type: range i is d_src[d_ext[i] .. d_ext[i+1]) (d_ext non-decreasing,

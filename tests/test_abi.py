@@ -167,17 +167,17 @@ def test_host_xxh3_matches_xxhash():
         assert _lib.xxh3_64(b) == xxhash.xxh3_64_intdigest(b), n
 
 
-def _build_c_example(out_dir) -> str:
-    """Compiles examples/c_abi_decode.c (plain C11 against include/tpz_gpu.h + the HIP runtime)."""
+def _build_c_example(out_dir, name: str = "c_abi_decode") -> str:
+    """Compiles examples/<name>.c (plain C11 against include/tpz_gpu.h + the HIP runtime)."""
     import shutil
     import subprocess
     if not shutil.which("gcc") or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
         pytest.skip("gcc or the HIP runtime headers are absent")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = os.path.join(str(out_dir), "c_abi_decode")
+    exe = os.path.join(str(out_dir), name)
     subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
                     "-I", os.path.join(root, "include"), "-I", "/opt/rocm/include",
-                    os.path.join(root, "examples", "c_abi_decode.c"), "-o", exe,
+                    os.path.join(root, "examples", name + ".c"), "-o", exe,
                     "-L", os.path.join(root, "topazdb_amd"), "-ltpz_gpu", "-L", "/opt/rocm/lib",
                     "-lamdhip64", "-Wl,-rpath," + os.path.join(root, "topazdb_amd"),
                     "-Wl,-rpath,/opt/rocm/lib"], check=True)
@@ -188,6 +188,7 @@ def test_c_example_compiles_against_the_header(tmp_path):
     """The ABI is consumable from plain C (what a cgo/Rust/JNI binding sees): the example links
     against libtpz_gpu.so with gcc, no C++ and no torch types."""
     assert os.path.exists(_build_c_example(tmp_path))
+    assert os.path.exists(_build_c_example(tmp_path, "c_host_decode"))
 
 
 def test_unaligned_src_is_rejected():

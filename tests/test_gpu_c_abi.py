@@ -15,3 +15,16 @@ def test_c_program_decodes_and_verifies(tmp_path):
     r = subprocess.run([exe, "30000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("ok ") and r.stdout.split()[2] == "30000"
+
+
+@pytest.mark.parametrize("chunk,pinned", [(37, 0), (1000, 1), (65536, 0)])
+def test_c_host_pipeline(tmp_path, chunk, pinned):
+    """tpz_decode_blocks_host from plain C (examples/c_host_decode.c): blocks in host memory
+    through the library's H2D -> decode -> D2H pipeline, several chunks per call, pageable or
+    pinned buffers; every status/CRC/key/value checked, including a corrupted block and a
+    spilled block's record."""
+    exe = _build_c_example(tmp_path, "c_host_decode")
+    r = subprocess.run([exe, "30000", str(chunk), str(pinned)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok ") and r.stdout.split()[2] == "30000"

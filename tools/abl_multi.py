@@ -27,7 +27,8 @@ from bench import make_shard  # noqa: E402
 from topazdb_amd import _lib  # noqa: E402
 from topazdb_amd.batch import DeviceBatch, SlottedColumns  # noqa: E402
 
-PHASES = ["wait+stage", "issue next", "parse", "copy", "crc", "status+loop"]
+PHASES = ["wait+stage", "issue next", "parse", "copy", "copy+crc steps", "status+loop",
+          "crc combine+compare"]
 
 
 def load(name: str):
@@ -103,7 +104,7 @@ def main():
             nw = 256 * 16
             buf = np.zeros(nw * 8, np.uint64)
             assert L.tpz_debug_stamps(buf.ctypes.data, nw) == 0
-            per = buf.reshape(nw, 8)[:, :6].astype(np.float64).sum(0)
+            per = buf.reshape(nw, 8)[:, :7].astype(np.float64).sum(0)
             out["phase_share"] = {p: round(float(x / per.sum()), 4) for p, x in zip(PHASES, per)}
             out["cycles_per_block_per_wave"] = round(float(per.sum() / batch.n_blocks), 1)
         print(json.dumps(out), flush=True)

@@ -50,6 +50,14 @@ class Table(C.Structure):
                 ("d_spill_off", C.c_void_p)]
 
 
+class HostColumns(C.Structure):
+    """tpz_host_columns: tpz_decode_blocks_host's outputs in host memory."""
+    _fields_ = [("h_data", C.c_void_p), ("h_ends", C.c_void_p), ("ends_cap", C.c_uint64),
+                ("h_first", C.c_void_p), ("h_count", C.c_void_p), ("h_status", C.c_void_p),
+                ("h_crc", C.c_void_p), ("h_spill", C.c_void_p), ("spill_cap", C.c_uint64),
+                ("h_spill_off", C.c_void_p), ("h_spill_used", C.c_void_p)]
+
+
 _lib = None
 
 
@@ -101,6 +109,9 @@ def lib() -> C.CDLL:
         L.tpz_pack_ends.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
                                     C.c_void_p, C.c_void_p, C.c_void_p]
         L.tpz_pack_ends.restype = C.c_int
+        L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.POINTER(HostColumns), C.c_uint32]
+        L.tpz_decode_blocks_host.restype = C.c_int
         L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
         L.tpz_host_xxh3_64.restype = C.c_uint64
         L.tpz_layout_spill_stream.argtypes = [C.c_uint64]
@@ -188,6 +199,16 @@ class Context:
         c = Columns(*[cols[f] for f in COLUMN_FIELDS])
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")
+
+    def decode_host_ptrs(self, h_src: int, h_ext: int, n_blocks: int, cols: HostColumns,
+                         chunk_blocks: int = 0) -> int:
+        """tpz_decode_blocks_host (blocks in host memory; H2D, decode, D2H inside the library).
+        Returns the tpz_err (SUCCESS, or ERR_NOMEM when ends/spill capacity was short)."""
+        rc = lib().tpz_decode_blocks_host(self.handle, C.c_void_p(h_src), C.c_void_p(h_ext),
+                                          n_blocks, C.byref(cols), chunk_blocks)
+        if rc not in (SUCCESS, ERR_NOMEM):
+            check(rc, "tpz_decode_blocks_host")
+        return rc
 
     def decompressed_sizes_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
                                 d_size: int, stream: int = 0) -> None:

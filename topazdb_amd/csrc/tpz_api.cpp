@@ -183,6 +183,9 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
 
 }  // namespace
 
+int tpz_internal_device(tpz_ctx* c) { return c->device; }
+tpz_err tpz_internal_hip_fail(hipError_t e, const char* what) { return hip_fail(e, what); }
+
 extern "C" {
 
 uint64_t tpz_layout_slot_base(uint64_t ext_i, uint64_t i) { return tpz_slot_base(ext_i, i); }

@@ -165,7 +165,19 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
 // ------------------------------------------------------------------ CRC-32 (table driven)
 // tab = kNumCrcTables x 256 u32 in LDS. T_k[b] = R0(b || 0^k): raw CRC (init 0, no xorout).
 // ids 0..15: T_0..T_15 (slice-by-16); ids 16+4j+i: T_{n_j-1-i}, n_j = kCrcShiftBytes[j].
+#if defined(TPZ_ABL_NOCF)
+// diagnostic (timing only, wrong CRCs): the same lookups, made bank-conflict-free
+__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
+  return tab[id * 256 + ((byte & 0x20u) | (threadIdx.x & 31u))];
+}
+#elif defined(TPZ_ABL_LUTVALU)
+// diagnostic (timing only, wrong CRCs): no LDS lookup, one VALU op in its place
+__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
+  return __builtin_amdgcn_alignbyte(byte, byte ^ (u32)id, 1);
+}
+#else
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
+#endif
 
 // a ^ b ^ c in one v_bitop3_b32.
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -210,6 +222,28 @@ __device__ __forceinline__ u32 gf_mul(u32 a, u32 b) {
     b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
   }
   return p;
+}
+
+// a * b mod P with a per-lane multiplier a (bit 31 = x^0): 5 VALU per bit, no tables.
+__device__ __forceinline__ u32 gf_mul_lane(u32 a, u32 b) {
+  u32 p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    const u32 m = (u32)((int)(a << i) >> 31);            // all ones iff a holds x^i
+    p ^= b & m;
+    b = (b >> 1) ^ (0xEDB88320u & (u32)(-(int)(b & 1u)));
+  }
+  return p;
+}
+
+// XOR of x over the wave (uniform result): DPP row shifts, then the four row totals.
+__device__ __forceinline__ u32 wave_xor(u32 x) {
+  x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + 1, 0xF, 0xF, true);
+  x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + 2, 0xF, 0xF, true);
+  x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + 4, 0xF, 0xF, true);
+  x ^= (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + 8, 0xF, 0xF, true);
+  return __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 16) ^
+         __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
 }
 
 // shift_n(A) = R_A(0^n) = XOR_i T_{n-1-i}[byte_i(A)], n = kCrcShiftBytes[J].
@@ -382,7 +416,7 @@ __device__ __forceinline__ u32 lanes_below(u64 mask) {
 constexpr int kStampWaves = 256 * kWavesPerWG;
 __device__ u64 g_stamps[2 * kStampWaves * 8];   // wave kernel, then the big kernel
 struct Stamps {
-  u64 t[6] = {0, 0, 0, 0, 0, 0};
+  u64 t[7] = {0, 0, 0, 0, 0, 0, 0};
   u64 last = 0;
 };
 __device__ __forceinline__ u64 stamp_now() {
@@ -433,6 +467,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)0x7FFFFFF0, 0x00020000);
 }
 __device__ __forceinline__ void put_meta(const Out& o, u32 b, u32 st, u32 n, u32 crc) {
+#ifdef TPZ_ABL_NOMETA
+  asm volatile("" ::"v"(st), "v"(n), "v"(crc));   // timing build only: no per-block meta stores
+  return;
+#endif
   const bool l0 = lane_id() == 0;
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)st, whole_rsrc(o.status), l0 ? b : kOob, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32(n, whole_rsrc(o.count), l0 ? 4 * b : kOob, 0, 0);
@@ -629,7 +667,8 @@ __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, cons
 template <class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
-                                              const uint8_t* win, int pb, u32 Pa) {
+                                              const uint8_t* win, int pb, u32 Pa, u32 kshift,
+                                              Stamps& St) {
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
@@ -652,7 +691,14 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   cw[4] = carry;
   crc_step(tab, win, pb, L, 4);
   if (nw > 4) carry = copy_fast(src, col, map, F, 4u, carry, rare);
+  TPZ_STAMP(St, 4);
+#ifdef TPZ_GF_COMBINE
+  // lane l's run ends 80 l bytes before the end: shift it there with one GF(2) multiply by
+  // x^(640 l) mod P (a per-lane constant), then XOR the lanes
+  const u32 R = wave_xor(gf_mul_lane(kshift, L.c));
+#else
   const u32 R = crc_combine(tab, L.c);
+#endif
   if (rare) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rewrite lands after the fast stores
     for (u32 w = 0; w < nw; w++)
@@ -666,7 +712,7 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
 template <class Col, class MapT, int kMapLen, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
-                                             const Out& o, Stamps& S) {
+                                             const Out& o, u32 kshift, Stamps& S) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
@@ -754,10 +800,12 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         knz_all = __builtin_popcountll(kmask);
       }
       const u32 vs = (ktot + 15) & ~15u;  // value stream start (tpz_value_start)
+#ifndef TPZ_ABL_NOENDS
       __builtin_amdgcn_raw_buffer_store_b64(
           __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
                              act ? make_uint2(ki, vi) : make_uint2(0, 0)),
           whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
+#endif
       if (act && slots_fit) {
         // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
         // after the segment's end (ends beyond the map only occur in blocks that spill)
@@ -827,10 +875,15 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     u32 R;
     if (!BIG && fuse)
       R = copy_crc_fused(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb, P + k);
+                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb, P + k,
+                         kshift, S);
     else
       R = wave_crc(tab, win, pb, P + k);
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+#if defined(TPZ_ABL_NOCF) || defined(TPZ_ABL_LUTVALU)
+    asm volatile("" ::"v"(R));   // keep the CRC work, report a match (timing builds only)
+    crc = stored;
+#endif
 #endif
   } else {
     u32 c = 0xFFFFFFFFu;
@@ -844,7 +897,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     st = TPZ_BLOCK_CHECKSUM_MISMATCH;
     cnt = 0;
   }
-  TPZ_STAMP(S, 4);
+  TPZ_STAMP(S, 6);
   put_meta(o, b, st, cnt, crc);
 }
 
@@ -892,6 +945,7 @@ struct Params {
   const u32* crc_tables;
   Out out;
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
+  u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
 };
 
 // ------------------------------------------------------------------ wave path kernel
@@ -903,6 +957,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
+  const u32 kshift = p.lane_shift[lane];
   uint8_t* slot = lds + kTableBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
@@ -952,9 +1007,12 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     const u64 e16 = (e + 15) & ~(u64)15;
     const u64 lim = p.src_bytes < e16 ? p.src_bytes : e16;
     __amdgpu_buffer_rsrc_t rs = window_rsrc(p.src, lim, ws);
+    // all five loads unconditionally: the descriptor drops the pieces past the block (no
+    // traffic), and the loads issue back to back with no branch between them (measured 2.3 %
+    // faster than loading only the block's rounds, profiles/r2/ablations.jsonl)
 #pragma unroll
     for (int r = 0; r < kWinRounds; r++)
-      if ((u32)r < rounds) v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
+      v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
     if (e + 16 > p.src_bytes) {
 #pragma unroll
       for (int r = 0; r < kWinRounds; r++)
@@ -992,7 +1050,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     TPZ_STAMP(S, 1);
     if (fits) {
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bcur, s, p.out, S);
+                                                           len64, bcur, s, p.out, kshift, S);
     } else if (len64 > kBigMaxLen) {
       defer_to(p.out.spill_list, p.out.spill_count, bcur);
     } else {
@@ -1004,7 +1062,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kWavesPerWG + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
-    for (int k = 0; k < 6; k++) g_stamps[gw * 8 + k] = S.t[k];
+    for (int k = 0; k < 7; k++) g_stamps[gw * 8 + k] = S.t[k];
 #endif
 }
 
@@ -1389,6 +1447,21 @@ static const u32* big_super_shifts() {
   return xp.v;
 }
 
+// x^(8 * 80 l) mod P (reflected), l < 64: lane l's CRC run ends 80 l bytes before the range end.
+static const u32* lane_run_shifts() {
+  static const struct Ls {
+    u32 v[64];
+    Ls() {
+      u32 x = 0x80000000u;
+      for (int l = 0; l < 64; l++) {
+        v[l] = x;
+        for (int i = 0; i < 8 * kCrcLaneBytes; i++) x = (x >> 1) ^ ((x & 1u) ? 0xEDB88320u : 0u);
+      }
+    }
+  } ls;
+  return ls.v;
+}
+
 void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   Params p;
   p.src = a.src;
@@ -1402,6 +1475,8 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
               a.spill_list, a.spill_count};
   const u32* xp = big_super_shifts();
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
+  const u32* ls = lane_run_shifts();
+  for (int l = 0; l < 64; l++) p.lane_shift[l] = ls[l];
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;

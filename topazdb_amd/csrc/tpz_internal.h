@@ -6,6 +6,10 @@
 
 #include "../../include/tpz_gpu.h"
 
+// Context accessors for the host pipeline (tpz_host_pipeline.cpp; defined in tpz_api.cpp).
+int tpz_internal_device(tpz_ctx* c);
+tpz_err tpz_internal_hip_fail(hipError_t e, const char* what);
+
 namespace tpz {
 
 // CRC-32 lookup tables of the block decode, uploaded once per context (tpz_api.cpp):
@@ -150,6 +154,9 @@ struct PackLaunch {
   uint32_t* dense;
 };
 void launch_pack_ends(const PackLaunch& a, hipStream_t stream);
+// first[i] = exclusive prefix of count over decoded (OK / OK_SPILLED) blocks, first[n] = total.
+void launch_count_prefix(const uint32_t* count, const uint8_t* status, uint32_t n,
+                         uint64_t* first, hipStream_t stream);
 
 struct CodecLaunch {
   const uint8_t* src;

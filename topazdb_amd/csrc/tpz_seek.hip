@@ -194,7 +194,38 @@ __global__ __launch_bounds__(256) void pack_ends_kernel(PackLaunch a, uint2* den
   }
 }
 
+// first[i] = sum of count[j] for j < i over the decoded blocks (OK / OK_SPILLED), i <= n: one
+// 1024-thread workgroup, each thread a contiguous run (the host pipeline's chunks are <= 2^20).
+__global__ __launch_bounds__(1024) void count_prefix_kernel(const u32* count, const uint8_t* status,
+                                                            u32 n, u64* first) {
+  __shared__ u64 part[1024];
+  const u32 t = threadIdx.x, per = (n + 1023) / 1024;
+  const u32 lo = min(n, t * per), hi = min(n, lo + per);
+  u64 s = 0;
+  for (u32 i = lo; i < hi; i++)
+    s += (status[i] == TPZ_BLOCK_OK || status[i] == TPZ_BLOCK_OK_SPILLED) ? count[i] : 0u;
+  part[t] = s;
+  __syncthreads();
+  for (u32 o = 1; o < 1024; o <<= 1) {          // Hillis-Steele inclusive scan of the parts
+    const u64 v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  u64 run = t ? part[t - 1] : 0;
+  for (u32 i = lo; i < hi; i++) {
+    first[i] = run;
+    run += (status[i] == TPZ_BLOCK_OK || status[i] == TPZ_BLOCK_OK_SPILLED) ? count[i] : 0u;
+  }
+  if (t == 1023) first[n] = part[1023];
+}
+
 }  // namespace
+
+void launch_count_prefix(const u32* count, const uint8_t* status, u32 n, u64* first,
+                         hipStream_t stream) {
+  hipLaunchKernelGGL(count_prefix_kernel, dim3(1), dim3(1024), 0, stream, count, status, n, first);
+}
 
 void launch_pack_ends(const PackLaunch& a, hipStream_t stream) {
   u32 grid = (a.n_blocks + 3) / 4;
