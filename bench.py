@@ -153,6 +153,59 @@ def write_sst_files(src, ext, gen, n_ent, dirpath, blocks_per_sst, max_files):
     return paths
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """The host threads the CPU baseline may use: this process's affinity, capped by the job's
+    CPU share where the launcher states one (OMP_NUM_THREADS; 16 per GPU on the GPU box, whose
+    nproc counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share and share.isdigit() else n
+
+
+def ref_dataset_baseline(target_s: float = 1.0) -> dict:
+    """benches/sstable_iter_read.rs:60-79 on its own dataset (1000 pairs key_{i*5:03} /
+    value_{i:010}, LsmOptions::default block size 4096) with each of its three codecs: the C
+    port's create_and_read pass (pread per block, codec, CRC, per-entry copies) on one thread,
+    us per pass. The reference quotes 40.36 us (codec ambiguous)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    keys, kpos, vals, vpos = synth.reference_bench_entries(1000)
+    src, ext = synth.build_blocks(keys, kpos, vals, vpos, 4096)
+    n_ent = np.array([int(src[int(ext[b])]) << 8 | int(src[int(ext[b]) + 1])
+                      for b in range(len(ext) - 1)], np.int64)
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="tpz_ref_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        for name, enc in (("uncompress", None), ("snappy", synth.snappy_blocks),
+                          ("lz4", synth.lz4_blocks)):
+            s2, e2 = (src, ext) if enc is None else enc(src, ext)
+            d = os.path.join(tmp, name)
+            os.mkdir(d)
+            paths = write_sst_files(s2, e2, (keys, kpos, vals, vpos), n_ent, d, len(n_ent), 1)
+            dt1, _, _ = O.bench_iter_read(paths, 1, 100)
+            iters = max(100, int(target_s / max(dt1 / 100, 1e-7)))
+            dt, by, en = O.bench_iter_read(paths, 1, iters)
+            assert en == 1000, (name, en)
+            out[name] = {"us_per_pass": round(dt / iters * 1e6, 3), "block_bytes": int(by),
+                         "blocks": len(n_ent), "passes": iters}
+            for q in paths:
+                os.unlink(q)
+            os.rmdir(d)
+    finally:
+        os.rmdir(tmp)
+    return out
+
+
 def cpu_baseline(src, ext, gen, n_ent, threads, target_s=12.0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
@@ -174,7 +227,9 @@ def cpu_baseline(src, ext, gen, n_ent, threads, target_s=12.0):
             "sample": f"{len(paths)} SST files x {per_sst} blocks (64 MiB each, 4k config), "
                       f"{iters} pass(es), one file per thread, {dt:.1f} s; "
                       f"single-thread {single:.3f} GiB/s",
-            "value_1core": round(single, 3)}
+            "value_1core": round(single, 3), "cpu_model": cpu_model(),
+            "nproc": os.cpu_count(), "threads_note": "threads = the job's CPU share "
+            "(process affinity capped by OMP_NUM_THREADS); nproc counts the whole host"}
 
 
 # ------------------------------------------------------------------ H2D/D2H-inclusive
@@ -380,14 +435,19 @@ def seek_rate(ctx, batch: DeviceBatch, cols: SlottedColumns, config: str, dev,
             "mqueries_s": round(n_q / ms / 1e3, 1)}
 
 
-def codec_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, codec: str = "snappy",
-               nb: int = 1 << 18, steps: int = 10) -> dict:
-    """The same blocks with the Snappy codec (topazdb's default, src/opt.rs:48) or the Lz4 one:
-    device codec step (tpz_decompress_blocks, compress.rs:104-111) + tpz_decode_blocks per step,
-    inputs resident. Checks that the decompressed batch equals the Uncompress one. Not the
-    metric; DESIGN.md §4."""
+_CODEC_REGION = {}
+
+
+def codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, steps: int = 10) -> dict:
+    """2^18 blocks of the compressible "4kc" shape (synth.py; ~0.66 compressed/uncompressed)
+    with the Snappy codec (topazdb's default, src/opt.rs:48) or the Lz4 one: the device codec
+    step (tpz_decompress_blocks, compress.rs:104-111) + tpz_decode_blocks per step, inputs
+    resident. Checks that the decompressed batch equals the Uncompress one. Not the metric;
+    DESIGN.md §4."""
     from topazdb_amd.batch import decompress_batch
-    nb = min(nb, len(ext) - 1)
+    if nb not in _CODEC_REGION:
+        _CODEC_REGION[nb] = synth.make_region("4kc", nb)
+    src, ext = _CODEC_REGION[nb]
     raw = src[:int(ext[nb])]
     enc = synth.snappy_blocks if codec == "snappy" else synth.lz4_blocks
     s2, e2 = enc(raw, ext[:nb + 1])
@@ -424,7 +484,9 @@ def codec_rate(ctx, src: np.ndarray, ext: np.ndarray, dev, codec: str = "snappy"
     ms_codec = ev[0].elapsed_time(ev[1]) / steps
     ms_dec = ev[1].elapsed_time(ev[2]) / steps
     t = (ms_codec + ms_dec) * 1e-3
-    return {"blocks": nb, "compressed_bytes": int(e2[-1]), "uncompressed_bytes": int(ext[nb]),
+    return {"blocks": nb, "data": "4kc (compressible 4k shape, synth.py)",
+            "compressed_bytes": int(e2[-1]), "uncompressed_bytes": int(ext[nb]),
+            "ratio": round(int(e2[-1]) / int(ext[nb]), 3),
             "ms_codec": round(ms_codec, 4), "ms_decode": round(ms_dec, 4),
             "gib_s_compressed_input": round(int(e2[-1]) / t / GIB, 1),
             "gib_s_uncompressed": round(int(ext[nb]) / t / GIB, 1)}
@@ -672,19 +734,22 @@ def main():
     snappy = lz4 = None
     if side and not args.no_snappy:
         try:
-            snappy = codec_rate(ctx, src, ext, dev, "snappy")
+            snappy = codec_rate(ctx, dev, "snappy")
         except Exception as ex:  # reported, never the metric
             log(rank, f"snappy measurement failed: {ex}")
     if side and not args.no_lz4:
         try:
-            lz4 = codec_rate(ctx, src, ext, dev, "lz4")
+            lz4 = codec_rate(ctx, dev, "lz4")
         except Exception as ex:  # reported, never the metric
             log(rank, f"lz4 measurement failed: {ex}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(src, ext, gen, n_ent, threads)
+        cpu = cpu_baseline(src, ext, gen, n_ent, cpu_threads())
+        try:
+            cpu["reference_bench_dataset"] = ref_dataset_baseline()
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"reference-dataset baseline failed: {ex}")
 
     ceiling = None
     try:   # last: the copy overwrites the decoded columns

@@ -494,11 +494,36 @@ static uint64_t iter_read_pass(const sstfile* s, volatile uint64_t* sink, uint64
     uint8_t* raw = (uint8_t*)malloc(len ? len : 1);
     if (pread(s->fd, raw, len, (off_t)s->ext[b]) != (ssize_t)len) { free(raw); return ents; }
     by += len;
-    if (len == 0 || raw[len - 1] != 1 || len < 5) { free(raw); continue; }
-    uint8_t* data = (uint8_t*)malloc(len - 1);
-    memcpy(data, raw, len - 1);
+    if (len == 0) { free(raw); continue; }
+    /* compress::decode (compress.rs:95-113): the codec's output buffer (one decode pass, as
+     * snap / LZ4_decompress_safe do), or the BytesMut copy of an Uncompress payload */
+    const uint8_t tag = raw[len - 1];
+    uint8_t* data = NULL;
+    size_t dlen = 0;
+    if (tag == 1) {
+      dlen = len - 1;
+      data = (uint8_t*)malloc(dlen ? dlen : 1);
+      memcpy(data, raw, dlen);
+    } else if (tag == 2) {
+      uint64_t want = 0, got = 0;
+      if (tpzo_snappy_uncompressed_len(raw, len - 1, &want) == 0) {
+        data = (uint8_t*)malloc(want ? want : 1);
+        if (tpzo_snappy_decompress(raw, len - 1, data, want, &got) != 0) { free(data); data = NULL; }
+        dlen = got;
+      }
+    } else if (tag == 3) {
+      int64_t size = 0;
+      if (tpzo_lz4_prefixed_size(raw, len - 1, &size) == 0) {
+        data = (uint8_t*)malloc(size ? (size_t)size : 1);
+        const int64_t r = tpzo_lz4_decompress_safe(raw + 4, (int64_t)len - 5, data, size);
+        if (r < 0) { free(data); data = NULL; }
+        dlen = r < 0 ? 0 : (size_t)r;
+      }
+    }
     free(raw);
-    size_t plen = len - 5;
+    if (!data) continue;
+    if (dlen < 4) { free(data); continue; }
+    size_t plen = dlen - 4;
     if (tpzo_crc32_fast(data, plen) != be32(data + plen) || plen < 2) { free(data); continue; }
     uint32_t n = be16(data);
     if (plen < 2 + 2 * (size_t)n) { free(data); continue; }

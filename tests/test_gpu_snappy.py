@@ -128,3 +128,31 @@ def test_past_the_window_sizes(ctx):
         assert s_ == _lib.BLOCK_OK and o == O.snappy_decompress(b[:-1]) + b"\x01"
     s2, e2 = batch_of(blocks)
     assert_parity(ctx, s2, e2)
+
+
+def test_periodic_and_overlapping_copies(ctx):
+    """Streams full of copies that overlap their own output: periods 1..80 (the one-block-per-lane
+    kernel's register path for offsets < 16, its step split for 16 <= offset < 64, and the
+    stored-line path for longer ones), at every output alignment, in batches whose blocks start
+    at every offset of the output buffer's lines."""
+    rng = np.random.default_rng(11)
+    blocks = []
+    for period in range(1, 81):
+        for mode in (0, 1, 2):
+            unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+            pre = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+            body = pre + unit * (int(rng.integers(300, 3000)) // period + 1)
+            blocks.append(O.snappy_compress(body, mode) + b"\x02")
+    # the compressible 4kc shape, and tiny blocks (outputs shorter than a line)
+    src, ext = synth.make_region("4kc", 64)
+    blocks += [O.snappy_block(src[int(ext[i]):int(ext[i + 1])].tobytes(), i % 3) for i in range(64)]
+    blocks += [O.snappy_compress(bytes(rng.integers(0, 4, k, dtype=np.uint8)), 0) + b"\x02"
+               for k in range(1, 40)]
+    order = rng.permutation(len(blocks))
+    blocks = [blocks[i] for i in order]
+    outs, st = device_codec(ctx, blocks)
+    for i, b in enumerate(blocks):
+        ost, ob = O.decompress_block(b)
+        assert st[i] == ost, i
+        if ost == O.OK:
+            assert outs[i] == ob, i

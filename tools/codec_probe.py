@@ -48,9 +48,14 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 18)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lz4"])
+    ap.add_argument("--data", default="4kc", choices=["4kc", "4k"])
     a = ap.parse_args()
 
-    src, ext, _, _, _, _ = make_shard("4k", a.blocks, 0)
+    if a.data == "4k":
+        src, ext, _, _, _, _ = make_shard("4k", a.blocks, 0)
+    else:
+        src, ext = synth.make_region("4kc", a.blocks)
+    raw = torch.from_numpy(src[:int(ext[a.blocks])].copy()).cuda()
     enc = synth.snappy_blocks if a.codec == "snappy" else synth.lz4_blocks
     s2, e2 = enc(src[:int(ext[a.blocks])], ext[:a.blocks + 1])
     batch = DeviceBatch(s2, e2)
@@ -83,12 +88,24 @@ def main():
         ev[1].record(stream)
         torch.cuda.synchronize()
         ms = ev[0].elapsed_time(ev[1]) / a.steps
-        line = {"variant": name, "ms": round(ms, 4), "ok": int((st == 0).sum())}
+        line = {"variant": name, "ms": round(ms, 4), "ok": int((st == 0).sum()),
+                "equals_uncompressed": bool(torch.equal(dst, raw)), "data": a.data,
+                "ratio": round(batch.src_bytes / raw.numel(), 3)}
         if ref is None:
             ref = dst.clone()
         else:
             line["same_bytes"] = bool(torch.equal(ref, dst))
         if name == "cstamps":
+            L.tpz_debug_lane_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+            lb = (C.c_ulonglong * 8)()
+            L.tpz_debug_lane_stamps(lb, 0)
+            lv = list(lb)
+            waves = max(lv[1], 1)
+            line["lane"] = {"cycles_per_wave": round(lv[0] / waves),
+                            "elements_per_block": round((lv[2] + lv[5]) / max(nb * (a.steps + 1), 1), 2),
+                            "wave_trips": round(lv[3] / waves, 1),
+                            "stored_source_trips": round(lv[4] / waves, 1),
+                            "cycles_per_trip": round(lv[0] / max(lv[3], 1), 1)}
             L.tpz_debug_codec_stamps(buf, 0)
             v = list(buf)
             tot = sum(v[:6])

@@ -876,6 +876,549 @@ __global__ __launch_bounds__(kWave * kGroupWaves) void snappy_group_kernel(Codec
   }
 }
 
+// ------------------------------------------------------------------ snappy, one block per lane
+// The wave-per-block element loop runs its ~70 wave-uniform instructions once per element per
+// block. Here every lane walks its own block's element chain straight from HBM to HBM, so each
+// header decode and copy instruction serves 64 blocks at once; the lanes diverge only in which
+// copy path an element takes and for how many 16-byte pieces. The output is written in 16-byte
+// pieces at the element's (unaligned) position: a piece that runs past the element holds bytes
+// that later elements overwrite (the lane's stores land in program order), and no store passes the
+// block's `want` bytes, so neighbouring blocks are never touched. Back-references read the lane's
+// own earlier output (single-thread read-after-write through memory).
+typedef unsigned __int128 u128;
+
+__device__ __forceinline__ u128 ld16u(const uint8_t* p) {    // unaligned 16-byte load
+  u128 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16u(uint8_t* p, u128 v) { __builtin_memcpy(p, &v, 16); }
+
+// 16 bytes at base[a ..] of a buffer of size >= 16 bytes: the load is clamped inside the buffer
+// and the bytes past its end read as zero (branch-free, so the waits on a lane's loads stay exact)
+__device__ __forceinline__ u128 ld16c(const uint8_t* base, u64 size, u64 a) {
+  const u64 ac = a + 16 <= size ? a : size - 16;
+  const u128 v = ld16u(base + ac);
+  const u64 sh = a - ac;
+  return sh == 0 ? v : (sh >= 16 ? (u128)0 : v >> (8 * sh));
+}
+
+// Stores whose piece does not belong to the block go here instead (never read).
+__device__ u128 g_store_sink[1024];
+__device__ __forceinline__ uint8_t* sink_for_lane() {
+  return reinterpret_cast<uint8_t*>(&g_store_sink[threadIdx.x & 1023]);
+}
+
+// The last bytes of a block: out[k .. room) = the low bytes of v, exact width (no byte past it)
+__device__ __noinline__ void put_tail(uint8_t* o, u64 k, u128 v, u64 room) {
+  const u32 r = (u32)(room - k);
+  uint8_t* q = o + k;
+  if (r & 8) { const u64 w = (u64)v; __builtin_memcpy(q, &w, 8); q += 8; v >>= 64; }
+  if (r & 4) { const u32 w = (u32)v; __builtin_memcpy(q, &w, 4); q += 4; v >>= 32; }
+  if (r & 2) { const uint16_t w = (uint16_t)v; __builtin_memcpy(q, &w, 2); q += 2; v >>= 16; }
+  if (r & 1) *q = (uint8_t)v;
+}
+
+// Up to four pieces k0 + 16 j (j < 4, k0 + 16 j < len) of an element at o: whole pieces inside
+// the block's room are stored (bytes past the element are rewritten by later elements), a piece
+// past the room goes to the sink and its in-room bytes are stored exactly afterwards.
+__device__ __forceinline__ void put4(uint8_t* o, u64 k0, const u128 (&v)[4], u64 len, u64 room) {
+  uint8_t* sink = sink_for_lane();
+  bool tail = false;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const u64 k = k0 + 16 * j;
+    const bool whole = k + 16 <= room;
+    tail |= !whole && k < len;
+    st16u(whole ? o + k : sink, v[j]);
+  }
+  if (tail) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const u64 k = k0 + 16 * j;
+      if (k + 16 > room && k < len) put_tail(o, k, v[j], room);
+    }
+  }
+}
+
+// The 16 bytes p[(r + i) mod off], i < 16, of the sequence with period off (< 16) whose first
+// off bytes are pat's low bytes: the period rotated by r, then doubled in registers.
+__device__ __forceinline__ u128 periodic16(u128 pat, u32 off, u32 r) {
+  const u128 lo = pat >> (8 * r), hi = pat & (((u128)1 << (8 * r)) - 1);
+  u128 v = (lo & (((u128)1 << (8 * (off - r))) - 1)) | (hi << (8 * (off - r)));
+  for (u32 L = off; L < 16; L *= 2) v |= v << (8 * L);
+  return v;
+}
+
+// A lane's element copies. The pieces of a copy are loaded together and then stored together,
+// branch-free: a lane's loads and stores complete in order (one vmcnt), so any load issued after a
+// store also waits for it; grouping keeps that to about one wait per element instead of one per
+// piece. `pos` is the absolute output position in dst, `room` the block's bytes from there.
+// out[pos .. pos + len) = src[q .. q + len)
+__device__ __forceinline__ void lane_lit(const uint8_t* src, u64 src_bytes, u64 q, uint8_t* dst,
+                                         u64 pos, u64 len, u64 room) {
+  u128 v[4];
+  for (u64 k = 0; k < len; k += 64) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = ld16c(src, src_bytes, q + k + 16 * j);
+    put4(dst + pos, k, v, len, room);
+  }
+}
+
+// out[pos .. pos + len) repeats the bytes `off` back (0 = zeros, LZ4's offset-0 match)
+__device__ __forceinline__ void lane_match(uint8_t* dst, u64 dst_bytes, u64 pos, u64 off, u64 len,
+                                           u64 room) {
+  u128 v[4];
+  uint8_t* o = dst + pos;
+  if (off == 0 || off >= len || off >= 64) {
+    // the source of every 64-byte round ends before it: final bytes (earlier rounds included)
+    for (u64 k = 0; k < len; k += 64) {
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        v[j] = off == 0 ? (u128)0
+                        : ld16c(dst, dst_bytes, pos - off + k + (k + 16 * j < len ? 16 * j : 0));
+      put4(o, k, v, len, room);
+    }
+  } else if (off < 16) {
+    // period off: every piece from the off bytes before pos, in registers
+    const u64 a = pos >= 16 ? pos - 16 : 0;
+    const u128 w = ld16u(dst + a);
+    const u128 pat = w >> (8 * (pos - a - off));
+    const u32 o32 = (u32)off, s16 = 16u % o32;
+    u32 r = 0;
+    for (u64 k = 0; k < len; k += 64) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        v[j] = periodic16(pat, o32, r);
+        r += s16;
+        r = r >= o32 ? r - o32 : r;
+      }
+      put4(o, k, v, len, room);
+    }
+  } else {
+    // 16 <= off < len, off < 64: piece k reads piece k - off of this copy
+    for (u64 k = 0; k < len; k += 16) {
+      const u128 t = ld16u(o + k - off);
+      if (k + 16 <= room) st16u(o + k, t);
+      else put_tail(o, k, t, room);
+    }
+  }
+}
+
+#ifdef TPZ_CODEC_STAMPS
+// lane kernel diagnostics: [0] wave cycles, [1] waves, [2] elements (all lanes), [3] wave loop
+// trips, [4] literal rounds, [5] match rounds
+__device__ unsigned long long g_lstamps[8];
+#define LCOUNT(v) (v)++
+#else
+#define LCOUNT(v) (void)0
+#endif
+
+__device__ bool snappy_lane(const uint8_t* src, u64 src_bytes, u64 s, u64 n, u64 ip,
+                            uint8_t* dst, u64 dst_bytes, u64 D0, u64 want, u32& elems) {
+  u64 d = 0;
+  u128 hv = ld16c(src, src_bytes, s + ip);
+  while (ip < n) {
+    // the tag and the 4 bytes after it (bytes past the block are don't-care: the checks below
+    // reject any element that needs them)
+    const u64 h = (u64)hv;
+    const u32 tag = (u32)h & 0xFF, kind = tag & 3, t6 = tag >> 2;
+    const u32 x = (u32)(h >> 8);
+    u64 len, off = 0, hl;
+    if (kind == 0) {
+      const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
+      len = (u64)(nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1))) + 1;
+      hl = 1 + nb;
+    } else {
+      len = kind == 1 ? 4 + (t6 & 7) : t6 + 1;
+      hl = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+      off = kind == 1 ? (((tag >> 5) << 8) | (x & 0xFF)) : (kind == 2 ? (x & 0xFFFF) : x);
+    }
+    const u64 next = ip + hl + (kind == 0 ? len : 0);
+    // snap's Err: output overrun, element past the input, copy offset 0 or before the output
+    if (d + len > want || next > n || (kind != 0 && (off == 0 || off > d))) return false;
+    hv = ld16c(src, src_bytes, s + next);                    // the next header, in flight now
+    LCOUNT(elems);
+    if (kind == 0) lane_lit(src, src_bytes, s + ip + hl, dst, D0 + d, len, want - d);
+    else lane_match(dst, dst_bytes, D0 + d, off, len, want - d);
+    ip = next;
+    d += len;
+  }
+  return d == want;
+}
+
+// LZ4 through lz4_walk, one block per lane: input bytes from a 16-byte register window that is
+// reloaded when the walk leaves it; copies as above.
+struct Lz4LaneSrc {
+  const uint8_t* src;
+  u64 src_bytes, base;          // in[0] is src[base]
+  mutable u64 cpos;
+  mutable u128 cv;
+  __device__ u32 byte(int64_t i) const {
+    const u64 a = base + (u64)i;
+    if (a - cpos >= 16) {
+      cpos = a;
+      cv = ld16c(src, src_bytes, a);
+    }
+    return (u32)(cv >> (8 * (a - cpos))) & 0xFFu;
+  }
+};
+struct Lz4LaneOut {
+  const uint8_t* src;
+  u64 src_bytes, ibase;         // in[0] is src[ibase]
+  uint8_t* dst;
+  u64 dst_bytes, D0, r;         // the block's output: dst[D0 .. D0 + r)
+  __device__ void lit(int64_t op, int64_t ip, int64_t len) const {
+    lane_lit(src, src_bytes, ibase + (u64)ip, dst, D0 + (u64)op, (u64)len, r - (u64)op);
+  }
+  __device__ void match(int64_t op, int64_t off, int64_t len) const {
+    lane_match(dst, dst_bytes, D0 + (u64)op, (u64)off, (u64)len, r - (u64)op);
+  }
+};
+
+__device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u32& elems);
+
+// One thread per block. Takes the snappy and LZ4 blocks whose decoded length agrees with the sizes
+// pass; every other block, and any block whose stream turns out invalid, gets status 0xFF and is
+// left to codec_wave_kernel (which runs next, skips the rest and reports the codec's Err exactly).
+__global__ __launch_bounds__(256) void codec_lane_kernel(CodecParams p) {
+  const u32 b = blockIdx.x * 256 + threadIdx.x;
+  u32 elems = 0;
+#if defined(TPZ_CODEC_STAMPS) && defined(TPZ_CODEC_LANE_SNAPPY)
+  const u64 t0 = __builtin_amdgcn_s_memtime();
+  codec_lane_block(p, b, elems);
+  const u64 t1 = __builtin_amdgcn_s_memtime();
+  u32 mx = 0;
+  for (int l = 0; l < 64; l++) mx = max(mx, (u32)__builtin_amdgcn_readlane(elems, l));
+  atomicAdd(&g_lstamps[2], (unsigned long long)elems);
+  if (lane_id() == 0) {
+    atomicAdd(&g_lstamps[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&g_lstamps[1], 1ull);
+    atomicAdd(&g_lstamps[3], (unsigned long long)mx);
+  }
+#else
+  codec_lane_block(p, b, elems);
+#endif
+}
+
+__device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u32& elems) {
+  if (b >= p.n_blocks) return;
+#ifndef TPZ_CODEC_LANE_SNAPPY
+  if (p.status[b] != kLeftForWaveKernel) return;              // decoded by snappy_ring_kernel
+#endif
+  const u64 s = p.ext[b], e = p.ext[b + 1], len = e - s;
+  const u64 D0 = p.dst_ext[b], dn = p.dst_ext[b + 1] - D0;
+  const u32 tag = len ? p.src[e - 1] : 0u;
+  const u64 dst_bytes = p.dst_ext[p.n_blocks];
+  // (tiny batches, errors, empty outputs and other tags: the wave kernel)
+#ifdef TPZ_CODEC_LANE_SNAPPY
+  bool ok = len > 1 && (tag == 2 || tag == 3) && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16;
+#else
+  bool ok = len > 1 && tag == 3 && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16;
+  if (!ok) return;                                            // status stays 0xFF
+#endif
+  if (ok && tag == 2) {
+    u64 want = 0;
+    const u32 h = snappy_header(p.src + s, len - 1, want);
+    ok = h != 0 && want + 1 == dn &&
+         snappy_lane(p.src, p.src_bytes, s, len - 1, h, p.dst, dst_bytes, D0, want, elems);
+  } else if (ok) {
+    const int64_t size = lz4_prefix(p.src + s, len - 1);
+    ok = size >= 0;
+    if (ok) {
+      Lz4LaneSrc in{p.src, p.src_bytes, s + 4, ~0ull, 0};
+      const int64_t r = lz4_walk(in, (int64_t)len - 5,
+                                 Lz4LaneOut{p.src, p.src_bytes, s + 4, p.dst, dst_bytes, D0, dn - 1},
+                                 size);
+      ok = r >= 0 && (u64)r + 1 == dn;
+    }
+  }
+  if (ok) p.dst[D0 + dn - 1] = 1;                              // re-tagged Uncompress
+  p.status[b] = ok ? (uint8_t)TPZ_BLOCK_OK : kLeftForWaveKernel;
+}
+
+// ------------------------------------------------------------------ snappy, one block per lane, LDS ring
+// Per-lane 16-byte stores to 64 different blocks run at ~1 TB/s on this chip, while a wave whose
+// lanes cover whole lines in groups (4 lanes per 64-byte line) stores at 3.6-4.8 TB/s
+// (tools/ubench_lane.hip). So each lane decodes its block into a 256-byte ring in LDS (4 lines of
+// 64 bytes at the output's absolute alignment) and, after every step, the wave stores the lines
+// its lanes completed cooperatively: 16 lines per store instruction. The line a block shares with
+// its neighbour at either end is stored by its own lane with exact-width stores.
+// The ring is written in aligned 16-byte slots only: a step's bytes are funnelled into slots in
+// registers (the slot holding the output frontier is kept in a register too, so no slot is read
+// back before it is rewritten); unaligned reads are two aligned slot reads and a funnel. So no
+// write passes the frontier's slot, and two lines (128 bytes per lane, 16 waves per CU) hold
+// the current line and the previous one intact at every step.
+// A step produces at most 64 bytes of one element per lane. Copy sources come from the ring when
+// they lie in the current or the previous line, otherwise from the lines already stored: those
+// loads wait for the wave's earlier stores (vmcnt) and bypass L1 (device scope), so they see the
+// stored bytes.
+constexpr u32 kRingWG = 256;                                 // blocks (threads) per workgroup
+constexpr u32 kRing = 128, kRingLine = 64, kRingStep = 64;
+static_assert(kRingWG * kRing + (kRingWG / kWave) * kWave * 12 <= 81920, "ring LDS");
+
+__device__ __forceinline__ u128 lds16(const uint8_t* q) {
+  return *reinterpret_cast<const u128*>(q);                  // aligned
+}
+__device__ __forceinline__ void lds16w(uint8_t* q, u128 v) { *reinterpret_cast<u128*>(q) = v; }
+__device__ __forceinline__ u128 lowbytes(u128 v, u32 m) {    // the low m (< 16) bytes of v
+  return v & (((u128)1 << (8 * m)) - 1);
+}
+
+// The 16 ring bytes at absolute address a (R[a % kRing ..], any alignment).
+__device__ __forceinline__ u128 ring_read(const uint8_t* R, u64 a) {
+  const u32 o = (u32)a & (kRing - 1), m = o & 15, o0 = o & ~15u;
+  const u128 s0 = lds16(R + o0), s1 = lds16(R + ((o0 + 16) & (kRing - 1)));
+  return m ? (s0 >> (8 * m)) | (s1 << (8 * (16 - m))) : s0;
+}
+
+// Writes the step's output bytes [P, P + c) (c <= 64; v[j] = bytes [P + 16 j, P + 16 j + 16))
+// into the ring's aligned slots. acc holds the slot containing P (its bytes below P are the
+// output); on return it holds the slot containing P + c.
+__device__ __forceinline__ void ring_emit(uint8_t* R, u64 P, u32 c, const u128 (&v)[4], u128& acc) {
+  const u32 m = (u32)P & 15, K = (m + c + 15) >> 4, Kn = (m + c) >> 4;
+  const u64 A = P & ~(u64)15;
+  u128 carry = m ? lowbytes(acc, m) : (u128)0, nacc = acc;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const u128 cur = k < 4 ? v[k < 4 ? k : 0] : (u128)0;
+    const u128 slot = m ? carry | (cur << (8 * m)) : cur;
+    if ((u32)k < K) lds16w(R + ((u32)(A + 16 * k) & (kRing - 1)), slot);
+    if ((u32)k == Kn) nacc = slot;
+    carry = m ? cur >> (8 * (16 - m)) : (u128)0;
+  }
+  acc = nacc;
+}
+
+// dst[x0 .. x1) from the ring, exact width (the lines a block shares with its neighbours)
+__device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst, u64 x0, u64 x1) {
+  for (u64 k = 0; x0 + k < x1; k += 16) {
+    const u128 v = ring_read(R, x0 + k);
+    if (x0 + k + 16 <= x1) st16u(dst + x0 + k, v);
+    else put_tail(dst + x0, k, v, x1 - x0);
+  }
+}
+
+__global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t rings[kRingWG * kRing];
+  __shared__ u64 fl_addr[kRingWG / kWave][kWave];
+  __shared__ u32 fl_lane[kRingWG / kWave][kWave];
+  const u32 lane = lane_id(), wid = threadIdx.x >> 6;
+  uint8_t* R = rings + threadIdx.x * kRing;
+  const u32 b = blockIdx.x * kRingWG + threadIdx.x;
+  const u64 dst_bytes = p.dst_ext[p.n_blocks];
+  // buffer descriptors over the whole source and output (batches below 2 GiB: the offsets are
+  // 32-bit); a masked-off piece reads at an out-of-range offset, which returns zeros without a
+  // memory access, so every load is issued branch-free
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      p.dst, (short)0, (int)(dst_bytes < 0x7FFFFFF0ull ? dst_bytes : 0x7FFFFFF0ull), 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.src, (short)0, (int)(p.src_bytes < 0x7FFFFFF0ull ? p.src_bytes : 0x7FFFFFF0ull),
+      0x00020000);
+
+  bool live = false;
+  u64 s = 0, n = 0, ip = 0, want = 0, D0 = 0, dn = 0;
+  if (b < p.n_blocks) {
+    s = p.ext[b];
+    const u64 e = p.ext[b + 1], len = e - s;
+    D0 = p.dst_ext[b];
+    dn = p.dst_ext[b + 1] - D0;
+    const u32 tag = len ? p.src[e - 1] : 0u;
+    live = len > 1 && tag == 2 && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
+           dst_bytes < 0x7FFFFFF0ull && p.src_bytes < 0x7FFFFFF0ull;
+    if (live) {
+      const u32 h = snappy_header(p.src + s, len - 1, want);
+      live = h != 0 && want + 1 == dn;
+      ip = h;
+      n = len - 1;
+    }
+    if (!live) p.status[b] = kLeftForWaveKernel;
+  }
+  u64 d = 0;                                  // bytes produced
+  const u64 head_end = (D0 + kRingLine - 1) & ~(u64)(kRingLine - 1);
+  u64 fl = D0;                                // bytes below fl are stored
+  u128 hv = live ? ld16c(p.src, p.src_bytes, s + ip) : (u128)0;
+  u32 hvv = 16;                               // hv holds the input bytes [ip, ip + hvv)
+  u128 acc = 0;                               // the ring slot holding the frontier D0 + d
+  u32 ek = 0;                                 // element: 0 literal, 1 copy
+  u64 erem = 0, esrc = 0, eoff = 0;
+#ifdef TPZ_CODEC_STAMPS
+  const u64 t0 = __builtin_amdgcn_s_memtime();
+  u64 trips = 0, gtrips = 0, elems = 0;
+#endif
+
+  while (__ballot(live)) {
+#ifdef TPZ_CODEC_STAMPS
+    trips++;
+#endif
+    bool finish = false, fail = false;
+    if (live && erem == 0) {
+      if (ip >= n) {
+        finish = true;
+      } else {
+        const u64 h = (u64)hv;
+        const u32 tag = (u32)h & 0xFF, kind = tag & 3, t6 = tag >> 2;
+        const u32 x = (u32)(h >> 8);
+        u64 len, off = 0, hl;
+        if (kind == 0) {
+          const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
+          len = (u64)(nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1))) + 1;
+          hl = 1 + nb;
+        } else {
+          len = kind == 1 ? 4 + (t6 & 7) : t6 + 1;
+          hl = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+          off = kind == 1 ? (((tag >> 5) << 8) | (x & 0xFF)) : (kind == 2 ? (x & 0xFFFF) : x);
+        }
+        const u64 next = ip + hl + (kind == 0 ? len : 0);
+        // snap's Err: output overrun, element past the input, copy offset 0 or before the output
+        if (d + len > want || next > n || (kind != 0 && (off == 0 || off > d))) {
+          fail = true;
+        } else {
+          ek = kind == 0 ? 0u : 1u;
+          erem = len;
+          esrc = s + ip + hl;
+          eoff = off;
+          ip = next;
+          // the next header: still in hv after a copy or a short literal (a header is at most 5
+          // bytes), else loaded now, in flight while this element is produced (clamped near the
+          // end of the source)
+          const u32 used = (u32)(kind == 0 ? (hl + len < 16 ? hl + len : 16) : hl);
+          hv = used < 16 ? hv >> (8 * used) : (u128)0;
+          hvv = hvv > used ? hvv - used : 0u;
+          if (hvv < 5) {
+            hv = s + next + 16 <= p.src_bytes
+                     ? __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(srs, (u32)(s + next), 0, 0))
+                     : ld16c(p.src, p.src_bytes, s + next);
+            hvv = 16;
+          }
+#ifdef TPZ_CODEC_STAMPS
+          elems++;
+#endif
+        }
+      }
+    }
+    // produce up to kRingStep bytes of the current element (a copy with off >= 16: at most off,
+    // so every source byte precedes the step)
+    const bool prod = live && !finish && !fail && erem > 0;
+    const u64 P = D0 + d;
+    u64 c = prod ? (erem < kRingStep ? erem : (u64)kRingStep) : 0;
+    if (prod && ek == 1 && eoff >= 16 && eoff < c) c = eoff;
+    const u64 Pl = P & ~(u64)(kRingLine - 1);
+    const u64 ring_lo = Pl >= kRingLine ? Pl - kRingLine : 0;        // previous line: intact
+    const bool gcopy = prod && ek == 1 && eoff >= 16 && P - eoff < ring_lo;
+    if (__ballot(gcopy)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stored lines landed
+#ifdef TPZ_CODEC_STAMPS
+      gtrips++;
+#endif
+    }
+    if (prod) {
+      u128 v[4];
+      if (ek == 0) {
+        // the pieces the step needs (a piece straddling the source's end: clamped, below)
+        const bool tail = esrc + kRingStep + 16 > p.src_bytes;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          v[j] = __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(
+                                              srs, (16 * j < c && !tail) ? (u32)(esrc + 16 * j) : 0x80000000u,
+                                              0, 0));
+        if (tail)
+#pragma unroll
+          for (int j = 0; j < 4; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
+        esrc += c;
+      } else if (eoff < 16) {
+        // period off: every piece from the off bytes before P (in the ring), in registers
+        const u128 pat = ring_read(R, P - 16) >> (8 * (16 - eoff));
+        const u32 o32 = (u32)eoff, s16 = 16u % o32;
+        u32 r = 0;                       // a snappy copy (<= 64 bytes) takes one step
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          v[j] = periodic16(pat, o32, r);
+          r += s16;
+          r = r >= o32 ? r - o32 : r;
+        }
+      } else {
+        // off >= c: the sources end before P; each piece from stored lines or from the ring
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const u64 a = P - eoff + 16 * j;
+          v[j] = __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(
+                                              drs, (16 * j < c && a < ring_lo) ? (u32)a : 0x80000000u,
+                                              0, 16));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const u64 a = P - eoff + 16 * j;
+          if (16 * j < c && a >= ring_lo) v[j] = ring_read(R, a);
+        }
+      }
+      ring_emit(R, P, (u32)c, v, acc);
+      d += c;
+      erem -= c;
+    }
+    if (fail) {
+      live = false;
+      p.status[b] = kLeftForWaveKernel;
+    }
+    if (finish) {
+      live = false;
+      if (d == want) {
+        // re-tagged Uncompress: the tag byte joins the frontier slot
+        const u64 T = D0 + want;
+        const u32 m = (u32)T & 15;
+        const u128 slot = lowbytes(acc, m) | ((u128)1 << (8 * m));
+        lds16w(R + ((u32)(T & ~(u64)15) & (kRing - 1)), slot);
+        ring_store_exact(R, p.dst, fl, D0 + dn);
+        fl = D0 + dn;
+        p.status[b] = TPZ_BLOCK_OK;
+      } else {
+        p.status[b] = kLeftForWaveKernel;
+      }
+    }
+    // the head line (shared with the previous block) once complete, then whole lines
+    const u64 F = D0 + d;
+    if (live && fl < head_end && F >= head_end) {
+      ring_store_exact(R, p.dst, fl, head_end);
+      fl = head_end;
+    }
+    for (;;) {
+      const bool has = live && fl >= head_end && fl + kRingLine <= F;
+      const u64 mk = __ballot(has);
+      if (mk == 0) break;
+      const u32 cnt = __builtin_popcountll(mk);
+      if (has) {
+        const u32 k = __builtin_amdgcn_mbcnt_hi((u32)(mk >> 32), __builtin_amdgcn_mbcnt_lo((u32)mk, 0u));
+        fl_addr[wid][k] = fl;
+        fl_lane[wid][k] = lane;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (u32 q = 0; q < cnt; q += kWave / 4) {
+        const u32 k = q + (lane >> 2);
+        if (k < cnt) {
+          const u64 a = fl_addr[wid][k];
+          const uint8_t* Rs = rings + (wid * kWave + fl_lane[wid][k]) * kRing;
+          const u32 o = ((u32)a & (kRing - 1)) + 16 * (lane & 3);
+          st16u(p.dst + a + 16 * (lane & 3), lds16(Rs + o));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (has) fl += kRingLine;
+    }
+  }
+#ifdef TPZ_CODEC_STAMPS
+  const u64 t1 = __builtin_amdgcn_s_memtime();
+  atomicAdd(&g_lstamps[5], (unsigned long long)elems);
+  if (lane == 0) {
+    atomicAdd(&g_lstamps[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&g_lstamps[1], 1ull);
+    atomicAdd(&g_lstamps[3], (unsigned long long)trips);
+    atomicAdd(&g_lstamps[4], (unsigned long long)gtrips);
+  }
+#endif
+}
+
 __global__ __launch_bounds__(kWave) void codec_big_kernel(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kGuard + kBigIn + kBigOut];
   const u32 cnt = uni(*p.defer_count);
@@ -907,6 +1450,17 @@ extern "C" int tpz_debug_codec_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+#ifdef TPZ_CODEC_STAMPS
+extern "C" int tpz_debug_lane_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lstamps), sizeof(g_lstamps)) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lstamps), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
 void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream) {
   CodecParams p{};
   p.src = a.src;
@@ -928,7 +1482,7 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
   p.status = a.status;
   p.defer_list = a.defer_list;
   p.defer_count = a.defer_count;
-#ifndef TPZ_CODEC_NO_GROUPS
+#if defined(TPZ_CODEC_GROUPS)
   {
     u32 gg = (a.n_blocks + kGroupBlocks * kGroupWaves - 1) / (kGroupBlocks * kGroupWaves);
     if (gg > a.num_cus) gg = a.num_cus;
@@ -936,6 +1490,15 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
     p.group_pass = 1;
     hipLaunchKernelGGL(snappy_group_kernel<kGroupBlocks>, dim3(gg), dim3(kWave * kGroupWaves), 0,
                        stream, p);
+  }
+#elif !defined(TPZ_CODEC_NO_LANES)
+  if (a.n_blocks) {
+    p.group_pass = 1;
+#ifndef TPZ_CODEC_LANE_SNAPPY
+    hipLaunchKernelGGL(snappy_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),
+                       0, stream, p);
+#endif
+    hipLaunchKernelGGL(codec_lane_kernel, dim3((a.n_blocks + 255) / 256), dim3(256), 0, stream, p);
   }
 #endif
   u32 grid = (a.n_blocks + kSmallWaves - 1) / kSmallWaves;

@@ -8,6 +8,10 @@ Configs (BASELINE.json `configs`):
          -> 34 entries, 4155 B per block
   "64k"  block_size 65536, 32 B keys, 1 KiB values -> 61 entries, 64,789 B per block
   "zipf" block_size 4096,  key length Zipf(s=1.2) over [8, 256] B, 100 B values
+  "4kc"  the 4k shape with compressible values for the codec paths (snappy / lz4): 16 B keys
+         (8 B big-endian counter + 8 splitmix64 bytes), 100 B values = 56 splitmix64 bytes +
+         one of 8 fixed 44-byte text fields (picked by splitmix64), so a block compresses to
+         about 0.6 of its size (the reference's codec tests expect >= 10 %, compress.rs:135-175)
   "ref"  benches/sstable_iter_read.rs dataset: key_{i*5:03} / value_{i:010}, block 4096
 """
 from __future__ import annotations
@@ -22,7 +26,24 @@ CONFIGS = {
     "4k": dict(block_size=4096, klen=16, vlen=100, seed=0x5EED0001),
     "64k": dict(block_size=65536, klen=32, vlen=1024, seed=0x5EED0002),
     "zipf": dict(block_size=4096, klen=None, vlen=100, seed=0x5EED0003),
+    "4kc": dict(block_size=4096, klen=16, vlen=100, seed=0x5EED0004, fields=True),
 }
+
+# 44-byte text fields of the "4kc" values (repeated across entries: what snappy / lz4 find)
+_FIELDS = [(f'"status":"{st}","region":"{rg}","v":{i}').ljust(44).encode()[:44]
+           for i, (st, rg) in enumerate([("active", "eu-west-1"), ("idle", "us-east-2"),
+                                         ("active", "ap-south-1"), ("paused", "eu-north-1"),
+                                         ("active", "us-west-2"), ("closed", "sa-east-1"),
+                                         ("active", "ca-central"), ("idle", "me-south-1")])]
+
+
+def splitmix64(seed: int, n: int) -> np.ndarray:
+    """n outputs of the splitmix64 generator seeded with `seed` (SURVEY.md §8d's value stream)."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
 
 
 def _pool(rng: np.random.Generator, nbytes: int) -> np.ndarray:
@@ -82,6 +103,14 @@ def entries(config: str, n_entries: int, seed: int | None = None):
     vl = np.full(n_entries, cfg["vlen"], np.int64)
     vpos = np.zeros(n_entries + 1, np.uint64)
     np.cumsum(vl, out=vpos[1:])
+    if cfg.get("fields"):
+        seed0 = cfg["seed"] if seed is None else seed
+        r = splitmix64(seed0, 9 * n_entries).reshape(n_entries, 9)
+        keys.reshape(n_entries, 16)[:, 8:] = r[:, 0:1].view(np.uint8).reshape(n_entries, 8)
+        v = np.empty((n_entries, 100), np.uint8)
+        v[:, :56] = r[:, 1:8].copy().view(np.uint8).reshape(n_entries, 56)
+        v[:, 56:] = np.frombuffer(b"".join(_FIELDS), np.uint8).reshape(8, 44)[r[:, 8] % np.uint64(8)]
+        return keys, kpos, v.reshape(-1), vpos
     vals = _fill(pool, int(vpos[-1]), int(rng.integers(0, 1 << 24)))
     return keys, kpos, vals, vpos
 
