@@ -4,6 +4,9 @@
 //   st_al / st_mis   16-byte stores, aligned / misaligned
 //   cp_al / cp_mis   load + store (a lane-wise copy), aligned / misaligned
 //   ld4_al           4-byte loads (aligned)
+//   ld_oob75         buffer loads, 3 of 4 lanes at an out-of-range offset (a masked-off piece)
+//   ld_exec25        the same loads with 3 of 4 lanes switched off by the exec mask
+//   ld_buf           buffer loads, every lane in range
 //   st_line8/4       each group of 8 (4) lanes stores one whole 128-byte (64-byte) line of its
 //                    group's region per instruction (a wave flushing 8 (16) blocks' lines)
 // Prints one JSON line per variant: median ms and lane accesses per ns.
@@ -45,6 +48,15 @@ __global__ __launch_bounds__(256) void k(uint8_t* a, uint8_t* b, uint32_t* sink)
       u128 v;
       __builtin_memcpy(&v, pa + 16 * i, 16);
       __builtin_memcpy(pb + 16 * i, &v, 16);
+    } else if (MODE == 6 || MODE == 7 || MODE == 8) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a, (short)0, 0x7FFFFFF0, 0x00020000);
+      const uint32_t off = (uint32_t)((uint64_t)t * kRegion + 16 * i) & 0x3FFFFFFFu;
+      const bool on = MODE == 8 || (t & 3) == 0;
+      if (MODE == 7) {
+        if (on) acc ^= (uint32_t)__builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      } else {
+        acc ^= (uint32_t)__builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(rs, on ? off : 0x80000000u, 0, 0));
+      }
     } else if (MODE == 4 || MODE == 5) {
       // G lanes per line: region of the group, line i of it; lane's 16-byte piece
       constexpr uint32_t G = MODE == 4 ? 8 : 4;
@@ -87,6 +99,9 @@ int main(int argc, char** argv) {
       else if (v == "cp_mis") k<2, 3><<<g, bl>>>(a, b, s);
       else if (v == "ld4_al") k<3, 0><<<g, bl>>>(a, b, s);
       else if (v == "st_line8") k<4, 0><<<g, bl>>>(a, b, s);
+      else if (v == "ld_oob75") k<6, 0><<<g, bl>>>(a, b, s);
+      else if (v == "ld_exec25") k<7, 0><<<g, bl>>>(a, b, s);
+      else if (v == "ld_buf") k<8, 0><<<g, bl>>>(a, b, s);
       else if (v == "st_line4") k<5, 0><<<g, bl>>>(a, b, s);
     };
     for (int w = 0; w < 2; w++) launch();

@@ -1285,7 +1285,13 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
           const u32 used = (u32)(kind == 0 ? (hl + len < 16 ? hl + len : 16) : hl);
           hv = used < 16 ? hv >> (8 * used) : (u128)0;
           hvv = hvv > used ? hvv - used : 0u;
-          if (hvv < 5) {
+          // a literal whose final step's last piece ends 5..15 bytes past the literal carries the
+          // next header: taken from that piece when the literal completes (hvv = 0 until then)
+          const u32 cf = (u32)(kind == 0 ? (len - 1) % kRingStep + 1 : 0), rf = cf & 15;
+          const bool from_lit = kind == 0 && hvv < 5 && rf >= 1 && rf <= 11 &&
+                                s + next + 5 <= p.src_bytes;
+          if (from_lit) hvv = 0;
+          else if (hvv < 5) {
             hv = s + next + 16 <= p.src_bytes
                      ? __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(srs, (u32)(s + next), 0, 0))
                      : ld16c(p.src, p.src_bytes, s + next);
@@ -1326,6 +1332,13 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
 #pragma unroll
           for (int j = 0; j < 4; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
         esrc += c;
+        if (c == erem && hvv == 0) {
+          // the literal's last piece holds the next header (see the decode above)
+          const u32 r16 = (u32)c & 15, last = ((u32)c - 1) >> 4;
+          const u128 lp = last == 0 ? v[0] : last == 1 ? v[1] : last == 2 ? v[2] : v[3];
+          hv = lp >> (8 * r16);
+          hvv = 16 - r16;
+        }
       } else if (eoff < 16) {
         // period off: every piece from the off bytes before P (in the ring), in registers
         const u128 pat = ring_read(R, P - 16) >> (8 * (16 - eoff));
