@@ -205,8 +205,8 @@ tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* c
  * SsTable::read_block for a whole run of blocks that sit in HOST memory (src/table.rs:154-164;
  * the bytes FileObject::read's pread returns, src/table/file_object.rs:23-27): the library
  * copies the blocks to the device in chunks, decodes them (tpz_decode_blocks), packs the used
- * entry ends (tpz_pack_ends) and copies every output back, with chunk k+1's upload and decode
- * overlapping chunk k's downloads on two streams. Synchronous: returns when every output is in
+ * entry ends (tpz_pack_ends) and copies every output back, on three streams (upload, decode,
+ * download) so that both PCIe directions stay busy. Synchronous: returns when every output is in
  * host memory. The caller's buffers are page-locked for the duration of the call when they are
  * not already (hipHostRegister); pinned buffers (hipHostMalloc) avoid that cost.
  *
@@ -221,7 +221,8 @@ tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* c
  *             blocks' records (the library's device arenas grow as needed)
  * Returns TPZ_ERR_NOMEM when ends_cap or spill_cap is too small: h_first[n] and *h_spill_used
  * then hold the sizes needed (the call can be repeated with larger buffers). chunk_blocks = 0
- * picks the default (65,536 blocks per chunk). */
+ * picks the default (8,192 blocks per chunk: 34 MB of 4 KiB blocks, the fastest of 4K..64K on
+ * MI355X, profiles/r2/e2e_sweep.jsonl). */
 typedef struct {
   uint8_t* h_data;
   uint32_t* h_ends;

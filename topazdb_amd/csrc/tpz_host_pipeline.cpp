@@ -16,11 +16,13 @@
 // [ext[lo], ext[hi]) are uploaded; the decode never reads the bytes of the device buffer before
 // the chunk's first block (the first 16-byte piece is masked, tpz_decode.hip zero_head).
 //
-// Per chunk, in stream order: H2D blocks and extents, decode, the entry prefix
-// (count_prefix_kernel), D2H of the per-block metadata; then the host waits for that metadata
-// (while the other stream runs the next chunk), grows the spill arena and decodes again if it
-// overflowed, and issues the pack of the used ends and the D2H of the slots, the dense ends and
-// the spill records.
+// Three streams and three buffer slots, so that the two copy directions run at once:
+//   up:    H2D of chunk k's blocks and extents (after chunk k-3's downloads freed its slot)
+//   comp:  decode, the entry prefix (count_prefix_kernel), D2H of the per-block metadata;
+//          later, once the host has placed the chunk, tpz_pack_ends
+//   down:  D2H of the slots, the packed ends and the spill records
+// The host waits only for chunk k's metadata (entry total, spill bytes), while chunk k+1 uploads
+// and chunk k-1 downloads; a spill arena that overflowed is grown and the chunk decoded again.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -69,8 +71,11 @@ struct Pin {
 };
 
 struct Slot {
-  hipStream_t s = nullptr;
-  hipEvent_t ev = nullptr;
+  hipEvent_t ev = nullptr;        // metadata landed (comp)
+  hipEvent_t ev_up = nullptr;     // blocks uploaded (up)
+  hipEvent_t ev_pack = nullptr;   // ends packed (comp)
+  hipEvent_t ev_down = nullptr;   // downloads done: the slot is free (down)
+  bool used = false;
   Buf d_src, d_ext, d_data, d_ends, d_count, d_status, d_crc, d_spill, d_spill_off, d_used,
       d_first, d_dense;
   Buf h_ext, h_first, h_count, h_status, h_crc, h_spill_off, h_used;
@@ -81,8 +86,8 @@ struct Slot {
         h_used.host = true;
   }
   ~Slot() {
-    if (ev) (void)hipEventDestroy(ev);
-    if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : {ev, ev_up, ev_pack, ev_down})
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -107,7 +112,7 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   *o->h_spill_used = 0;
   if (n == 0) return TPZ_SUCCESS;
   PIPE_HIP(hipSetDevice(tpz_internal_device(ctx)));
-  const uint32_t cb = chunk_blocks ? chunk_blocks : 65536u;
+  const uint32_t cb = chunk_blocks ? chunk_blocks : 8192u;
   const uint64_t src_bytes = h_ext[n];
 
   // the largest chunk's byte span (from its 384-aligned base)
@@ -122,10 +127,21 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   pin_ends.pin(o->h_ends, o->ends_cap * 4);
   pin_spill.pin(o->h_spill, o->spill_cap);
 
-  Slot slot[2];
+  struct Streams {
+    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+    ~Streams() {
+      for (hipStream_t q : {up, comp, down})
+        if (q) (void)hipStreamDestroy(q);
+    }
+  } st;
+  PIPE_HIP(hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking));
+  PIPE_HIP(hipStreamCreateWithFlags(&st.comp, hipStreamNonBlocking));
+  PIPE_HIP(hipStreamCreateWithFlags(&st.down, hipStreamNonBlocking));
+  constexpr int kSlots = 3;
+  Slot slot[kSlots];
   for (Slot& S : slot) {
-    PIPE_HIP(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking));
-    PIPE_HIP(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    for (hipEvent_t* e : {&S.ev, &S.ev_up, &S.ev_pack, &S.ev_down})
+      PIPE_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     const uint64_t m = std::min<uint64_t>(cb, n);
     PIPE_HIP(S.d_src.ensure(max_span + 16));
     PIPE_HIP(S.d_ext.ensure((m + 1) * 8));
@@ -162,21 +178,30 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     cols.d_spill_off = S.d_spill_off.as<uint64_t>();
     cols.d_spill_used = S.d_used.as<uint64_t>();
     const tpz_batch b{S.d_src.as<uint8_t>(), S.d_ext.as<uint64_t>(), m, span};
-    tpz_err r = tpz_decode_blocks(ctx, &b, &cols, S.s);
+    PIPE_HIP(hipStreamWaitEvent(st.comp, S.ev_up, 0));
+    tpz_err r = tpz_decode_blocks(ctx, &b, &cols, st.comp);
     if (r != TPZ_SUCCESS) return r;
-    tpz::launch_count_prefix(cols.d_count, cols.d_status, m, S.d_first.as<uint64_t>(), S.s);
+    tpz::launch_count_prefix(cols.d_count, cols.d_status, m, S.d_first.as<uint64_t>(), st.comp);
     PIPE_HIP(hipGetLastError());
-    PIPE_HIP(hipMemcpyAsync(S.h_first.p, S.d_first.p, (m + 1) * 8, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipMemcpyAsync(S.h_count.p, S.d_count.p, m * 4, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipMemcpyAsync(S.h_status.p, S.d_status.p, m, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipMemcpyAsync(S.h_crc.p, S.d_crc.p, m * 4, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipMemcpyAsync(S.h_spill_off.p, S.d_spill_off.p, m * 8, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipMemcpyAsync(S.h_used.p, S.d_used.p, 8, hipMemcpyDeviceToHost, S.s));
-    PIPE_HIP(hipEventRecord(S.ev, S.s));
+    PIPE_HIP(hipMemcpyAsync(S.h_first.p, S.d_first.p, (m + 1) * 8, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_count.p, S.d_count.p, m * 4, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_status.p, S.d_status.p, m, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_crc.p, S.d_crc.p, m * 4, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_spill_off.p, S.d_spill_off.p, m * 8, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_used.p, S.d_used.p, 8, hipMemcpyDeviceToHost, st.comp));
+    PIPE_HIP(hipEventRecord(S.ev, st.comp));
     return TPZ_SUCCESS;
   };
 
   auto issue = [&](Slot& S, uint32_t lo) -> tpz_err {
+    if (S.used) {
+      // the slot's previous chunk: its downloads must be done before the upload overwrites the
+      // device buffers (a stream wait), and its extents upload before h_ext is rewritten (long
+      // done; its metadata was consumed by finish())
+      PIPE_HIP(hipStreamWaitEvent(st.up, S.ev_down, 0));
+      PIPE_HIP(hipEventSynchronize(S.ev_up));
+    }
+    S.used = true;
     S.lo = lo;
     S.hi = std::min(n, lo + cb);
     S.base = h_ext[lo] - h_ext[lo] % 384;
@@ -184,9 +209,10 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     for (uint32_t i = S.lo; i <= S.hi; i++) e[i - S.lo] = h_ext[i] - S.base;
     const uint64_t off = h_ext[lo] - S.base;
     PIPE_HIP(hipMemcpyAsync(S.d_src.as<uint8_t>() + off, h_src + h_ext[lo], h_ext[S.hi] - h_ext[lo],
-                            hipMemcpyHostToDevice, S.s));
+                            hipMemcpyHostToDevice, st.up));
     PIPE_HIP(hipMemcpyAsync(S.d_ext.p, S.h_ext.p, (S.hi - S.lo + 1) * 8, hipMemcpyHostToDevice,
-                            S.s));
+                            st.up));
+    PIPE_HIP(hipEventRecord(S.ev_up, st.up));
     return decode_chunk(S);
   };
 
@@ -197,7 +223,7 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     const uint32_t m = S.hi - S.lo;
     uint64_t used = *S.h_used.as<uint64_t>();
     if (used > S.d_spill.n) {                 // the spill arena overflowed: grow, decode again
-      PIPE_HIP(hipStreamSynchronize(S.s));
+      PIPE_HIP(hipStreamSynchronize(st.comp));
       PIPE_HIP(S.d_spill.ensure(used + (used >> 2)));
       tpz_err r = decode_chunk(S);
       if (r != TPZ_SUCCESS) return r;
@@ -211,12 +237,14 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     const uint64_t d0 = tpz_slot_base(h_ext[S.lo] - S.base, 0);
     const uint64_t d1 = tpz_slot_base(span, m);
     const uint64_t h0 = tpz_slot_base(h_ext[S.lo], S.lo);
+    PIPE_HIP(hipStreamWaitEvent(st.down, S.ev, 0));
     PIPE_HIP(hipMemcpyAsync(o->h_data + h0, S.d_data.as<uint8_t>() + d0, d1 - d0,
-                            hipMemcpyDeviceToHost, S.s));
+                            hipMemcpyDeviceToHost, st.down));
     // the used entry ends, packed
     if (2 * (g_first + total) <= o->ends_cap) {
       if (2 * total * 4 > S.d_dense.n) {      // only spilled blocks can exceed the slot bound
-        PIPE_HIP(hipStreamSynchronize(S.s));
+        PIPE_HIP(hipStreamSynchronize(st.comp));
+        PIPE_HIP(hipStreamSynchronize(st.down));
         PIPE_HIP(S.d_dense.ensure(2 * total * 4));
       }
       tpz_columns cols{};
@@ -227,11 +255,13 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       cols.d_spill_off = S.d_spill_off.as<uint64_t>();
       const tpz_batch b{S.d_src.as<uint8_t>(), S.d_ext.as<uint64_t>(), m, span};
       tpz_err r = tpz_pack_ends(ctx, &b, &cols, S.d_first.as<uint64_t>(), S.d_dense.as<uint32_t>(),
-                                S.s);
+                                st.comp);
       if (r != TPZ_SUCCESS) return r;
+      PIPE_HIP(hipEventRecord(S.ev_pack, st.comp));
+      PIPE_HIP(hipStreamWaitEvent(st.down, S.ev_pack, 0));
       if (total)
         PIPE_HIP(hipMemcpyAsync(o->h_ends + 2 * g_first, S.d_dense.p, 2 * total * 4,
-                                hipMemcpyDeviceToHost, S.s));
+                                hipMemcpyDeviceToHost, st.down));
     } else {
       short_ends = true;
     }
@@ -239,41 +269,43 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     if (g_spill + used <= o->spill_cap) {
       if (used)
         PIPE_HIP(hipMemcpyAsync(o->h_spill + g_spill, S.d_spill.p, used, hipMemcpyDeviceToHost,
-                                S.s));
+                                st.down));
     } else {
       short_spill = true;
     }
     // per-block metadata
-    const uint8_t* st = S.h_status.as<uint8_t>();
+    const uint8_t* bst = S.h_status.as<uint8_t>();
     const uint64_t* soff = S.h_spill_off.as<uint64_t>();
     std::memcpy(o->h_count + S.lo, S.h_count.p, m * 4);
     std::memcpy(o->h_status + S.lo, S.h_status.p, m);
     std::memcpy(o->h_crc + S.lo, S.h_crc.p, m * 4);
     for (uint32_t j = 0; j < m; j++) {
       o->h_first[S.lo + j] = g_first + first[j];
-      if (st[j] == TPZ_BLOCK_OK_SPILLED) o->h_spill_off[S.lo + j] = g_spill + soff[j];
+      if (bst[j] == TPZ_BLOCK_OK_SPILLED) o->h_spill_off[S.lo + j] = g_spill + soff[j];
     }
     g_first += total;
     g_spill += used;
     o->h_first[S.hi] = g_first;
     *o->h_spill_used = g_spill;
+    PIPE_HIP(hipEventRecord(S.ev_down, st.down));
     return TPZ_SUCCESS;
   };
 
-  uint32_t k = 0;
-  int pending = -1;
-  for (uint32_t lo = 0; lo < n; lo += cb, k++) {
-    Slot& S = slot[k & 1];
-    tpz_err r = issue(S, lo);
-    if (r != TPZ_SUCCESS) return r;
-    if (pending >= 0) {
-      r = finish(slot[pending]);
+  // chunk k is issued, then chunk k-1 finished: the host waits for k-1's metadata while k
+  // uploads and k-2 downloads
+  const uint32_t n_chunks = (n + cb - 1) / cb;
+  for (uint32_t k = 0; k <= n_chunks; k++) {
+    if (k < n_chunks) {
+      tpz_err r = issue(slot[k % kSlots], k * cb);
       if (r != TPZ_SUCCESS) return r;
     }
-    pending = (int)(k & 1);
+    if (k >= 1) {
+      tpz_err r = finish(slot[(k - 1) % kSlots]);
+      if (r != TPZ_SUCCESS) return r;
+    }
   }
-  tpz_err r = finish(slot[pending]);
-  if (r != TPZ_SUCCESS) return r;
-  for (Slot& S : slot) PIPE_HIP(hipStreamSynchronize(S.s));
+  PIPE_HIP(hipStreamSynchronize(st.up));
+  PIPE_HIP(hipStreamSynchronize(st.comp));
+  PIPE_HIP(hipStreamSynchronize(st.down));
   return (short_ends || short_spill) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
 }
