@@ -107,6 +107,7 @@ def main():
             per = buf.reshape(nw, 8)[:, :7].astype(np.float64).sum(0)
             out["phase_share"] = {p: round(float(x / per.sum()), 4) for p, x in zip(PHASES, per)}
             out["cycles_per_block_per_wave"] = round(float(per.sum() / batch.n_blocks), 1)
+            out["rare_windows_per_block"] = round(float(buf.reshape(nw, 8)[:, 7].sum()) / batch.n_blocks, 4)
         print(json.dumps(out), flush=True)
 
 

@@ -254,6 +254,17 @@ __device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
               tlook(tab, b0 + 2, (a >> 16) & 0xFF)) ^ tlook(tab, b0 + 3, a >> 24);
 }
 
+// Keep the first k bytes of a 16-byte piece and zero the rest (k in 0..16): the stream's last
+// chunk, whose bytes past the stream would otherwise be whatever LDS held (unspecified, but it
+// made the output differ from run to run).
+__device__ __forceinline__ uint4 keep_head(uint4 v, u32 k) {
+  const u64 lo = (u64)v.y << 32 | v.x, hi = (u64)v.w << 32 | v.z;
+  const u64 mlo = k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1);
+  const u64 mhi = k >= 16 ? ~0ull : (k <= 8 ? 0ull : ((1ull << (8 * (k - 8))) - 1));
+  const u64 a = lo & mlo, b = hi & mhi;
+  return make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
+}
+
 // Zero the first k bytes of a 16-byte piece (k in 0..15).
 __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
   const u64 lo = (u64)v.y << 32 | v.x, hi = (u64)v.w << 32 | v.z;
@@ -418,6 +429,7 @@ __device__ u64 g_stamps[2 * kStampWaves * 8];   // wave kernel, then the big ker
 struct Stamps {
   u64 t[7] = {0, 0, 0, 0, 0, 0, 0};
   u64 last = 0;
+  u64 rare = 0;      // copy windows rewritten by copy_window (the fused copy's rare path)
 };
 __device__ __forceinline__ u64 stamp_now() {
   u64 t;
@@ -535,8 +547,9 @@ struct Src16 {
 // One window of the copy (chunks 64 w .. 64 w + 63); returns the carry for the next window.
 template <class Col, class MapT, class S>
 __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const MapT* map, u32 nk,
-                                           u32 nch, u32 npad, uint8_t* dst, u32 map_len, u32 w,
+                                           u32 tot, u32 npad, uint8_t* dst, u32 map_len, u32 w,
                                            u32 carry) {
+  const u32 nch = (tot + 15) >> 4;
   const u32 lane = lane_id();
   const u32 last = nk ? nk - 1 : 0u;
   const u32 c = 64 * w + lane;
@@ -583,7 +596,8 @@ __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const M
       acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
     }
   }
-  // 4. store (pad chunks up to the 128-byte line are zeroed)
+  // 4. store (bytes past the stream and pad chunks up to the 128-byte line are zeroed)
+  if (act && x0 + 16 > tot) acc = keep_head(acc, tot - x0);
   const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
 #ifdef TPZ_ABL_NOSTORE
   asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
@@ -605,7 +619,7 @@ __device__ __forceinline__ void copy_stream(const S& src, const Col& col, const 
   return;
 #endif
   u32 carry = 0;
-  for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, nch, npad, dst, map_len, w, carry);
+  for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, tot, npad, dst, map_len, w, carry);
 }
 
 // ------------------------------------------------------------------ fused copy + CRC (wave path)
@@ -632,7 +646,7 @@ __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int
 }
 
 struct FastWin {
-  u32 nk, nch, npad, last;
+  u32 nk, tot, nch, npad, last;
   __amdgpu_buffer_rsrc_t out;  // the slot, npad * 16 bytes
 };
 
@@ -654,11 +668,53 @@ __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, cons
   const bool cross = act && j + 1 < F.nk && e0 < x0 + 16;
   uint4 acc = src(act ? (int)x0 + d0 : -kGuard);
   const uint4 nx = src(cross ? (int)x0 + d1 : -kGuard);
-  if (__ballot(act && (e0 <= x0 || (cross && e1 < x0 + 16 && j + 2 < F.nk)))) rare |= 1u << w;
+  // a window where a lane needs copy_window's rare path is left to it whole (no store here, so
+  // the two never write the same bytes)
+  const bool rw = __ballot(act && (e0 <= x0 || (cross && e1 < x0 + 16 && j + 2 < F.nk))) != 0;
+  if (rw) rare |= 1u << w;
   if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
+  if (act && x0 + 16 > F.tot) acc = keep_head(acc, F.tot - x0);   // the stream's last chunk
   // an idle lane read the zeroed guard: its pad chunk stores zeros without a select
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
-                                         F.out, x0, 0, 0);
+                                         F.out, rw ? kOob : x0, 0, 0);
+  return carry_out;
+}
+
+// copy_fast for blocks with segments shorter than 16 bytes (the Zipf keys): a chunk may hold
+// three segments, and two segments ending in one chunk may have lost the map race (the map
+// then names the earlier one). Entries j .. j+3 come from two ds_read2_b32; the chunk starts in
+// j or j + 1 and takes up to three segments' bytes. Anything longer (segments under 8 bytes)
+// is left to copy_window.
+template <class S>
+__device__ __forceinline__ u32 copy_fast3(const S& src, const ColSmall& col, const uint16_t* map,
+                                          const FastWin& F, u32 w, u32 carry, u32& rare) {
+  const u32 lane = lane_id();
+  const u32 c = 64 * w + lane;
+  const u32 x0 = 16 * c;
+  const bool act = c < F.nch;
+  u32 j = map[min(c, (u32)kWaveMapLen - 1)];
+  j = max(wave_scan_max(act ? j : 0u), carry);
+  const u32 carry_out = readlane(j, 63);
+  u32 e0, e1, e2, e3;
+  int d0, d1, d2, d3;
+  col.get2(min(j, F.last), e0, d0, e1, d1);
+  col.get2(min(j + 2, F.last), e2, d2, e3, d3);
+  if (act && e0 <= x0) {            // a lost map race: the next entry holds the chunk start
+    j++;
+    e0 = e1, d0 = d1, e1 = e2, d1 = d2, e2 = e3, d2 = d3;
+  }
+  const bool b1 = act && j + 1 < F.nk && e0 < x0 + 16;
+  const bool b2 = b1 && j + 2 < F.nk && e1 < x0 + 16;
+  uint4 acc = src(act ? (int)x0 + d0 : -kGuard);
+  const uint4 n1 = src(b1 ? (int)x0 + d1 : -kGuard);
+  const uint4 n2 = src(b2 ? (int)x0 + d2 : -kGuard);
+  const bool rw = __ballot(act && (e0 <= x0 || (b2 && e2 < x0 + 16 && j + 3 < F.nk))) != 0;
+  if (rw) rare |= 1u << w;
+  if (b1) acc = merge_at(acc, n1, (int)(e0 - x0));
+  if (b2) acc = merge_at(acc, n2, (int)(e1 - x0));
+  if (act && x0 + 16 > F.tot) acc = keep_head(acc, F.tot - x0);   // the stream's last chunk
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
+                                         F.out, rw ? kOob : x0, 0, 0);
   return carry_out;
 }
 
@@ -668,10 +724,11 @@ template <class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const uint8_t* win, int pb, u32 Pa, u32 kshift,
-                                              Stamps& St) {
+                                              bool short_segs, Stamps& St) {
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
+  F.tot = tot;
   F.nch = (tot + 15) >> 4;
   F.npad = (F.nch + 7) & ~7u;
   F.last = nk ? nk - 1 : 0u;
@@ -686,11 +743,14 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   for (int t = 0; t < 4; t++) {
     cw[t] = carry;
     crc_step(tab, win, pb, L, t);
-    carry = copy_fast(src, col, map, F, (u32)t, carry, rare);
+    carry = short_segs ? copy_fast3(src, col, map, F, (u32)t, carry, rare)
+                       : copy_fast(src, col, map, F, (u32)t, carry, rare);
   }
   cw[4] = carry;
   crc_step(tab, win, pb, L, 4);
-  if (nw > 4) carry = copy_fast(src, col, map, F, 4u, carry, rare);
+  if (nw > 4)
+    carry = short_segs ? copy_fast3(src, col, map, F, 4u, carry, rare)
+                       : copy_fast(src, col, map, F, 4u, carry, rare);
   TPZ_STAMP(St, 4);
 #ifdef TPZ_GF_COMBINE
   // lane l's run ends 80 l bytes before the end: shift it there with one GF(2) multiply by
@@ -699,10 +759,12 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
 #else
   const u32 R = crc_combine(tab, L.c);
 #endif
+#ifdef TPZ_ABL_STAMPS
+  St.rare += __builtin_popcount(rare);
+#endif
   if (rare) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rewrite lands after the fast stores
     for (u32 w = 0; w < nw; w++)
-      if (rare & (1u << w)) copy_window(src, col, map, nk, F.nch, F.npad, dst, (u32)kWaveMapLen, w, cw[w]);
+      if (rare & (1u << w)) copy_window(src, col, map, nk, F.tot, F.npad, dst, (u32)kWaveMapLen, w, cw[w]);
   }
   return R;
 }
@@ -735,6 +797,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   // turns out wrong reports CHECKSUM_MISMATCH with count 0; its slot holds unspecified bytes.
   u32 st = TPZ_BLOCK_OK, cnt = n;
   bool fuse = false;           // copy fused with the CRC (wave path)
+  bool f_short = false;        // segments under 16 bytes (copy_fast3)
   u32 f_nk = 0, f_tot = 0;
   uint8_t* f_dst = nullptr;
   if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
@@ -778,7 +841,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       }
     }
     u32 kc = 0, vc = 0, knz = 0, vnz = 0;
-    bool bad = false;
+    bool bad = false, short_segs = false;
     for (u32 g0 = 0; g0 < n; g0 += 64) {
       const u32 i = g0 + lane;
       const bool act = i < n;
@@ -792,6 +855,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         if (!ok) kl = vl = 0;
       }
       bad |= __ballot(act && !ok) != 0;
+      short_segs |= __ballot((kl != 0 && kl < 16) || (vl != 0 && vl < 16)) != 0;
       const u32 ki = wave_scan_incl(kl) + kc;
       const u32 vi = wave_scan_incl(vl) + vc;
       const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
@@ -846,6 +910,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 #if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY) && !defined(TPZ_ABL_NOFUSE)
       if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
         fuse = true;
+        f_short = short_segs;
         f_nk = knz + vnz;
         f_tot = vs + vc;
         f_dst = o.data + slot_base(ext_b, b);
@@ -876,7 +941,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     if (!BIG && fuse)
       R = copy_crc_fused(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                          reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb, P + k,
-                         kshift, S);
+                         kshift, f_short, S);
     else
       R = wave_crc(tab, win, pb, P + k);
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
@@ -1063,6 +1128,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 gw = blockIdx.x * kWavesPerWG + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
     for (int k = 0; k < 7; k++) g_stamps[gw * 8 + k] = S.t[k];
+  if (lane == 0 && gw < (u32)kStampWaves) g_stamps[gw * 8 + 7] = S.rare;
 #endif
 }
 
@@ -1285,7 +1351,7 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     for (u32 j = wid; j < nw; j += kBigWaves) {
       u32 m = lane < j ? wmax[lane] : 0u;
       if (lane + 64 < j) m = max(m, wmax[lane + 64]);
-      copy_window(Src16{win}, col, map, nk, nch, npad, dst, (u32)kBigMapLen, j, wave_max(m));
+      copy_window(Src16{win}, col, map, nk, tot, npad, dst, (u32)kBigMapLen, j, wave_max(m));
     }
     TPZ_STAMP(S, 3);
   }
