@@ -108,6 +108,16 @@ def main():
             out["phase_share"] = {p: round(float(x / per.sum()), 4) for p, x in zip(PHASES, per)}
             out["cycles_per_block_per_wave"] = round(float(per.sum() / batch.n_blocks), 1)
             out["rare_windows_per_block"] = round(float(buf.reshape(nw, 8)[:, 7].sum()) / batch.n_blocks, 4)
+            # the big-block kernel's waves (a second table after the wave kernel's)
+            bb = np.zeros(nw * 8, np.uint64)
+            L.tpz_debug_stamps.argtypes = [C.c_void_p, C.c_int]
+            full2 = np.zeros(2 * nw * 8, np.uint64)
+            assert L.tpz_debug_stamps(full2.ctypes.data, 2 * nw) == 0
+            bb = full2[nw * 8:].reshape(nw, 8)[:, :6].astype(np.float64).sum(0)
+            if bb.sum() > 0:
+                names = ["wait+stage", "parse", "copy map max", "copy", "crc", "status+loop"]
+                out["big_phase_share"] = {p: round(float(x / bb.sum()), 4) for p, x in zip(names, bb)}
+                out["big_cycles_per_block_per_wave"] = round(float(bb.sum() / batch.n_blocks), 1)
         print(json.dumps(out), flush=True)
 
 
