@@ -177,7 +177,8 @@ def long_block(rng, n_small: int, big: int = 65000) -> bytes:
 
 def test_blocks_past_the_lds_window(ctx):
     """Blocks longer than TPZ_LDS_BLOCK_BYTES (Block::decode has no length limit) decode
-    through the spill path, straight from HBM, with the reference's answer: well-formed long
+    through the bigwave kernel (n < 64) or the spill path, straight from HBM, with the
+    reference's answer: well-formed long
     blocks, corrupted ones (CHECKSUM_MISMATCH) and random block_size <= 200000 builder output
     (mostly MALFORMED: the builder's u16 offsets wrap past 64 KiB)."""
     rng = np.random.default_rng(12)
@@ -196,7 +197,12 @@ def test_blocks_past_the_lds_window(ctx):
     lens = np.diff(ext.astype(np.int64))
     g, o = assert_parity(ctx, src, ext)
     big = lens > _lib.LDS_BLOCK_BYTES
-    assert (g.raw_status[big & (o.status == O.OK)] == _lib.BLOCK_OK_SPILLED).all()
+    n_ent = np.array([int(src[int(ext[i])]) << 8 | int(src[int(ext[i]) + 1])
+                      for i in range(len(ext) - 1)])
+    # fewer than 64 entries: the one-wave-per-block kernel (any length); more: the spill path
+    ok_big = big & (o.status == O.OK)
+    assert (g.raw_status[ok_big & (n_ent >= 64)] == _lib.BLOCK_OK_SPILLED).all()
+    assert (g.raw_status[ok_big & (n_ent < 64)] == _lib.BLOCK_OK).all()
     assert (big & (o.status == O.OK)).sum() >= 8 and (big & (o.status == O.CHECKSUM)).any()
     assert (big & (o.status == O.MALFORMED)).any()
 
@@ -289,3 +295,46 @@ def test_concurrent_streams(ctx):
         o = O.decode_batch(np.ascontiguousarray(src, np.uint8), np.asarray(ext, np.uint64))
         np.testing.assert_array_equal(g.status, o.status)
         assert g.vals.tobytes() == o.vals[np.repeat(np.repeat(o.status == O.OK, o.count.astype(np.int64)), o.vlen.astype(np.int64))].tobytes()
+
+
+def test_long_blocks_few_entries(ctx):
+    """Blocks past the wave slot with fewer than 64 entries: one wave per block straight from HBM
+    (tpz_bigwave.hip). Entry shapes that stress its windowed copy (keys of 1..40 B, so several
+    segments meet in one chunk; 1..3 entries, so a chunk's source can start before the block;
+    values up to 60 KiB), corrupted payloads, malformed offsets, repeated offsets (spill path),
+    at every alignment of the batch."""
+    rng = np.random.default_rng(21)
+    blocks = []
+    for t in range(60):
+        n = [1, 2, 3, 7, 20, 40, 63][t % 7]
+        bb = MG.BlockBuilder(1 << 17)
+        budget = int(rng.integers(4400, 60000))
+        for i in range(n):
+            kl = int(rng.integers(1, 41))
+            vl = max(0, budget // n - kl - 4 + int(rng.integers(-30, 30)))
+            bb.add(b"k%05d" % i + rng.bytes(max(0, kl - 6)) if kl > 6 else (b"k%05d" % i)[:kl],
+                   rng.bytes(vl))
+        offs, data = bb.build()
+        if max(offs) >= 65536:
+            continue
+        b = MG.encode_block(offs, data)
+        if len(b) <= 4336:
+            continue
+        if t % 9 == 4:
+            b = bytearray(b)
+            b[int(rng.integers(0, len(b) - 5))] ^= 0x10          # checksum mismatch
+            b = bytes(b)
+        if t % 11 == 5 and n >= 2:
+            b = bytearray(b)                                     # offset 1 := offset 0 (repeat)
+            b[4:6] = b[2:4]
+            p = bytes(b[:-5])
+            b = p + MG.crc32(p).to_bytes(4, "big") + b"\x01"
+        blocks.append(b)
+    assert len(blocks) >= 40
+    for pad in (0, 1, 7, 13):
+        src = np.frombuffer(bytes(range(pad)) + b"".join(blocks), np.uint8)
+        ext = np.zeros(len(blocks) + 1, np.uint64)
+        ext[0] = pad
+        ext[1:] = pad + np.cumsum([len(b) for b in blocks])
+        g, o = assert_parity(ctx, src, ext)
+        assert (o.status == O.OK).sum() >= 25 and (o.status == O.CHECKSUM).any()

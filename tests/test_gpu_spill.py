@@ -185,12 +185,13 @@ def test_large_value_block_every_codec(ctx):
 
 def test_long_blocks_every_codec(ctx):
     """Well-formed blocks past TPZ_LDS_BLOCK_BYTES (and compressed past the codec window) in
-    tags 1, 2 and 3, beside ordinary blocks: codec step from HBM to HBM, then the spill path."""
+    tags 1, 2 and 3, beside ordinary blocks: codec step from HBM to HBM, then the one-wave
+    kernel (7 entries) or the spill path (77 entries)."""
     from test_gpu_decode import long_block
     rng = np.random.default_rng(4)
     blocks = []
     for t in range(2):
-        blk = long_block(rng, 5 + 20 * t, 60000 + 5000 * t)
+        blk = long_block(rng, 5 + 70 * t, 60000 + 5000 * t)
         assert len(blk) > _lib.LDS_BLOCK_BYTES
         blocks += [blk, O.snappy_block(blk, 0), O.lz4_block(blk, 0)]
         small = MG.BlockBuilder(4096)
@@ -198,8 +199,8 @@ def test_long_blocks_every_codec(ctx):
         blocks.append(MG.encode_block(*small.build()))
     src, ext = batch_of(blocks)
     g, o = assert_parity(ctx, src, ext, expect_all_ok=True)
-    assert (g.raw_status[[0, 1, 2, 4, 5, 6]] == _lib.BLOCK_OK_SPILLED).all()
-    assert (g.raw_status[[3, 7]] == _lib.BLOCK_OK).all()
+    assert (g.raw_status[[4, 5, 6]] == _lib.BLOCK_OK_SPILLED).all()
+    assert (g.raw_status[[0, 1, 2, 3, 7]] == _lib.BLOCK_OK).all()
 
 
 def sst_from_blocks(blocks: list[bytes], first_keys: list[bytes]) -> bytes:

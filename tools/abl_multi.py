@@ -118,6 +118,18 @@ def main():
                 names = ["wait+stage", "parse", "copy map max", "copy", "crc", "status+loop"]
                 out["big_phase_share"] = {p: round(float(x / bb.sum()), 4) for p, x in zip(names, bb)}
                 out["big_cycles_per_block_per_wave"] = round(float(bb.sum() / batch.n_blocks), 1)
+        if v == "bwstamps":
+            L, h = libs[v]
+            L.tpz_debug_bw_stamps.argtypes = [C.c_void_p, C.c_int]
+            sb = np.zeros(8, np.uint64)
+            L.tpz_debug_bw_stamps(sb.ctypes.data, 1)
+            run(v, 1)
+            torch.cuda.synchronize()
+            L.tpz_debug_bw_stamps(sb.ctypes.data, 0)
+            names = ["parse", "map+issue", "-", "merge+store", "crc", "other"]
+            tot = float(sb[:6].sum())
+            out["bw_phase_share"] = {n: round(float(sb[i]) / tot, 4) for i, n in enumerate(names)}
+            out["bw_cycles_per_block"] = round(tot / batch.n_blocks, 1)
         print(json.dumps(out), flush=True)
 
 

@@ -117,8 +117,9 @@ std::vector<uint32_t> build_rep_tables(const std::vector<uint32_t>& range) {
 // per-workgroup entry tables and the range-CRC accumulators. Decodes on different streams run
 // concurrently, so each stream has its own; calls on one stream are ordered by the stream.
 struct tpz_workspace {
-  uint32_t* d_defer = nullptr;  // [0] big/codec counter, [1] spill counter, [2, 2 + cap) big or
-                                // codec list, [2 + cap, 2 + 2 cap) spill list
+  uint32_t* d_defer = nullptr;  // [0] big/codec counter, [1] spill counter, [2] bigwave counter,
+                                // [4, 4 + cap) big or codec list, [4 + cap, 4 + 2 cap) spill list,
+                                // [4 + 2 cap, 4 + 3 cap) bigwave list
   uint32_t defer_cap = 0;
   uint64_t* d_big_scratch = nullptr;
   uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
@@ -168,7 +169,7 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
     TPZ_HIP(hipMalloc(&w.d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t)));
   if (!w.d_defer || w.defer_cap < max_blocks) {
     uint32_t* d = nullptr;
-    TPZ_HIP(hipMalloc(&d, (2 * (size_t)max_blocks + 2) * 4));
+    TPZ_HIP(hipMalloc(&d, (3 * (size_t)max_blocks + 4) * 4));
     if (w.d_defer) {
       // an earlier decode on this stream may still be reading the old list
       (void)hipStreamSynchronize((hipStream_t)stream);
@@ -272,7 +273,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
     if (r != TPZ_SUCCESS) return r;
   }
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 8, s));   // both worklist counters
+  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 16, s));  // the three worklist counters
   tpz::LaunchArgs a{};
   a.src = b->d_src;
   a.ext = b->d_ext;
@@ -285,9 +286,12 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.status = o->d_status;
   a.crc = o->d_crc;
   a.defer_count = w->d_defer;
-  a.defer_list = w->d_defer + 2;
+  a.defer_list = w->d_defer + 4;
   a.spill_count = w->d_defer + 1;
-  a.spill_list = w->d_defer + 2 + w->defer_cap;
+  a.spill_list = w->d_defer + 4 + w->defer_cap;
+  a.bw_count = w->d_defer + 2;
+  a.bw_list = w->d_defer + 4 + 2 * (size_t)w->defer_cap;
+  a.rep = c->d_rep_tables;
   a.spill = o->d_spill;
   a.spill_cap = o->d_spill ? o->spill_cap : 0;
   a.spill_off = o->d_spill_off;
@@ -372,7 +376,7 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
   a.dst_ext = d_dst_ext;
   a.status = d_status;
   a.defer_count = w->d_defer;
-  a.defer_list = w->d_defer + 2;
+  a.defer_list = w->d_defer + 4;
   a.num_cus = c->num_cus;
   tpz::launch_decompress(a, s);
   TPZ_HIP(hipGetLastError());

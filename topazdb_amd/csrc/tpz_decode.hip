@@ -462,6 +462,8 @@ struct Out {
   u32* defer_count;
   u32* spill_list;
   u32* spill_count;
+  u32* bw_list;        // long blocks with n < 64: decode_bigwave_kernel (tpz_bigwave.hip)
+  u32* bw_count;
 };
 
 // Lane 0 appends block b to a worklist (the big path's or the spill path's).
@@ -1116,10 +1118,14 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (fits) {
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
                                                            len64, bcur, s, p.out, kshift, S);
-    } else if (len64 > kBigMaxLen) {
-      defer_to(p.out.spill_list, p.out.spill_count, bcur);
     } else {
-      defer_to(p.out.defer_list, p.out.defer_count, bcur);
+      // a long block: one with fewer than 64 entries (the 64 KiB config: 61) goes to the
+      // one-wave-per-block kernel; more entries to the LDS big path, or past its window to the
+      // spill path
+      const u32 nent = uni(((u32)p.src[s] << 8) | p.src[s + 1]);
+      if (nent < 64 && p.out.bw_list) defer_to(p.out.bw_list, p.out.bw_count, bcur);
+      else if (len64 > kBigMaxLen) defer_to(p.out.spill_list, p.out.spill_count, bcur);
+      else defer_to(p.out.defer_list, p.out.defer_count, bcur);
     }
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
@@ -1538,7 +1544,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.big_scratch = a.big_scratch;
   p.spill_used = a.spill_used;
   p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count,
-              a.spill_list, a.spill_count};
+              a.spill_list, a.spill_count, a.bw_list, a.bw_count};
   const u32* xp = big_super_shifts();
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   const u32* ls = lane_run_shifts();
@@ -1547,6 +1553,13 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
+  if (a.bw_list) {
+    // before the big kernel: it may hand a block with 64+ entries to the big list
+    BigWaveLaunch bw{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.bw_count,
+                     a.data, a.ends, a.count, a.status, a.crc, a.spill_list, a.spill_count,
+                     a.defer_list, a.defer_count, a.num_cus};
+    launch_bigwave(bw, stream);
+  }
   hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p);
   SpillLaunch sp{a.src, a.ext, a.src_bytes, a.crc_tables, a.spill_list, a.spill_count, a.spill,
                  a.spill_cap, a.spill_off, a.spill_used, a.count, a.status, a.crc, a.num_cus};

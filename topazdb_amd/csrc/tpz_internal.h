@@ -72,9 +72,34 @@ struct LaunchArgs {
   uint64_t spill_cap;
   uint64_t* spill_off;
   uint64_t* spill_used;   // zeroed before the launch
+  uint32_t* bw_list;      // workspace: n_blocks entries (blocks for the bigwave kernel)
+  uint32_t* bw_count;     // workspace: one u32, zeroed before the launch
+  const uint32_t* rep;    // replicated slice-by-4 tables (the bigwave kernel's CRC)
 };
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
+
+// Long blocks with few entries (tpz_bigwave.hip): one wave per block, straight from HBM.
+struct BigWaveLaunch {
+  const uint8_t* src;
+  const uint64_t* ext;
+  uint64_t src_bytes;
+  const uint32_t* rep;          // replicated slice-by-4 tables
+  const uint32_t* crc_tables;   // the decode tables (small shifts, inverse table)
+  const uint32_t* list;
+  const uint32_t* list_count;
+  uint8_t* data;
+  uint32_t* ends;
+  uint32_t* count;
+  uint8_t* status;
+  uint32_t* crc;
+  uint32_t* spill_list;
+  uint32_t* spill_count;
+  uint32_t* big_list;
+  uint32_t* big_count;
+  uint32_t grid;
+};
+void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream);
 
 // The spill path (tpz_spill.hip): blocks the LDS paths hand over, decoded into the arena.
 struct SpillLaunch {
