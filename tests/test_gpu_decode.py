@@ -338,3 +338,30 @@ def test_long_blocks_few_entries(ctx):
         ext[1:] = pad + np.cumsum([len(b) for b in blocks])
         g, o = assert_parity(ctx, src, ext)
         assert (o.status == O.OK).sum() >= 25 and (o.status == O.CHECKSUM).any()
+
+
+def test_long_blocks_crc_window_edges(ctx):
+    """Long one-entry blocks (the one-wave-per-block kernel) whose payload start lies in the last
+    bytes of the lowest 16 KiB CRC window, so the init-value bytes [s, s + 4) straddle two
+    windows, and whose padded end lands on every alignment of a window boundary; tiny filler
+    blocks between them set each block's start modulo 16."""
+    rng = np.random.default_rng(31)
+    parts, cur = [], 0
+    for m in (1, 2, 4):
+        for pad in (13, 14, 15, 0, 5):
+            for j in range(0, 16, 3):
+                fill = (pad - cur) % 16
+                if fill:
+                    parts.append(bytes([0] * (fill - 1)) + b"\x07")    # BAD_TAG filler
+                    cur += fill
+                P = 16384 * m + 2 - pad + j
+                bb = MG.BlockBuilder(1 << 17)
+                assert bb.add(rng.bytes(16), rng.bytes(P - 24))
+                blk = MG.encode_block(*bb.build())
+                assert len(blk) == P + 5
+                parts.append(blk)
+                cur += len(blk)
+    src = np.frombuffer(b"".join(parts), np.uint8)
+    ext = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+    g, o = assert_parity(ctx, src, ext)
+    assert (o.status == O.OK).sum() == 3 * 5 * 6

@@ -28,6 +28,20 @@
 
 #include "tpz_internal.h"
 
+// copy/CRC pipeline shape (variants: tools/abl_multi.py)
+// (measured on the 64k config, profiles/r2/bw_shapes.log: 16 waves, one group at a time, 4 KiB
+// copy groups and 4 KiB CRC steps 2.16 ms; 12 waves with 6 KiB 2.21; 8 waves with 8 KiB 2.32;
+// two 2 KiB groups in flight 2.50; two 4 KiB groups spill VGPRs)
+#ifndef TPZ_BW_KU
+#define TPZ_BW_KU 4
+#endif
+#ifndef TPZ_BW_STEPRUN
+#define TPZ_BW_STEPRUN 64
+#endif
+#ifndef TPZ_BW_PIPE
+#define TPZ_BW_PIPE 0
+#endif
+
 namespace tpz {
 
 namespace {
@@ -36,13 +50,19 @@ typedef uint32_t u32;
 typedef uint64_t u64;
 
 constexpr int kWave = 64;
-constexpr int kWaves = 16;
+#ifndef TPZ_BW_WAVES
+#define TPZ_BW_WAVES 16
+#endif
+constexpr int kWaves = TPZ_BW_WAVES;              // waves per workgroup (one workgroup per CU)
 constexpr int kThreads = kWave * kWaves;
-constexpr u32 kRun = 128;                         // CRC bytes per lane per window
+constexpr u32 kRun = 128;                         // CRC bytes per lane per window (256: VGPR spills)
 constexpr u32 kCrcWin = kRun * kWave;             // 8 KiB
-constexpr int kSegs = 128;                        // entry-table slots per wave (2 n <= 126)
-constexpr int kU = 4;                             // copy windows in flight per wave
-constexpr int kWaveLds = kSegs * 8 + kU * kWave * 4;   // entry table + kU u32 chunk maps
+constexpr u32 kStepRun = TPZ_BW_STEPRUN;          // fused CRC: bytes per lane per step
+constexpr int kStepPieces = kStepRun / 16;
+constexpr u32 kStep = kStepRun * kWave;           // 4 KiB per step, one step per copy group
+constexpr int kSegs = 128;                        // entry-table slots per wave (2 n <= 126, + 2 sentinels)
+constexpr int kU = TPZ_BW_KU;                     // copy windows per group
+constexpr int kWaveLds = kSegs * 8 + kU * kWave;   // entry table + kU u8 chunk maps
 constexpr int kLdsBytes = kCrcRepWords * 4 + kWaves * kWaveLds;
 static_assert(kLdsBytes <= 163840, "bigwave LDS");
 constexpr u32 kOob = 0x80000000u;
@@ -96,6 +116,14 @@ __device__ __forceinline__ u32 scan_max(u32 x) {
   x = max(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast15, 0xA, 0xF, false));
   x = max(x, (u32)__builtin_amdgcn_update_dpp(0, (int)x, kRowBcast31, 0xC, 0xF, false));
   return x;
+}
+// LDS written by this wave and read back by other lanes of it: the LDS executes one wave's
+// instructions in order, so only the compiler must keep them in order. (A wavefront-scope fence
+// makes the compiler wait for every outstanding global load and store, s_waitcnt vmcnt(0), which
+// drained the copy pipeline at every window group: 3.0 ms vs ... on the 64k config.)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ u32 lanes_below(u64 mask) {
   return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
@@ -152,6 +180,8 @@ struct BWParams {
   u32 lane_shift[64];       // x^(8 * 128 l) mod P
   u32 win_shift;            // x^(8 * 8192) mod P
   u32 half_shift;           // x^(8 * 64) mod P
+  u32 step_lane_shift[64];  // x^(8 * 64 l) mod P (the fused CRC steps' lane runs)
+  u32 step_shift;           // x^(8 * 4096) mod P
 };
 
 __device__ __forceinline__ u32 gtab(const BWParams& p, int id, u32 b) { return p.tab[id * 256 + b]; }
@@ -169,6 +199,16 @@ __device__ __forceinline__ u32 unshift_small(const BWParams& p, u32 r, u32 k) {
 }
 
 __device__ __forceinline__ u32 be16_at(const uint8_t* q) { return ((u32)q[0] << 8) | q[1]; }
+
+// A block's header words: lane l < 33 holds block bytes [4 l, 4 l + 4) (n and up to 63 offsets),
+// lane 62 the four bytes of the stored CRC, lane 63 the last four bytes (the tag on top).
+__device__ __forceinline__ u32 hdr_load(const BWParams& p, u64 s, u64 e) {
+  const u32 lane = lane_id(), len = (u32)(e - s);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.src + s), (short)0, (int)len, 0x00020000);
+  const u32 off = lane < 33 ? 4 * lane : (lane == 62 ? len - 5 : (lane == 63 ? len - 4 : kOob));
+  return (u32)__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+}
 
 __device__ __forceinline__ void put_meta(const BWParams& p, u32 b, u32 st, u32 n, u32 crc) {
   if (lane_id() == 0) {
@@ -192,17 +232,20 @@ __device__ __forceinline__ u32 block_crc(const BWParams& p, const u32* rep, u64 
   u32 acc = 0;
   for (u32 wi = W; wi-- > 0;) {                            // lowest window first
     const u64 wend = Pa - (u64)kCrcWin * wi;
-    const u64 r0 = wend - (u64)kRun * (lane + 1);         // this lane's run [r0, r0 + 128)
-    uint4 v[8];
+    const u64 r0 = wend - (u64)kRun * (lane + 1);         // this lane's run [r0, r0 + kRun)
+    uint4 v[kRun / 16];
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
+    for (int t = 0; t < (int)(kRun / 16); t++) {
       const u64 a = r0 + 16 * t;
       v[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                            rs, (int64_t)a >= (int64_t)base ? (u32)(a - base) : kOob, 0, 0));
     }
-    // keep payload bytes [s, pend) only; complement bytes [s, s + 4) (the init value)
+    // keep payload bytes [s, pend) only; complement bytes [s, s + 4) (the init value): only the
+    // highest window and the windows that start before s + 4 (the lowest, and the next one when
+    // [s, s + 4) crosses into it) hold such pieces
+    if (wi == 0 || (int64_t)(wend - kCrcWin) < (int64_t)(s + 4)) {
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
+    for (int t = 0; t < (int)(kRun / 16); t++) {
       const u64 a = r0 + 16 * t;
       if (a < s + 4 || a + 16 > pend) {
         u64 klo, khi, xlo, xhi;
@@ -214,20 +257,22 @@ __device__ __forceinline__ u32 block_crc(const BWParams& p, const u32* rep, u64 
         v[t] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
       }
     }
+    }
     // two independent chains (the run's halves) halve the lookup latency chain; the first half
     // is shifted past the second with x^(8*64)
     u32 ca = 0, cb = 0;
     const u32 r = lane & 31;
+    constexpr int H = kRun / 32;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
+    for (int t = 0; t < H; t++) {
       ca = slice4(rep, r, ca ^ v[t].x);
-      cb = slice4(rep, r, cb ^ v[t + 4].x);
+      cb = slice4(rep, r, cb ^ v[t + H].x);
       ca = slice4(rep, r, ca ^ v[t].y);
-      cb = slice4(rep, r, cb ^ v[t + 4].y);
+      cb = slice4(rep, r, cb ^ v[t + H].y);
       ca = slice4(rep, r, ca ^ v[t].z);
-      cb = slice4(rep, r, cb ^ v[t + 4].z);
+      cb = slice4(rep, r, cb ^ v[t + H].z);
       ca = slice4(rep, r, ca ^ v[t].w);
-      cb = slice4(rep, r, cb ^ v[t + 4].w);
+      cb = slice4(rep, r, cb ^ v[t + H].w);
     }
     const u32 c = gf_mul(p.half_shift, ca) ^ cb;
     const u32 part = wave_xor(gf_mul(ls, c));
@@ -236,15 +281,18 @@ __device__ __forceinline__ u32 block_crc(const BWParams& p, const u32* rep, u64 
   return acc;
 }
 
-// The 16 block bytes at block offset a (any int: a chunk's bytes are the segment's source
-// shifted by the chunk's start, which can lie up to 15 bytes before the block when a short
-// block's first entry starts near byte 0; those leading bytes read as zero).
-__device__ __forceinline__ uint4 seg_load(__amdgpu_buffer_rsrc_t rs, u32 sa, int a, bool on) {
-  const int c = a < 0 ? 0 : a;
+// The 16 bytes at descriptor offset c (the block starts at sa in the descriptor, 16..31 bytes in
+// unless the block starts within 16 bytes of d_src). A chunk's second piece is its segment's source
+// shifted back by up to 15 bytes, so c < 0 only for a block at the very start of d_src; those
+// leading bytes read as zero (they are masked out by the merge anyway).
+__device__ __forceinline__ uint4 seg_load(__amdgpu_buffer_rsrc_t rs, int c, bool on) {
+#ifdef TPZ_BW_NOLOAD
+  return make_uint4(c, c, on, 7);                     // timing build only
+#endif
   const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rs, on ? sa + (u32)c : kOob, 0, 0));
-  if (a >= 0) return v;
-  const u32 sh = (u32)(-a) * 8;                       // 8..120 bits
+                                                rs, on ? (u32)(c < 0 ? 0 : c) : kOob, 0, 0));
+  if (c >= 0) return v;
+  const u32 sh = (u32)(-c) * 8;                       // 8..120 bits
   u64 lo = (u64)v.y << 32 | v.x, hi = (u64)v.w << 32 | v.z;
   if (sh >= 64) {
     hi = lo << (sh - 64);
@@ -256,10 +304,176 @@ __device__ __forceinline__ uint4 seg_load(__amdgpu_buffer_rsrc_t rs, u32 sa, int
   return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
 }
 
+// bytes [0, k) of a, bytes [k, 16) of b (k in 0..16)
+__device__ __forceinline__ u32 keep_mask(u32 k, u32 d) {
+  const int sel = (int)k - 4 * (int)d;
+  return sel >= 4 ? 0xFFFFFFFFu : (sel <= 0 ? 0u : ~(0xFFFFFFFFu << (8 * sel)));
+}
+__device__ __forceinline__ uint4 merge16(uint4 a, uint4 b, u32 k) {
+  return make_uint4((a.x & keep_mask(k, 0)) | (b.x & ~keep_mask(k, 0)),
+                    (a.y & keep_mask(k, 1)) | (b.y & ~keep_mask(k, 1)),
+                    (a.z & keep_mask(k, 2)) | (b.z & ~keep_mask(k, 2)),
+                    (a.w & keep_mask(k, 3)) | (b.w & ~keep_mask(k, 3)));
+}
+
 struct Seg {
-  u32 end;      // exclusive end in the output stream
-  int delta;    // (offset of its first byte in the block) - (its start in the stream)
+  u32 end;      // exclusive end in the output stream (0xFFFFFFFF: the sentinels past the last)
+  int delta;    // (offset of its first byte in the descriptor) - (its start in the stream)
 };
+
+// One group of kU 1 KiB output windows, mapped and loaded (its merges and stores come later, so
+// the next group's loads are in flight while this group's stores drain).
+struct Group {
+  uint4 a[kU], b[kU];
+  u32 kj[kU];   // bytes of the chunk from a (16: all of it) | the segment after the chunk's
+                // first one << 8 (for chunks that meet 3+ segments)
+  bool more;    // some chunk meets 3+ segments (segments under 16 B)
+};
+
+// Maps windows w0 .. w0 + kU - 1 to segments and issues their loads. m0 = the number of segments
+// ending at or before the group's first chunk start minus 16 (every segment from m0 on ends in or
+// after the group's first chunk slot). Segment k ending at stream byte E marks chunk slot
+// ceil(E / 16) (relative to the group) with k + 1 (an LDS max: two segments ending in one chunk
+// leave the later); a prefix max per window, carried across windows, is then the number of
+// segments ending at or before each chunk's start: the index of the segment holding its first
+// byte. Returns m0 for the next group.
+__device__ __forceinline__ u32 map_group(u32 w0, u32 m0, u32 nseg, const Seg* seg, uint8_t* cmap,
+                                         __amdgpu_buffer_rsrc_t rs, Group& g) {
+  const u32 lane = lane_id();
+#pragma unroll
+  for (int i = 0; i < kU * kWave / 16; i += kWave)
+    if (i + (int)lane < kU * kWave / 16) reinterpret_cast<uint4*>(cmap)[i + lane] = make_uint4(0, 0, 0, 0);
+  wave_lds_sync();
+  for (u32 k0 = m0;; k0 += kWave) {
+    const u32 k = k0 + lane;
+    const u32 E = seg[k < nseg ? k : nseg].end;
+    const u32 rel = k < nseg ? ((E + 15) >> 4) - 64 * w0 : 0xFFFFFFFFu;
+    // segments end in increasing order: of those ending in one slot only the last writes
+    const u32 En = seg[k + 1 < nseg ? k + 1 : nseg].end;
+    const u32 reln = k + 1 < nseg ? ((En + 15) >> 4) - 64 * w0 : 0xFFFFFFFFu;
+    if (rel < 64u * kU && rel != reln) cmap[rel] = (uint8_t)(k + 1);
+    if (k0 + kWave >= nseg || readlane(rel, 63) >= 64u * kU) break;   // wave-uniform
+  }
+  wave_lds_sync();
+  u32 carry = m0;
+  bool more = false;
+#pragma unroll
+  for (int u = 0; u < kU; u++) {
+    const u32 x0 = 1024 * (w0 + u) + 16 * lane;
+    const u32 j = max(scan_max(cmap[u * kWave + lane]), carry);     // <= nseg (< 128)
+    carry = readlane(j, 63);
+    const Seg g0 = seg[j], g1 = seg[j + 1];                         // sentinels past nseg
+    const bool two = g0.end < x0 + 16;
+    more |= two && g1.end < x0 + 16;
+    g.kj[u] = (two ? g0.end - x0 : 16u) | ((j + 1) << 8);
+    g.a[u] = seg_load(rs, (int)x0 + g0.delta, j < nseg);
+    g.b[u] = seg_load(rs, (int)x0 + g1.delta, two);
+  }
+  g.more = __ballot(more) != 0;
+  return carry;
+}
+
+// Merges and stores a mapped group: 64 lanes x 16 B per window, through a descriptor that ends at
+// the slot's last 128-byte line (chunks past it are dropped; bytes past the stream are zero).
+__device__ __forceinline__ void store_group(u32 w0, u32 tot, u32 nseg, const Seg* seg,
+                                            __amdgpu_buffer_rsrc_t rs,
+                                            __amdgpu_buffer_rsrc_t ds, const Group& g) {
+  const u32 lane = lane_id();
+#pragma unroll
+  for (int u = 0; u < kU; u++) {
+    const u32 x0 = 1024 * (w0 + u) + 16 * lane;
+    const u32 kk = g.kj[u] & 0xFFu;
+    uint4 v = merge16(g.a[u], g.b[u], kk);
+    if (g.more) {
+      // chunks meeting 3+ segments (segments under 16 B): the rest one by one
+      u32 jj = g.kj[u] >> 8;
+      u32 e = seg[jj].end;
+      if (kk < 16u) {
+        while (e < x0 + 16 && jj + 1 < nseg) {
+          jj++;
+          const Seg s = seg[jj];
+          v = merge16(v, seg_load(rs, (int)x0 + s.delta, true), e - x0);
+          e = s.end;
+        }
+      }
+    }
+    if (1024 * (w0 + u + 1) > tot)                                  // the stream's end
+      v = merge16(v, make_uint4(0, 0, 0, 0), x0 < tot ? min(tot - x0, 16u) : 0u);
+#ifdef TPZ_BW_NOSTORE
+    if (v.x == 0x9E3779B9u && v.y == 0x12345u)
+#endif
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, v),
+                                           ds, x0, 0, 0);
+  }
+}
+
+// The CRC fused into the copy loop: 4 KiB steps aligned to the payload's padded end Pa, lowest
+// first, one per copy group, so a step reads the source bytes the copy has just read (from L2 or
+// the Infinity Cache instead of HBM). Lane l folds the 64-byte run ending 64 l bytes before the
+// step's end; its raw CRCs are chained across steps per lane (Horner with x^(8*4096)), and the
+// lanes are shifted to Pa and XORed once per block.
+struct FusedCrc {
+  __amdgpu_buffer_rsrc_t rs;   // [base, min(src_bytes, Pa))
+  u64 s, pend, Pa, base;
+  u32 S;                       // steps
+};
+
+__device__ __forceinline__ FusedCrc fused_crc_init(const BWParams& p, u64 s, u32 P) {
+  FusedCrc c;
+  c.s = s;
+  c.pend = s + P;
+  c.Pa = (c.pend + 15) & ~15ull;
+  c.base = s & ~15ull;
+  const u64 lim = (p.src_bytes < c.Pa ? p.src_bytes : c.Pa) - c.base;
+  c.rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.src + c.base), (short)0,
+                                           (int)(lim < 0x7FFFFFF0ull ? lim : 0x7FFFFFF0ull), 0x00020000);
+  c.S = (u32)((c.Pa - c.base + kStep - 1) / kStep);
+  return c;
+}
+
+__device__ __forceinline__ void fused_crc_issue(const FusedCrc& c, u32 i, uint4 (&v)[kStepPieces]) {
+  const u64 wend = c.Pa - (u64)kStep * (c.S - 1 - i);
+  const u64 r0 = wend - (u64)kStepRun * (lane_id() + 1);
+#pragma unroll
+  for (int t = 0; t < kStepPieces; t++) {
+    const u64 a = r0 + 16 * t;
+    v[t] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         c.rs, (int64_t)a >= (int64_t)c.base ? (u32)(a - c.base) : kOob, 0, 0));
+  }
+}
+
+__device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams& p, const u32* rep,
+                                              u32 i, uint4 (&v)[kStepPieces], u32 acc) {
+  const u64 wend = c.Pa - (u64)kStep * (c.S - 1 - i);
+  const u64 r0 = wend - (u64)kStepRun * (lane_id() + 1);
+  // keep payload bytes [s, pend) only; complement [s, s + 4) (the init value): only the top step
+  // and the steps starting before s + 4 hold such pieces
+  if (i + 1 == c.S || (int64_t)(wend - kStep) < (int64_t)(c.s + 4)) {
+#pragma unroll
+    for (int t = 0; t < kStepPieces; t++) {
+      const u64 a = r0 + 16 * t;
+      if (a < c.s + 4 || a + 16 > c.pend) {
+        u64 klo, khi, xlo, xhi;
+        range_mask((int)((int64_t)c.s - (int64_t)a), (int)((int64_t)c.pend - (int64_t)a), klo, khi);
+        range_mask((int)((int64_t)c.s - (int64_t)a), (int)((int64_t)c.s + 4 - (int64_t)a), xlo, xhi);
+        u64 lo = (u64)v[t].y << 32 | v[t].x, hi = (u64)v[t].w << 32 | v[t].z;
+        lo = (lo & klo) ^ xlo;
+        hi = (hi & khi) ^ xhi;
+        v[t] = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
+      }
+    }
+  }
+  const u32 r = lane_id() & 31;
+  u32 x = 0;
+#pragma unroll
+  for (int t = 0; t < kStepPieces; t++) {
+    x = slice4(rep, r, x ^ v[t].x);
+    x = slice4(rep, r, x ^ v[t].y);
+    x = slice4(rep, r, x ^ v[t].z);
+    x = slice4(rep, r, x ^ v[t].w);
+  }
+  return i == 0 ? x : (gf_mul(p.step_shift, acc) ^ x);
+}
 
 __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p) {
   const u32 cnt = uni(*p.list_count);
@@ -271,195 +485,189 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
   __syncthreads();
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
   Seg* seg = reinterpret_cast<Seg*>(lds + kCrcRepWords * 4 + wid * kWaveLds);
-  u32* cmap = reinterpret_cast<u32*>(seg + kSegs);   // kU maps of 64 chunk slots
+  uint8_t* cmap = reinterpret_cast<uint8_t*>(seg + kSegs);   // kU maps of 64 chunk slots
 
 #ifdef TPZ_BW_STAMPS
   u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   BW_T0();
-  for (u32 it = blockIdx.x * kWaves + wid; it < cnt; it += gridDim.x * kWaves) {
+  // Block i's list entry and extents are loaded during block i - 1 (scalar loads), and its
+  // header words (n, the offsets, the stored CRC and the tag) during block i - 1's CRC, so a
+  // block's parse starts with two memory round trips (key, then value lengths) instead of six.
+  const u32 stride = gridDim.x * kWaves;
+  u32 it = blockIdx.x * kWaves + wid;
+  if (it >= cnt) return;
+  u32 b = uni(p.list[it]);
+  u64 s = p.ext[b], e = p.ext[b + 1];
+  u32 hw = hdr_load(p, s, e);
+  u32 bn = uni(p.list[it + stride < cnt ? it + stride : it]);
+  for (; it < cnt; it += stride) {
     BW_ST(5);
-    const u32 b = uni(p.list[it]);
-    const u64 s = p.ext[b], e = p.ext[b + 1];
-    const u32 len = (u32)(e - s);                     // > 4336 (the wave path's limit)
-    const uint8_t* blk = p.src + s;
-    const u32 tag = blk[len - 1];                                              // compress.rs:99
-    if (tag == 0 || tag > 3) { put_meta(p, b, TPZ_BLOCK_BAD_TAG, 0, 0); continue; }  // :44-53
-    if (tag != 1) { put_meta(p, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); continue; }
-    const u32 P = len - 5;
-    const u32 stored = ((u32)blk[P] << 24) | ((u32)blk[P + 1] << 16) | ((u32)blk[P + 2] << 8) |
-                       blk[P + 3];                                             // block.rs:51
-    const u32 n = be16_at(blk);                                                // block.rs:54
-    if (n >= kWave) {                       // (the wave path routes only n < 64 here)
-      if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
-      continue;
-    }
-    u32 st = TPZ_BLOCK_OK, bcnt = n;
-    if (P < 2 + 2 * n) {                                                       // block.rs:54-59
-      st = TPZ_BLOCK_MALFORMED;
-      bcnt = 0;
-    } else {
-      // ---- parse: lane i = entry i (n <= 63)
-      const u32 dbo = 2 + 2 * n, dl = P - 2 - 2 * n;   // entries region, block offsets
-      const bool act = lane < n;
-      u32 off = 0, kl = 0, vl = 0;
-      bool ok = true;
-      if (act) {
-        off = be16_at(blk + 2 + 2 * lane);                                     // iterator.rs:74
-        ok = off + 2 <= dl;
-        if (ok) { kl = be16_at(blk + dbo + off); ok = off + 4 + kl <= dl; }     // :77-81
-        if (ok) { vl = be16_at(blk + dbo + off + 2 + kl); ok = off + 4 + kl + vl <= dl; }
-        if (!ok) kl = vl = 0;
+    const u32 itn2 = it + 2 * stride;
+    const u32 bnn = uni(p.list[itn2 < cnt ? itn2 : it]);
+    const u64 sn = p.ext[bn], en = p.ext[bn + 1];
+    bool hw_issued = false;
+    u32 hwn = 0;
+    auto issue_next_header = [&]() {
+      if (!hw_issued) hwn = hdr_load(p, sn, en);
+      hw_issued = true;
+    };
+    [&]() {
+      const u32 len = (u32)(e - s);                   // > 4336 (the wave path's limit)
+      const uint8_t* blk = p.src + s;
+      const u32 tag = readlane(hw, 63) >> 24;                                  // compress.rs:99
+      if (tag == 0 || tag > 3) { put_meta(p, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; }  // :44-53
+      if (tag != 1) { put_meta(p, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
+      const u32 P = len - 5;
+      const u32 stored = __builtin_bswap32(readlane(hw, 62));                 // block.rs:51
+      const u32 w0 = readlane(hw, 0);
+      const u32 n = ((w0 & 0xFFu) << 8) | ((w0 >> 8) & 0xFFu);                  // block.rs:54
+      if (n >= kWave) {                     // (the wave path routes only n < 64 here)
+        if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
+        return;
       }
-      const bool bad = __ballot(act && !ok) != 0;
-      const u32 ki = scan_incl(kl), vi = scan_incl(vl);
-      const u32 ktot = readlane(ki, 63), vtot = readlane(vi, 63);
-      const u32 vs = (ktot + 15) & ~15u;                                       // tpz_value_start
-      const bool slots_fit = 6u * n <= len;
-      // the {kend, vend} pairs, whole 128-byte lines (pairs past n are zero)
-      uint2* ends_g = reinterpret_cast<uint2*>(p.ends) + entry_base(s, b);
-      if (slots_fit && lane < ((n + 15) & ~15u)) ends_g[lane] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
-      if (bad) {
+      u32 st = TPZ_BLOCK_OK, bcnt = n;
+      // offset i: BE u16 at block byte 2 + 2 i, in header word (2 + 2 i) / 4
+      const u32 q = 2 + 2 * lane;
+      const u32 ow = (u32)__builtin_amdgcn_ds_bpermute((int)((q >> 2) << 2), (int)hw);
+      const u32 osh = (q & 3u) * 8;
+      if (P < 2 + 2 * n) {                                                     // block.rs:54-59
         st = TPZ_BLOCK_MALFORMED;
         bcnt = 0;
-      } else if (!slots_fit || (u64)vs + vtot > (u64)len + 2) {
-        // entries overlap or repeat: the spill path decodes the block (CRC included)
-        if (lane == 0) p.spill_list[atomicAdd(p.spill_count, 1u)] = b;
-        continue;
       } else {
-        BW_ST(0);
-        // ---- entry table: non-empty keys, then non-empty values, in stream order
-        const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
-        const u32 knz = __builtin_popcountll(kmask), nseg = knz + __builtin_popcountll(vmask);
-        if (kl) seg[lanes_below(kmask)] = Seg{ki, (int)(dbo + off + 2) - (int)(ki - kl)};
-        if (vl) seg[knz + lanes_below(vmask)] = Seg{vs + vi, (int)(dbo + off + 4 + kl) - (int)(vs + vi - vl)};
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- copy, 1 KiB windows
-        const u32 tot = vs + vtot, nch = (tot + 15) >> 4, npad = (nch + 7) & ~7u;
-        uint8_t* dst = p.data + slot_base(s, b);
-        const u64 rb = s & ~15ull;                     // the block's bytes through a descriptor
-        const u64 rlim = (p.src_bytes < e + 16 ? p.src_bytes : e + 16) - rb;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(p.src + rb), (short)0, (int)(rlim < 0x7FFFFFF0ull ? rlim : 0x7FFFFFF0ull), 0x00020000);
-        const u32 sa = (u32)(s - rb);                  // block byte 0 in the descriptor
-        // kU windows at a time. Their chunk maps are built together: segment k ending in chunk
-        // slot t = ceil(end / 16) of window u sets map_u[t - 64 w] = max(., k + 1) (an LDS atomic
-        // max: two segments ending in one chunk leave the larger index), then a prefix max per
-        // window names the segment holding each chunk's start; every window's loads are issued
-        // before any is used, so a wave has kU windows of loads in flight.
-        u32 carry = 0;                                 // segments ending at or before w0's start
+        // ---- parse: lane i = entry i (n <= 63)
+        const u32 dbo = 2 + 2 * n, dl = P - 2 - 2 * n;   // entries region, block offsets
+        const bool act = lane < n;
+        u32 off = 0, kl = 0, vl = 0;
+        bool ok = true;
+        if (act) {
+          off = (((ow >> osh) & 0xFFu) << 8) | ((ow >> (osh + 8)) & 0xFFu);    // iterator.rs:74
+          ok = off + 2 <= dl;
+          if (ok) { kl = be16_at(blk + dbo + off); ok = off + 4 + kl <= dl; }   // :77-81
+          if (ok) { vl = be16_at(blk + dbo + off + 2 + kl); ok = off + 4 + kl + vl <= dl; }
+          if (!ok) kl = vl = 0;
+        }
+        const bool bad = __ballot(act && !ok) != 0;
+        const u32 ki = scan_incl(kl), vi = scan_incl(vl);
+        const u32 ktot = readlane(ki, 63), vtot = readlane(vi, 63);
+        const u32 vs = (ktot + 15) & ~15u;                                     // tpz_value_start
+        const bool slots_fit = 6u * n <= len;
+        // the {kend, vend} pairs, whole 128-byte lines (pairs past n are zero)
+        uint2* ends_g = reinterpret_cast<uint2*>(p.ends) + entry_base(s, b);
+        if (slots_fit && lane < ((n + 15) & ~15u)) ends_g[lane] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
+        if (bad) {
+          st = TPZ_BLOCK_MALFORMED;
+          bcnt = 0;
+        } else if (!slots_fit || (u64)vs + vtot > (u64)len + 2) {
+          // entries overlap or repeat: the spill path decodes the block (CRC included)
+          if (lane == 0) p.spill_list[atomicAdd(p.spill_count, 1u)] = b;
+          return;
+        } else {
+          BW_ST(0);
+          // ---- entry table: non-empty keys, then non-empty values, in stream order, then two
+          // sentinels; deltas relative to the copy descriptor, which starts 16..31 bytes before
+          // the block (so a second piece shifted back by up to 15 bytes stays inside it)
+          const u64 rb = (s >= 16 ? s - 16 : 0) & ~15ull;
+          const u64 rlim = (p.src_bytes < e + 16 ? p.src_bytes : e + 16) - rb;
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(p.src + rb), (short)0, (int)(rlim < 0x7FFFFFF0ull ? rlim : 0x7FFFFFF0ull), 0x00020000);
+          const int sa = (int)(s - rb);                // block byte 0 in the descriptor
+          const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
+          const u32 knz = __builtin_popcountll(kmask), nseg = knz + __builtin_popcountll(vmask);
+          if (kl) seg[lanes_below(kmask)] = Seg{ki, sa + (int)(dbo + off + 2) - (int)(ki - kl)};
+          if (vl) seg[knz + lanes_below(vmask)] = Seg{vs + vi, sa + (int)(dbo + off + 4 + kl) - (int)(vs + vi - vl)};
+          if (lane < 2) seg[nseg + lane] = Seg{0xFFFFFFFFu, 0};
+          wave_lds_sync();
+          // ---- copy: groups of kU 1 KiB windows; group g + 1 is mapped and its loads issued
+          // before group g is merged and stored
+          const u32 tot = vs + vtot, npad = (((tot + 15) >> 4) + 7) & ~7u, nwin = (npad + 63) >> 6;
+          const __amdgpu_buffer_rsrc_t ds = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(p.data + slot_base(s, b)), (short)0, (int)(16 * npad), 0x00020000);
 #ifdef TPZ_BW_NOCOPY
-        if (npad) continue;                          // timing build only
+          if (npad) return;                          // timing build only
 #endif
-        for (u32 w0 = 0; 64 * w0 < npad; w0 += kU) {
-          u32 jv[kU], e0v[kU];
-          uint4 av[kU], nv[kU];
-          bool more = false;                           // a chunk meets 3+ segments
-#pragma unroll
-          for (int u = 0; u < kU; u++) cmap[u * kWave + lane] = 0;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          u32 cu[kU];                                  // segments ending at or before window u
-#pragma unroll
-          for (int u = 0; u < kU; u++) cu[u] = carry;
-          const u32 bend = 1024 * (w0 + kU);
-          for (u32 k0 = carry; k0 < nseg; k0 += kWave) {
-            const u32 k = k0 + lane;
-            const u32 end = k < nseg ? seg[k].end : 0xFFFFFFFFu;
-            const u32 t = (end + 15) >> 4;
-            if (k < nseg && t >= 64 * w0 && t < 64 * (w0 + kU))
-              atomicMax(&cmap[t - 64 * w0], k + 1);
-#pragma unroll
-            for (int u = 1; u < kU; u++)
-              cu[u] += __builtin_popcountll(__ballot(k < nseg && end <= 1024 * (w0 + u)));
-            if (readlane(end, 63) >= bend || k0 + kWave >= nseg) break;
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          u32 mv[kU];
-#pragma unroll
-          for (int u = 0; u < kU; u++) mv[u] = cmap[u * kWave + lane];
-#pragma unroll
-          for (int u = 0; u < kU; u++) {
-            const u32 w = w0 + u;
-            const u32 x0 = 1024 * w + 16 * lane, c = 64 * w + lane;
-            const bool live = c < nch;
-            u32 j = max(scan_max(mv[u]), cu[u]);
-            Seg g0 = seg[j < nseg ? j : nseg - 1];
-            while (live && j + 1 < nseg && g0.end <= x0) {   // (cannot happen: kept as a guard)
-              j++;
-              g0 = seg[j];
-            }
-            const bool two = live && j + 1 < nseg && g0.end < x0 + 16;
-            const Seg g1 = seg[two ? j + 1 : j];
-            more |= __ballot(two && g1.end < x0 + 16 && j + 2 < nseg) != 0;
-            av[u] = seg_load(rs, sa, (int)x0 + g0.delta, live);
-            nv[u] = seg_load(rs, sa, (int)x0 + g1.delta, two);
-            jv[u] = j;
-            e0v[u] = two ? g0.end : 0xFFFFFFFFu;
-            if (u == kU - 1) carry = readlane(j, 63);
-          }
+          // Iteration i: issue CRC step i's loads, map group i + 1 and issue its loads, merge and
+          // store group i, fold CRC step i. The waits for group i's loads and for step i's loads
+          // leave the later-issued loads in flight (vmcnt counts in issue order).
+          const FusedCrc fc = fused_crc_init(p, s, P);
+          const u32 G = (nwin + kU - 1) / kU, I = max(G, fc.S);
+          Group ga = {}, gb = {};                      // (initialised: not carried across blocks)
+          uint4 cv[kStepPieces];
+          u32 acc = 0;
+          u32 m0 = G ? map_group(0, 0, nseg, seg, cmap, rs, ga) : 0;
           BW_ST(1);
-#pragma unroll
-          for (int u = 0; u < kU; u++) {
-            const u32 w = w0 + u;
-            const u32 x0 = 1024 * w + 16 * lane, c = 64 * w + lane;
-            const bool live = c < nch;
-            uint4 acc = av[u];
-            u64 lo = (u64)acc.y << 32 | acc.x, hi = (u64)acc.w << 32 | acc.z;
-            if (e0v[u] != 0xFFFFFFFFu) {               // the next segment's bytes after e0
-              u64 mlo, mhi;
-              range_mask((int)(e0v[u] - x0), 16, mlo, mhi);
-              const u64 nlo = (u64)nv[u].y << 32 | nv[u].x, nhi = (u64)nv[u].w << 32 | nv[u].z;
-              lo = (lo & ~mlo) | (nlo & mlo);
-              hi = (hi & ~mhi) | (nhi & mhi);
-            }
-            if (more && live && e0v[u] != 0xFFFFFFFFu) {
-              // chunks meeting 3+ segments (segments under 16 B): the rest one by one
-              u32 jj = jv[u] + 1, eprev = seg[jj].end;
-              while (jj + 1 < nseg && eprev < x0 + 16) {
-                jj++;
-                const Seg g = seg[jj];
-                const uint4 nx = seg_load(rs, sa, (int)x0 + g.delta, true);
-                u64 mlo, mhi;
-                range_mask((int)(eprev - x0), 16, mlo, mhi);
-                const u64 nlo = (u64)nx.y << 32 | nx.x, nhi = (u64)nx.w << 32 | nx.z;
-                lo = (lo & ~mlo) | (nlo & mlo);
-                hi = (hi & ~mhi) | (nhi & mhi);
-                eprev = g.end;
-              }
-            }
-            // bytes past the stream are zero; pad chunks up to the 128-byte line are zero
-            u64 klo, khi;
-            range_mask(0, live ? (int)min(tot - x0, 16u) : 0, klo, khi);
-            lo &= klo;
-            hi &= khi;
-            if (c < npad)
-              *reinterpret_cast<uint4*>(dst + x0) = make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
+#if TPZ_BW_PIPE
+          for (u32 i = 0; i < I; i += 2) {             // unrolled by two: no group copies
+            if (i < fc.S) fused_crc_issue(fc, i, cv);
+            if (i + 1 < G) m0 = map_group((i + 1) * kU, m0, nseg, seg, cmap, rs, gb);
+            BW_ST(1);
+            if (i < G) store_group(i * kU, tot, nseg, seg, rs, ds, ga);
+            BW_ST(3);
+            if (i < fc.S) acc = fused_crc_fold(fc, p, rep, i, cv, acc);
+            BW_ST(4);
+            if (i + 1 >= I) break;
+            if (i + 1 < fc.S) fused_crc_issue(fc, i + 1, cv);
+            if (i + 2 < G) m0 = map_group((i + 2) * kU, m0, nseg, seg, cmap, rs, ga);
+            BW_ST(1);
+            if (i + 1 < G) store_group((i + 1) * kU, tot, nseg, seg, rs, ds, gb);
+            BW_ST(3);
+            if (i + 1 < fc.S) acc = fused_crc_fold(fc, p, rep, i + 1, cv, acc);
+            BW_ST(4);
           }
-          BW_ST(3);
+#else
+          for (u32 i = 0; i < I; i++) {                // one group at a time
+#ifndef TPZ_BW_NOCRC
+            if (i < fc.S) fused_crc_issue(fc, i, cv);
+#endif
+            if (i < G && i > 0) m0 = map_group(i * kU, m0, nseg, seg, cmap, rs, ga);
+            BW_ST(1);
+#ifndef TPZ_BW_NOCRC
+            if (i < fc.S) acc = fused_crc_fold(fc, p, rep, i, cv, acc);
+#endif
+            BW_ST(4);
+            if (i < G) store_group(i * kU, tot, nseg, seg, rs, ds, ga);
+            BW_ST(3);
+          }
+#endif
+          issue_next_header();
+          const u32 R = wave_xor(gf_mul(p.step_lane_shift[lane], acc));
+          const u32 k = (u32)(fc.Pa - fc.pend);
+#ifdef TPZ_BW_NOCRC
+          const u32 crc = stored + 0 * R * k;          // timing build only
+#else
+          const u32 crc = (R == shift_small(p, ~stored, k)) ? stored : ~unshift_small(p, R, k);
+#endif
+          if (crc != stored) {                                                 // checksum.rs:17
+            st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+            bcnt = 0;
+          }
+          put_meta(p, b, st, bcnt, crc);
+          return;
         }
       }
-    }
-    BW_ST(5);
-    // ---- CRC
+      BW_ST(5);
+      issue_next_header();                   // lands during this block's CRC
+      // ---- CRC (blocks that are not copied: malformed ones)
 #ifdef TPZ_BW_NOCRC
-    const u32 crc = stored;                        // timing build only
+      const u32 crc = stored;                        // timing build only
 #else
-    const u32 R = block_crc(p, rep, s, P);
-    const u32 k = (u32)(((s + P + 15) & ~15ull) - (s + P));
-    const u32 crc = (R == shift_small(p, ~stored, k)) ? stored : ~unshift_small(p, R, k);
+      const u32 R = block_crc(p, rep, s, P);
+      const u32 k = (u32)(((s + P + 15) & ~15ull) - (s + P));
+      const u32 crc = (R == shift_small(p, ~stored, k)) ? stored : ~unshift_small(p, R, k);
 #endif
-    if (crc != stored) {                                                       // checksum.rs:17
-      st = TPZ_BLOCK_CHECKSUM_MISMATCH;
-      bcnt = 0;
-    }
-    BW_ST(4);
-    put_meta(p, b, st, bcnt, crc);
+      if (crc != stored) {                                                     // checksum.rs:17
+        st = TPZ_BLOCK_CHECKSUM_MISMATCH;
+        bcnt = 0;
+      }
+      BW_ST(4);
+      put_meta(p, b, st, bcnt, crc);
+    }();
+    issue_next_header();
+    b = bn;
+    s = sn;
+    e = en;
+    hw = hwn;
+    bn = bnn;
   }
 #ifdef TPZ_BW_STAMPS
   if (lane == 0)
@@ -516,6 +724,8 @@ void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream) {
   p.big_list = a.big_list;
   p.big_count = a.big_count;
   for (int l = 0; l < 64; l++) p.lane_shift[l] = x8n_host((u64)kRun * l);
+  for (int l = 0; l < 64; l++) p.step_lane_shift[l] = x8n_host((u64)kStepRun * l);
+  p.step_shift = x8n_host(kStep);
   p.win_shift = x8n_host(kCrcWin);
   p.half_shift = x8n_host(kRun / 2);
   hipLaunchKernelGGL(decode_bigwave_kernel, dim3(a.grid), dim3(kThreads), 0, stream, p);

@@ -1404,9 +1404,11 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
         fl_addr[wid][k] = fl;
         fl_lane[wid][k] = lane;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      // LDS written and read back by this wave only: the LDS runs one wave's instructions in
+      // order, so a compiler barrier suffices (a wavefront fence also waits for every
+      // outstanding global load and store, s_waitcnt vmcnt(0))
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      asm volatile("" ::: "memory");
       for (u32 q = 0; q < cnt; q += kWave / 4) {
         const u32 k = q + (lane >> 2);
         if (k < cnt) {

@@ -471,6 +471,18 @@ __device__ __forceinline__ void defer_to(u32* list, u32* count, u32 b) {
   if (lane_id() == 0) list[atomicAdd(count, 1u)] = b;
 }
 
+// The lanes in `take` append their block bb to a worklist with one atomic per wave (a
+// single-address atomic per block serialises at the memory side: 0.75 ms per 65,536 long
+// blocks, profiles/r2/kernel_stats_64k.csv).
+__device__ __forceinline__ void defer_lanes(u32* list, u32* count, bool take, u32 bb) {
+  const u64 m = __ballot(take);
+  if (!m) return;
+  u32 base = 0;
+  if (lane_id() == (u32)__builtin_ctzll(m)) base = atomicAdd(count, (u32)__builtin_popcountll(m));
+  base = __builtin_amdgcn_readlane(base, __builtin_ctzll(m));
+  if (take) list[base + __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u))] = bb;
+}
+
 // Lane 0 stores block b's status, count and crc. Every lane issues the three buffer stores
 // (the others at an offset past the descriptor, which the hardware drops) instead of a
 // lane-0 branch: no exec-skip branch and its scalar bookkeeping per block, and the block's
@@ -1054,8 +1066,25 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     ge = p.ext[bb + 1];
   };
   auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
+  // Blocks that do not fit a wave slot are sent to their worklist when their extent group
+  // becomes current, 64 at a time: fewer than 64 entries -> the one-wave-per-block kernel,
+  // past the big path's window -> the spill path, else the LDS big path. The decode loop then
+  // skips them.
+  auto triage_group = [&](u32 g, u64 gs, u64 ge) {
+    const u64 bb = (u64)b0 + ((u64)g * 64 + lane) * nw;
+    const bool lng = bb < p.n_blocks && ge - gs > kWaveMaxLen;
+    if (!__ballot(lng)) return;
+    u32 nent = 0xFFFFu;
+    if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
+    const bool to_bw = lng && nent < 64 && p.out.bw_list;
+    const bool to_spill = lng && !to_bw && ge - gs > kBigMaxLen;
+    if (p.out.bw_list) defer_lanes(p.out.bw_list, p.out.bw_count, to_bw, (u32)bb);
+    defer_lanes(p.out.spill_list, p.out.spill_count, to_spill, (u32)bb);
+    defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
+  };
   load_group(0, gs_cur, ge_cur);
   load_group(1, gs_nxt, ge_nxt);
+  triage_group(0, gs_cur, ge_cur);
 
   // prefetch state for block b
   uint4 v[kWinRounds];
@@ -1110,6 +1139,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       gs_cur = gs_nxt;
       ge_cur = ge_nxt;
       load_group((k >> 6) + 1, gs_nxt, ge_nxt);
+      triage_group(k >> 6, gs_cur, ge_cur);
     }
     issue(b, k, s_cur, e_cur);       // next block's loads fly while this one decodes
     vm_pad<kVmAfter>(p.out);
@@ -1118,15 +1148,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (fits) {
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
                                                            len64, bcur, s, p.out, kshift, S);
-    } else {
-      // a long block: one with fewer than 64 entries (the 64 KiB config: 61) goes to the
-      // one-wave-per-block kernel; more entries to the LDS big path, or past its window to the
-      // spill path
-      const u32 nent = uni(((u32)p.src[s] << 8) | p.src[s + 1]);
-      if (nent < 64 && p.out.bw_list) defer_to(p.out.bw_list, p.out.bw_count, bcur);
-      else if (len64 > kBigMaxLen) defer_to(p.out.spill_list, p.out.spill_count, bcur);
-      else defer_to(p.out.defer_list, p.out.defer_count, bcur);
-    }
+    }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
   }
