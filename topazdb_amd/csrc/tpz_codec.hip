@@ -1168,8 +1168,8 @@ __device__ __forceinline__ u128 lowbytes(u128 v, u32 m) {    // the low m (< 16)
 }
 
 // The 16 ring bytes at absolute address a (R[a % kRing ..], any alignment).
-__device__ __forceinline__ u128 ring_read(const uint8_t* R, u64 a) {
-  const u32 o = (u32)a & (kRing - 1), m = o & 15, o0 = o & ~15u;
+__device__ __forceinline__ u128 ring_read(const uint8_t* R, u32 a) {
+  const u32 o = a & (kRing - 1), m = o & 15, o0 = o & ~15u;
   const u128 s0 = lds16(R + o0), s1 = lds16(R + ((o0 + 16) & (kRing - 1)));
   return m ? (s0 >> (8 * m)) | (s1 << (8 * (16 - m))) : s0;
 }
@@ -1177,15 +1177,25 @@ __device__ __forceinline__ u128 ring_read(const uint8_t* R, u64 a) {
 // Writes the step's output bytes [P, P + c) (c <= 64; v[j] = bytes [P + 16 j, P + 16 j + 16))
 // into the ring's aligned slots. acc holds the slot containing P (its bytes below P are the
 // output); on return it holds the slot containing P + c.
-__device__ __forceinline__ void ring_emit(uint8_t* R, u64 P, u32 c, const u128 (&v)[4], u128& acc) {
-  const u32 m = (u32)P & 15, K = (m + c + 15) >> 4, Kn = (m + c) >> 4;
-  const u64 A = P & ~(u64)15;
+__device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (&v)[4], u128& acc) {
+#ifdef TPZ_CODEC_CHEAPEMIT
+  {                                          // timing build only: no funnel (wrong bytes)
+    const u32 A = P & ~15u, K = (c + 15) >> 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), v[k]);
+    acc = v[0];
+    return;
+  }
+#endif
+  const u32 m = P & 15, K = (m + c + 15) >> 4, Kn = (m + c) >> 4;
+  const u32 A = P & ~15u;
   u128 carry = m ? lowbytes(acc, m) : (u128)0, nacc = acc;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
     const u128 cur = k < 4 ? v[k < 4 ? k : 0] : (u128)0;
     const u128 slot = m ? carry | (cur << (8 * m)) : cur;
-    if ((u32)k < K) lds16w(R + ((u32)(A + 16 * k) & (kRing - 1)), slot);
+    if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), slot);
     if ((u32)k == Kn) nacc = slot;
     carry = m ? cur >> (8 * (16 - m)) : (u128)0;
   }
@@ -1193,8 +1203,8 @@ __device__ __forceinline__ void ring_emit(uint8_t* R, u64 P, u32 c, const u128 (
 }
 
 // dst[x0 .. x1) from the ring, exact width (the lines a block shares with its neighbours)
-__device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst, u64 x0, u64 x1) {
-  for (u64 k = 0; x0 + k < x1; k += 16) {
+__device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst, u32 x0, u32 x1) {
+  for (u32 k = 0; x0 + k < x1; k += 16) {
     const u128 v = ring_read(R, x0 + k);
     if (x0 + k + 16 <= x1) st16u(dst + x0 + k, v);
     else put_tail(dst + x0, k, v, x1 - x0);
@@ -1203,7 +1213,7 @@ __device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst,
 
 __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kRingWG * kRing];
-  __shared__ u64 fl_addr[kRingWG / kWave][kWave];
+  __shared__ u32 fl_addr[kRingWG / kWave][kWave];
   __shared__ u32 fl_lane[kRingWG / kWave][kWave];
   const u32 lane = lane_id(), wid = threadIdx.x >> 6;
   uint8_t* R = rings + threadIdx.x * kRing;
@@ -1214,32 +1224,37 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       (void*)p.src, (short)0, (int)(p.src_bytes < 0x7FFFFFF0ull ? p.src_bytes : 0x7FFFFFF0ull),
       0x00020000);
 
+  // Every position is a 32-bit offset: live blocks need src_bytes and dst_bytes below 2^31.
   bool live = false;
-  u64 s = 0, n = 0, ip = 0, want = 0, D0 = 0, dn = 0;
+  u32 s = 0, n = 0, ip = 0, want = 0, D0 = 0, dn = 0;
   if (b < p.n_blocks) {
-    s = p.ext[b];
-    const u64 e = p.ext[b + 1], len = e - s;
-    D0 = p.dst_ext[b];
-    dn = p.dst_ext[b + 1] - D0;
-    const u32 tag = len ? p.src[e - 1] : 0u;
-    live = len > 1 && tag == 2 && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
+    const u64 s64 = p.ext[b], e64 = p.ext[b + 1], len = e64 - s64;
+    const u64 D064 = p.dst_ext[b], dn64 = p.dst_ext[b + 1] - D064;
+    const u32 tag = len ? p.src[e64 - 1] : 0u;
+    live = len > 1 && tag == 2 && dn64 >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
            dst_bytes < 0x7FFFFFF0ull && p.src_bytes < 0x7FFFFFF0ull;
     if (live) {
-      const u32 h = snappy_header(p.src + s, len - 1, want);
-      live = h != 0 && want + 1 == dn;
+      u64 want64 = 0;
+      const u32 h = snappy_header(p.src + s64, len - 1, want64);
+      live = h != 0 && want64 + 1 == dn64;
+      s = (u32)s64;
       ip = h;
-      n = len - 1;
+      n = (u32)(len - 1);
+      want = (u32)want64;
+      D0 = (u32)D064;
+      dn = (u32)dn64;
     }
     if (!live) p.status[b] = kLeftForWaveKernel;
   }
-  u64 d = 0;                                  // bytes produced
-  const u64 head_end = (D0 + kRingLine - 1) & ~(u64)(kRingLine - 1);
-  u64 fl = D0;                                // bytes below fl are stored
+  const u32 src_bytes = live ? (u32)p.src_bytes : 0u;
+  u32 d = 0;                                  // bytes produced
+  const u32 head_end = (D0 + kRingLine - 1) & ~(kRingLine - 1);
+  u32 fl = D0;                                // bytes below fl are stored
   u128 hv = live ? ld16c(p.src, p.src_bytes, s + ip) : (u128)0;
   u32 hvv = 16;                               // hv holds the input bytes [ip, ip + hvv)
   u128 acc = 0;                               // the ring slot holding the frontier D0 + d
   u32 ek = 0;                                 // element: 0 literal, 1 copy
-  u64 erem = 0, esrc = 0, eoff = 0;
+  u32 erem = 0, esrc = 0, eoff = 0;
 #ifdef TPZ_CODEC_STAMPS
   const u64 t0 = __builtin_amdgcn_s_memtime();
   u64 trips = 0, gtrips = 0, elems = 0;
@@ -1254,22 +1269,25 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       if (ip >= n) {
         finish = true;
       } else {
-        const u64 h = (u64)hv;
-        const u32 tag = (u32)h & 0xFF, kind = tag & 3, t6 = tag >> 2;
-        const u32 x = (u32)(h >> 8);
-        u64 len, off = 0, hl;
+        const u32 h0 = (u32)hv, x = (u32)(hv >> 8);
+        const u32 tag = h0 & 0xFF, kind = tag & 3, t6 = tag >> 2;
+        u32 len, off = 0, hl;
+        bool big = false;                     // a 4-byte literal length past any output
         if (kind == 0) {
           const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
-          len = (u64)(nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1))) + 1;
+          const u32 l0 = nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1));
+          big = l0 >= 0x7FFFFFF0u;
+          len = l0 + 1;
           hl = 1 + nb;
         } else {
           len = kind == 1 ? 4 + (t6 & 7) : t6 + 1;
           hl = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
           off = kind == 1 ? (((tag >> 5) << 8) | (x & 0xFF)) : (kind == 2 ? (x & 0xFFFF) : x);
         }
-        const u64 next = ip + hl + (kind == 0 ? len : 0);
+        const u32 next = ip + hl + (kind == 0 ? len : 0);
         // snap's Err: output overrun, element past the input, copy offset 0 or before the output
-        if (d + len > want || next > n || (kind != 0 && (off == 0 || off > d))) {
+        if (big || d + len > want || next > n || next < ip ||
+            (kind != 0 && (off == 0 || off > d))) {
           fail = true;
         } else {
           ek = kind == 0 ? 0u : 1u;
@@ -1280,18 +1298,18 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
           // the next header: still in hv after a copy or a short literal (a header is at most 5
           // bytes), else loaded now, in flight while this element is produced (clamped near the
           // end of the source)
-          const u32 used = (u32)(kind == 0 ? (hl + len < 16 ? hl + len : 16) : hl);
+          const u32 used = kind == 0 ? (hl + len < 16 ? hl + len : 16) : hl;
           hv = used < 16 ? hv >> (8 * used) : (u128)0;
           hvv = hvv > used ? hvv - used : 0u;
           // a literal whose final step's last piece ends 5..15 bytes past the literal carries the
           // next header: taken from that piece when the literal completes (hvv = 0 until then)
-          const u32 cf = (u32)(kind == 0 ? (len - 1) % kRingStep + 1 : 0), rf = cf & 15;
+          const u32 rf = kind == 0 ? ((len - 1) % kRingStep + 1) & 15 : 0u;
           const bool from_lit = kind == 0 && hvv < 5 && rf >= 1 && rf <= 11 &&
-                                s + next + 5 <= p.src_bytes;
+                                s + next + 5 <= src_bytes;
           if (from_lit) hvv = 0;
           else if (hvv < 5) {
-            hv = s + next + 16 <= p.src_bytes
-                     ? __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(srs, (u32)(s + next), 0, 0))
+            hv = s + next + 16 <= src_bytes
+                     ? __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(srs, s + next, 0, 0))
                      : ld16c(p.src, p.src_bytes, s + next);
             hvv = 16;
           }
@@ -1304,12 +1322,20 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
     // produce up to kRingStep bytes of the current element (a copy with off >= 16: at most off,
     // so every source byte precedes the step)
     const bool prod = live && !finish && !fail && erem > 0;
-    const u64 P = D0 + d;
-    u64 c = prod ? (erem < kRingStep ? erem : (u64)kRingStep) : 0;
-    if (prod && ek == 1 && eoff >= 16 && eoff < c) c = eoff;
-    const u64 Pl = P & ~(u64)(kRingLine - 1);
-    const u64 ring_lo = Pl >= kRingLine ? Pl - kRingLine : 0;        // previous line: intact
-    const bool gcopy = prod && ek == 1 && eoff >= 16 && P - eoff < ring_lo;
+    const u32 P = D0 + d;
+    u32 c = prod ? (erem < kRingStep ? erem : kRingStep) : 0u;
+    const bool lit = ek == 0, far = !lit && eoff >= 16;
+    if (prod && far && eoff < c) c = eoff;
+    const u32 Pl = P & ~(kRingLine - 1);
+    const u32 ring_lo = Pl >= kRingLine ? Pl - kRingLine : 0u;        // previous line: intact
+    const u32 q0 = P - eoff;                                          // a copy's first source byte
+    const bool gcopy = prod && far && q0 < ring_lo;
+    // the 16-byte pieces this step loads from memory (a prefix of the step's four): a literal's,
+    // or a far copy's pieces that start below the ring (the others come from the ring)
+    const bool tail = lit && esrc + kRingStep + 16 > src_bytes;
+    const u32 cp = (c + 15) >> 4;
+    const u32 np = !prod ? 0u : lit ? (tail ? 0u : cp)
+                 : !gcopy ? 0u : min(cp, (ring_lo - q0 + 15) >> 4);
     if (__ballot(gcopy)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stored lines landed
 #ifdef TPZ_CODEC_STAMPS
@@ -1321,46 +1347,39 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       // stored lines a far copy reads (the wave's own stores: same CU, visible after the vmcnt
       // wait above). Pieces a lane does not need are exec-masked off.
       u128 v[4];
-      const bool lit = ek == 0;
-      const bool tail = lit && esrc + kRingStep + 16 > p.src_bytes;
-      const bool far = !lit && eoff >= 16;
-      const uint8_t* base = lit ? p.src + esrc : p.dst + (P - eoff);
+      const uint8_t* base = lit ? p.src + esrc : p.dst + q0;
 #pragma unroll
       for (int j = 0; j < 4; j++) v[j] = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const bool need = 16 * j < c && (lit ? !tail : (far && P - eoff + 16 * j < ring_lo));
-        if (need) v[j] = *reinterpret_cast<const u128 __attribute__((aligned(1)))*>(base + 16 * j);
-      }
+      for (int j = 0; j < 4; j++)
+        if ((u32)j < np) v[j] = *reinterpret_cast<const u128 __attribute__((aligned(1)))*>(base + 16 * j);
       if (lit) {
         if (tail)
 #pragma unroll
           for (int j = 0; j < 4; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
         esrc += c;
         if (c == erem && hvv == 0) {
-          const u32 r16 = (u32)c & 15, last = ((u32)c - 1) >> 4;
+          const u32 r16 = c & 15, last = (c - 1) >> 4;
           const u128 lp = last == 0 ? v[0] : last == 1 ? v[1] : last == 2 ? v[2] : v[3];
           hv = lp >> (8 * r16);
           hvv = 16 - r16;
         }
-      } else if (eoff < 16) {
+      } else if (!far) {
         const u128 pat = ring_read(R, P - 16) >> (8 * (16 - eoff));
-        const u32 o32 = (u32)eoff, s16 = 16u % o32;
+        const u32 s16 = 16u % eoff;
         u32 r = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          v[j] = periodic16(pat, o32, r);
+          v[j] = periodic16(pat, eoff, r);
           r += s16;
-          r = r >= o32 ? r - o32 : r;
+          r = r >= eoff ? r - eoff : r;
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const u64 a = P - eoff + 16 * j;
-          if (16 * j < c && a >= ring_lo) v[j] = ring_read(R, a);
-        }
+        for (int j = 0; j < 4; j++)
+          if ((u32)j >= np && (u32)j < cp) v[j] = ring_read(R, q0 + 16 * j);
       }
-      ring_emit(R, P, (u32)c, v, acc);
+      ring_emit(R, P, c, v, acc);
       d += c;
       erem -= c;
     }
@@ -1372,10 +1391,10 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       live = false;
       if (d == want) {
         // re-tagged Uncompress: the tag byte joins the frontier slot
-        const u64 T = D0 + want;
-        const u32 m = (u32)T & 15;
+        const u32 T = D0 + want;
+        const u32 m = T & 15;
         const u128 slot = lowbytes(acc, m) | ((u128)1 << (8 * m));
-        lds16w(R + ((u32)(T & ~(u64)15) & (kRing - 1)), slot);
+        lds16w(R + ((T & ~15u) & (kRing - 1)), slot);
         ring_store_exact(R, p.dst, fl, D0 + dn);
         fl = D0 + dn;
         p.status[b] = TPZ_BLOCK_OK;
@@ -1384,7 +1403,7 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       }
     }
     // the head line (shared with the previous block) once complete, then whole lines
-    const u64 F = D0 + d;
+    const u32 F = D0 + d;
     if (live && fl < head_end && F >= head_end) {
       ring_store_exact(R, p.dst, fl, head_end);
       fl = head_end;
@@ -1407,9 +1426,9 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       for (u32 q = 0; q < cnt; q += kWave / 4) {
         const u32 k = q + (lane >> 2);
         if (k < cnt) {
-          const u64 a = fl_addr[wid][k];
+          const u32 a = fl_addr[wid][k];
           const uint8_t* Rs = rings + (wid * kWave + fl_lane[wid][k]) * kRing;
-          const u32 o = ((u32)a & (kRing - 1)) + 16 * (lane & 3);
+          const u32 o = (a & (kRing - 1)) + 16 * (lane & 3);
           st16u(p.dst + a + 16 * (lane & 3), lds16(Rs + o));
         }
       }
