@@ -321,6 +321,42 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* ctx, const uint8_t* d_filter, uint64_t fi
 /* xxh3_64 (seed 0) on the host: the hash the reference's bloom uses (xxhash-rust 0.8.5). */
 uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len);
 
+/* ---- device write side (SURVEY.md §8f row 4's alternative: compaction output) ------------
+ * A run of sorted entries in HBM becomes SST data-region blocks, byte for byte what
+ * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) writes with
+ * CompressOptions::Uncompress: BlockBuilder's fill rule (src/block/builder.rs:26-41: an entry
+ * joins the block while size + encode_len + 2 <= block_size), Block::encode (src/block.rs:31-44),
+ * Entry::encode (builder.rs:72-81), the CRC (src/checksum.rs:6-10) and the tag
+ * (src/block/compress.rs:85-89). Entry e: key = d_keys[d_kpos[e] .. d_kpos[e+1]), value =
+ * d_vals[d_vpos[e] .. d_vpos[e+1]) (d_kpos/d_vpos: n_entries + 1 non-decreasing offsets; key_bytes
+ * and val_bytes = the readable bytes at d_keys / d_vals, at least d_kpos[n] / d_vpos[n]).
+ *   tpz_plan_blocks: the block cuts. d_first[b] = first entry of block b, d_ext[b] = its byte
+ *     offset in the data region (SsTableBuilder's data.len() when it was built, i.e.
+ *     BlockMeta::offset), for b <= n_blocks (d_first[n_blocks] = n_entries, d_ext[n_blocks] = the
+ *     region's length); both need n_entries + 1 entries. SYNCHRONOUS on `stream` (it returns
+ *     *h_n_blocks). An empty key (builder.rs:27 asserts) or an entry no block can hold (encode_len
+ *     + 2 > block_size: SsTableBuilder::add recurses without end, table/builder.rs:57-60) makes it
+ *     return TPZ_ERR_INVALID_ARG with *h_bad_entry = the first such entry (UINT64_MAX otherwise).
+ *     block_size must be in (2, 65536]: past 64 KiB the reference's u16 offsets wrap.
+ *   tpz_encode_blocks: writes block b to d_out[d_ext[b] .. d_ext[b+1]) (d_out 16-byte aligned,
+ *     d_ext[n_blocks] bytes; no byte outside the blocks is written). Asynchronous on `stream`.
+ * BlockMeta::first_key of block b is entry d_first[b]'s key. */
+typedef struct {
+  const uint8_t* d_keys;
+  const uint64_t* d_kpos;
+  const uint8_t* d_vals;
+  const uint64_t* d_vpos;
+  uint32_t n_entries;
+  uint64_t key_bytes;
+  uint64_t val_bytes;
+} tpz_entries;
+
+tpz_err tpz_plan_blocks(tpz_ctx* ctx, const tpz_entries* entries, uint32_t block_size,
+                        uint32_t* d_first, uint64_t* d_ext, uint32_t* h_n_blocks,
+                        uint64_t* h_bad_entry, void* stream);
+tpz_err tpz_encode_blocks(tpz_ctx* ctx, const tpz_entries* entries, const uint32_t* d_first,
+                          const uint64_t* d_ext, uint32_t n_blocks, uint8_t* d_out, void* stream);
+
 /* ---- host write side (inputs for benches and the table facade) ---------------------------
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule
  * (src/block/builder.rs:26-41) and Block::encode + Uncompress (src/block.rs:31-44,

@@ -609,3 +609,80 @@ double tpzo_bench_iter_read(const char* const* paths, uint32_t n_paths, uint32_t
   *entries = en;
   return dt;
 }
+
+/* ---- write side: SsTableBuilder's data region with CompressOptions::Uncompress ------------
+ * The checker for tpz_plan_blocks / tpz_encode_blocks. Restates, entry by entry:
+ *   BlockBuilder::add           src/block/builder.rs:26-41 (assert key non-empty; full when
+ *                               encode_len + size + 2 > target_size; offsets as u16)
+ *   SsTableBuilder::add         src/table/builder.rs:49-64 (a full block is built, then the
+ *                               entry is added again: an entry that fits no block recurses
+ *                               forever in the reference -> -2 here)
+ *   SsTableBuilder::block_build src/table/builder.rs:66-85 (BlockMeta::offset = data.len())
+ *   Block::encode               src/block.rs:31-44 (n u16 BE, offsets u16 BE, data, crc BE)
+ *   Entry::encode               src/block/builder.rs:72-81 (klen u16 BE, key, vlen u16 BE, value)
+ *   compress::encode Uncompress src/block/compress.rs:85-89 (tag byte 1)
+ * Returns the number of blocks, -1 when out_cap / ext_cap are too small, -2 with *bad = the
+ * entry index for an empty key or an entry no block holds. ext gets n_blocks + 1 offsets,
+ * first the first entry of every block. */
+typedef struct {
+  uint32_t target, size;       /* BlockBuilder { target_size, size } */
+  uint64_t first, count;       /* entries [first, first + count) (data + offsets) */
+} tpzo_bb;
+
+static int bb_add(tpzo_bb* b, uint64_t klen, uint64_t vlen) {
+  const uint64_t enc = 2 + klen + 2 + vlen;           /* Entry::encode_len */
+  if (enc + b->size + 2 > b->target) return 0;
+  b->size += (uint32_t)enc;
+  b->count++;
+  return 1;
+}
+
+static void put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+int64_t tpzo_build_blocks(const uint8_t* keys, const uint64_t* kpos, const uint8_t* vals,
+                          const uint64_t* vpos, uint64_t n, uint32_t block_size, uint8_t* out,
+                          uint64_t out_cap, uint64_t* ext, uint64_t* first, uint64_t ext_cap,
+                          uint64_t* bad) {
+  uint64_t len = 0, nb = 0, e = 0;
+  tpzo_bb b = {block_size, 0, 0, 0};
+  for (;;) {
+    const int more = e < n;
+    if (more) {
+      const uint64_t kl = kpos[e + 1] - kpos[e], vl = vpos[e + 1] - vpos[e];
+      if (kl == 0) { *bad = e; return -2; }
+      if (bb_add(&b, kl, vl)) { e++; continue; }
+      if (b.count == 0) { *bad = e; return -2; }
+    }
+    if (b.count) {                                      /* block_build */
+      const uint64_t blen = 2 + 2 * b.count + b.size + 5;
+      if (len + blen > out_cap || nb + 2 > ext_cap) return -1;
+      uint8_t* p = out + len;
+      put_be16(p, (uint32_t)b.count);
+      uint32_t off = 0;
+      uint8_t* d = p + 2 + 2 * b.count;
+      for (uint64_t i = 0; i < b.count; i++) {
+        const uint64_t x = b.first + i, kl = kpos[x + 1] - kpos[x], vl = vpos[x + 1] - vpos[x];
+        put_be16(p + 2 + 2 * i, off);
+        put_be16(d + off, (uint32_t)kl);
+        memcpy(d + off + 2, keys + kpos[x], kl);
+        put_be16(d + off + 2 + kl, (uint32_t)vl);
+        memcpy(d + off + 4 + kl, vals + vpos[x], vl);
+        off += (uint32_t)(4 + kl + vl);
+      }
+      const uint64_t plen = 2 + 2 * b.count + b.size;
+      const uint32_t crc = tpzo_crc32(p, plen);
+      p[plen] = (uint8_t)(crc >> 24); p[plen + 1] = (uint8_t)(crc >> 16);
+      p[plen + 2] = (uint8_t)(crc >> 8); p[plen + 3] = (uint8_t)crc;
+      p[plen + 4] = 1;
+      ext[nb] = len;
+      first[nb] = b.first;
+      nb++;
+      len += blen;
+    }
+    if (!more) break;
+    b.size = 0; b.first = e; b.count = 0;
+  }
+  ext[nb] = len;
+  first[nb] = n;
+  return (int64_t)nb;
+}

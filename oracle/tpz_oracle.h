@@ -107,6 +107,14 @@ size_t tpzo_lz4_compress(const uint8_t* src, size_t n, uint8_t* dst, int mode);
 double tpzo_bench_iter_read(const char* const* paths, uint32_t n_paths, uint32_t threads,
                             uint32_t iters, uint64_t* bytes, uint64_t* entries);
 
+/* ---- write side: SsTableBuilder's data region (Uncompress), the checker of the device encode
+ * (builder.rs:26-81, table/builder.rs:49-85, block.rs:31-44). Returns n_blocks, -1 (capacity)
+ * or -2 (*bad = an entry with an empty key or too large for any block). */
+int64_t tpzo_build_blocks(const uint8_t* keys, const uint64_t* kpos, const uint8_t* vals,
+                          const uint64_t* vpos, uint64_t n, uint32_t block_size, uint8_t* out,
+                          uint64_t out_cap, uint64_t* ext, uint64_t* first, uint64_t ext_cap,
+                          uint64_t* bad);
+
 #ifdef __cplusplus
 }
 #endif

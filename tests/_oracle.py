@@ -55,6 +55,10 @@ def lib() -> C.CDLL:
         L.tpzo_lz4_prefixed_size.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_int64)]
         L.tpzo_lz4_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
         L.tpzo_lz4_compress.restype = C.c_size_t
+        L.tpzo_build_blocks.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_uint32, C.c_void_p,
+                                                           C.c_uint64, C.c_void_p, C.c_void_p,
+                                                           C.c_uint64, u64p]
+        L.tpzo_build_blocks.restype = C.c_int64
         L.tpzo_bench_iter_read.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
                                            C.c_uint32, u64p, u64p]
         L.tpzo_bench_iter_read.restype = C.c_double
@@ -64,6 +68,28 @@ def lib() -> C.CDLL:
 
 def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
+
+
+def build_blocks(keys, kpos, vals, vpos, block_size: int):
+    """SsTableBuilder's Uncompress data region restated (tpzo_build_blocks): (region bytes,
+    ext[n_blocks + 1], first entry of each block [n_blocks + 1]); raises ValueError(index) for
+    an entry the reference cannot take."""
+    kpos = np.ascontiguousarray(kpos, np.uint64)
+    vpos = np.ascontiguousarray(vpos, np.uint64)
+    n = len(kpos) - 1
+    keys = np.ascontiguousarray(keys, np.uint8) if len(keys) else np.zeros(1, np.uint8)
+    vals = np.ascontiguousarray(vals, np.uint8) if len(vals) else np.zeros(1, np.uint8)
+    cap = int(kpos[-1] - kpos[0] + vpos[-1] - vpos[0]) + 13 * n + 16
+    out = np.zeros(cap, np.uint8)
+    ext = np.zeros(n + 2, np.uint64)
+    first = np.zeros(n + 2, np.uint64)
+    bad = C.c_uint64()
+    nb = lib().tpzo_build_blocks(_ptr(keys), _ptr(kpos), _ptr(vals), _ptr(vpos), n, block_size,
+                                 _ptr(out), cap, _ptr(ext), _ptr(first), n + 2, C.byref(bad))
+    if nb == -2:
+        raise ValueError(int(bad.value))
+    assert nb >= 0
+    return out[:int(ext[nb])].copy(), ext[:nb + 1].copy(), first[:nb + 1].copy()
 
 
 def crc32(b: bytes) -> int:

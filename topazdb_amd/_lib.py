@@ -50,6 +50,13 @@ class Table(C.Structure):
                 ("d_spill_off", C.c_void_p)]
 
 
+class Entries(C.Structure):
+    """tpz_entries: sorted entries in HBM for the device write side."""
+    _fields_ = [("d_keys", C.c_void_p), ("d_kpos", C.c_void_p), ("d_vals", C.c_void_p),
+                ("d_vpos", C.c_void_p), ("n_entries", C.c_uint32), ("key_bytes", C.c_uint64),
+                ("val_bytes", C.c_uint64)]
+
+
 class HostColumns(C.Structure):
     """tpz_host_columns: tpz_decode_blocks_host's outputs in host memory."""
     _fields_ = [("h_data", C.c_void_p), ("h_ends", C.c_void_p), ("ends_cap", C.c_uint64),
@@ -112,6 +119,13 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
+        L.tpz_plan_blocks.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_uint32, C.c_void_p,
+                                      C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                      C.c_void_p]
+        L.tpz_plan_blocks.restype = C.c_int
+        L.tpz_encode_blocks.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_void_p, C.c_void_p,
+                                        C.c_uint32, C.c_void_p, C.c_void_p]
+        L.tpz_encode_blocks.restype = C.c_int
         L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
         L.tpz_host_xxh3_64.restype = C.c_uint64
         L.tpz_layout_spill_stream.argtypes = [C.c_uint64]
@@ -256,6 +270,27 @@ class Context:
                                           C.c_void_p(d_keys), C.c_void_p(d_key_pos), n_keys,
                                           C.c_void_p(d_out), C.c_void_p(stream)),
               "tpz_bloom_may_contain")
+
+    def plan_blocks_ptrs(self, ent: Entries, block_size: int, d_first: int, d_ext: int,
+                         stream: int = 0) -> tuple[int, int]:
+        """tpz_plan_blocks (synchronous): BlockBuilder's fill rule over the entries. Returns
+        (rc, n_blocks or the first bad entry): rc ERR_INVALID_ARG with a bad entry index when an
+        entry has an empty key or fits no block (the reference asserts / recurses forever)."""
+        nb, bad = C.c_uint32(), C.c_uint64()
+        rc = lib().tpz_plan_blocks(self.handle, C.byref(ent), block_size, C.c_void_p(d_first),
+                                   C.c_void_p(d_ext), C.byref(nb), C.byref(bad),
+                                   C.c_void_p(stream))
+        if rc == ERR_INVALID_ARG and bad.value != 2**64 - 1:
+            return rc, int(bad.value)
+        check(rc, "tpz_plan_blocks")
+        return rc, int(nb.value)
+
+    def encode_blocks_ptrs(self, ent: Entries, d_first: int, d_ext: int, n_blocks: int,
+                           d_out: int, stream: int = 0) -> None:
+        """tpz_encode_blocks: Block::encode + CRC + Uncompress tag for every planned block."""
+        check(lib().tpz_encode_blocks(self.handle, C.byref(ent), C.c_void_p(d_first),
+                                      C.c_void_p(d_ext), n_blocks, C.c_void_p(d_out),
+                                      C.c_void_p(stream)), "tpz_encode_blocks")
 
 
 def _pack_ends(ctx, d_ext: int, n_blocks: int, src_bytes: int, cols: dict, d_first: int,

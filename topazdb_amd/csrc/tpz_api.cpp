@@ -423,6 +423,112 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filt
   return TPZ_SUCCESS;
 }
 
+namespace {
+// Device scratch of one write-side call, freed on every exit path.
+struct DevScratch {
+  std::vector<void*> p;
+  ~DevScratch() {
+    for (void* x : p) (void)hipFree(x);
+  }
+  hipError_t get(void* out, size_t bytes) {  // out: a T** for any T
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
+    if (e == hipSuccess) p.push_back(d);
+    std::memcpy(out, &d, sizeof d);
+    return e;
+  }
+};
+}  // namespace
+
+tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, uint32_t* d_first,
+                        uint64_t* d_ext, uint32_t* h_n_blocks, uint64_t* h_bad_entry,
+                        void* stream) {
+  if (!c || !en || !d_first || !d_ext || !h_n_blocks || !h_bad_entry) return TPZ_ERR_INVALID_ARG;
+  *h_bad_entry = UINT64_MAX;
+  *h_n_blocks = 0;
+  if (block_size <= 2 || block_size > 65536 || en->n_entries == 0xFFFFFFFFu)
+    return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t n = en->n_entries;
+  if (n == 0) {  // SsTableBuilder with no entries: no block, an empty data region
+    TPZ_HIP(hipMemsetAsync(d_first, 0, 4, s));
+    TPZ_HIP(hipMemsetAsync(d_ext, 0, 8, s));
+    TPZ_HIP(hipStreamSynchronize(s));
+    return TPZ_SUCCESS;
+  }
+  if (!en->d_kpos || !en->d_vpos) return TPZ_ERR_INVALID_ARG;
+  DevScratch sc;
+  uint32_t *nx = nullptr, *info = nullptr;
+  TPZ_HIP(sc.get(&nx, (size_t)n * 4));
+  TPZ_HIP(sc.get(&info, 16));
+  uint32_t h_info[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
+  TPZ_HIP(hipMemcpyAsync(info, h_info, 16, hipMemcpyHostToDevice, s));
+  tpz::PlanLaunch a{};
+  a.phase = 0;
+  a.kpos = en->d_kpos;
+  a.vpos = en->d_vpos;
+  a.n = n;
+  a.block_size = block_size;
+  a.nx = nx;
+  a.info = info;
+  a.first = d_first;
+  a.ext = d_ext;
+  TPZ_HIP(tpz::launch_plan(a, s));
+  TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
+  TPZ_HIP(hipStreamSynchronize(s));
+  if (h_info[1] != 0xFFFFFFFFu) {
+    *h_bad_entry = h_info[1];
+    return TPZ_ERR_INVALID_ARG;
+  }
+  // chunks of at least w entries keep the transfer tables (K x w) within n entries
+  a.phase = 1;
+  a.w = h_info[0];
+  a.chunk = a.w > tpz::kPlanChunk ? a.w : tpz::kPlanChunk;
+  const uint64_t K = (n + (uint64_t)a.chunk - 1) / a.chunk;
+  TPZ_HIP(sc.get(&a.tab_a, K * a.w * 4));
+  TPZ_HIP(sc.get(&a.tab_b, K * a.w * 4));
+  TPZ_HIP(sc.get(&a.cnt, K * 4));
+  a.n_blocks = info + 2;
+  TPZ_HIP(tpz::launch_plan(a, s));
+  TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
+  TPZ_HIP(hipStreamSynchronize(s));
+  *h_n_blocks = h_info[2];
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_first,
+                          const uint64_t* d_ext, uint32_t n_blocks, uint8_t* d_out, void* stream) {
+  if (!c || !en || !d_first || !d_ext || !d_out) return TPZ_ERR_INVALID_ARG;
+  if (n_blocks == 0) return TPZ_SUCCESS;
+  if ((reinterpret_cast<uintptr_t>(d_out) & 15u) || !en->d_kpos || !en->d_vpos ||
+      (!en->d_keys && en->key_bytes) || (!en->d_vals && en->val_bytes))
+    return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  void* ws = nullptr;  // the big-block worklist: stream-ordered, freed behind the kernels
+  TPZ_HIP(hipMallocAsync(&ws, (size_t)n_blocks * 4 + 16, s));
+  tpz::EncodeLaunch a{};
+  a.keys = en->d_keys;
+  a.kpos = en->d_kpos;
+  a.key_bytes = en->key_bytes;
+  a.vals = en->d_vals;
+  a.vpos = en->d_vpos;
+  a.val_bytes = en->val_bytes;
+  a.first = d_first;
+  a.ext = d_ext;
+  a.n_blocks = n_blocks;
+  a.crc_tables = c->d_tables;
+  a.out = d_out;
+  a.big_count = static_cast<uint32_t*>(ws);
+  a.big_list = static_cast<uint32_t*>(ws) + 4;
+  a.num_cus = c->num_cus;
+  const hipError_t e = tpz::launch_encode(a, s);
+  (void)hipFreeAsync(ws, s);
+  TPZ_HIP(e);
+  return TPZ_SUCCESS;
+}
+
 tpz_err tpz_pack_ends(tpz_ctx* c, const tpz_batch* b, const tpz_columns* cols,
                       const uint64_t* d_first, uint32_t* d_dense, void* stream) {
   if (!c || !b || !cols || !d_first || !d_dense) return TPZ_ERR_INVALID_ARG;

@@ -1,0 +1,634 @@
+// tpz_encode.hip — gfx950 kernels for the write side of the block path: SsTableBuilder's block
+// cuts and Block::encode + checksum for a batch of sorted entries (compaction output,
+// src/table/builder.rs:49-85; SURVEY.md §8f row 4's alternative).
+//
+//  plan    BlockBuilder::add (src/block/builder.rs:26-41): an entry joins the current block while
+//          size + encode_len + 2 <= block_size (size = the block's entry bytes so far);
+//          SsTableBuilder::add (src/table/builder.rs:49-64) starts the next block with the entry
+//          that did not fit. The block starts are the chain 0 -> nx[0] -> ... over entries:
+//            plan_next_kernel   nx[a] = entries of a block that starts at entry a (binary search
+//                               over the entries' prefix sums S, closed form from kpos/vpos)
+//            plan_table_kernel  per chunk of C entries (C = max(2048, w)), the chain's exit offset into the
+//                               next chunk for every entry offset it can enter at (< w, the
+//                               longest block in entries)
+//            plan_round_kernel  Hillis-Steele scan of those transfer tables (function
+//                               composition, log2(chunks) rounds): the entry offset of every chunk
+//            plan_count_kernel + plan_scan_kernel + plan_write_kernel: one walk per chunk counts
+//                               and then writes its block starts and byte extents
+//  encode  Block::encode (src/block.rs:31-44) + Entry::encode (src/block/builder.rs:72-81) +
+//          checksum::calculate_checksum (src/checksum.rs:6-10) + compress::encode Uncompress
+//          (src/block/compress.rs:85-89): block b = [u16 n][n x u16 offset][entries][u32 crc]
+//          [tag 1] at ext[b] = S(first[b]) + 2 first[b] + 7 b (a closed form: no prefix pass).
+//            encode_wave_kernel  one wave per block (payload <= 5104 B, every block_size <= 4 KiB
+//                                block): lanes OR their entries into a zeroed LDS window (8-byte
+//                                LDS atomics, so entries shorter than a dword need no ownership
+//                                rules), the decode's CRC (80-B lane runs, slice-by-16, lane tree)
+//                                over the window, then 16-byte stores (the two lines shared with
+//                                the neighbouring blocks are written byte-exact)
+//            encode_big_kernel   one 16-wave workgroup per longer block (block_size <= 64 KiB):
+//                                a wave per entry copies it, 5120-B CRC super-rounds spread over
+//                                the waves and shifted to the end with GF(2) multiplies
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tpz_internal.h"
+
+namespace tpz {
+namespace {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef unsigned __int128 u128;
+
+constexpr int kWave = 64;
+constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB: the decode's CRC tables
+
+// wave path: 16 waves per CU, each with [guard 96][window 5152] (the window holds A (< 16) +
+// payload + crc + tag and the OR spill of the last piece)
+constexpr int kEncWaves = 16;
+constexpr int kEncThreads = kEncWaves * kWave;
+constexpr int kEncGuard = 96;                // zeroed: the CRC's front lane reads <= 79 B before
+constexpr int kEncWin = 5152;
+constexpr u32 kEncMaxP = 5120 - 16;          // one CRC super-round: A + payload + pad <= 5120
+constexpr int kEncSlot = kEncGuard + kEncWin;
+static_assert(kTableBytes + kEncWaves * kEncSlot <= 163840, "encode LDS");
+static_assert(kEncSlot % 16 == 0 && kTableBytes % 16 == 0, "slot alignment");
+
+// big path: one 16-wave workgroup per block, [tables][guard 96][window][wave CRCs]
+constexpr int kBigWaves = 16;
+constexpr int kBigThreads = kBigWaves * kWave;
+constexpr int kBigWin = 121536;
+constexpr u32 kBigMaxP = kBigWin - 48;
+constexpr int kBigSuper = (kBigWin + 5119) / 5120;   // CRC super-rounds
+static_assert(kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves <= 163840, "big encode LDS");
+
+// ------------------------------------------------------------------ small helpers
+__device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ u64 uni64(u64 x) {
+  const u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u32 readlane(u32 x, int l) { return __builtin_amdgcn_readlane(x, l); }
+template <int CTRL>
+__device__ __forceinline__ u32 dpp(u32 x) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+constexpr int kRowShl = 0x100;
+// Orders one wave's LDS accesses across lanes: the LDS executes a wave's instructions in order,
+// so only the compiler has to be kept from moving them.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ u32 be16(u32 x) { return ((x >> 8) & 0xFFu) | ((x & 0xFFu) << 8); }
+
+// ------------------------------------------------------------------ CRC-32 (the decode's tables)
+// tab = kNumCrcTables x 256 u32 in LDS: T_0..T_15 (slice-by-16), shift-by-80*2^j operators at
+// 16 + 4j, the inverse table at kCrcInvTable (tpz_api.cpp builds them; tpz_decode.hip §CRC).
+__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+__device__ __forceinline__ u32 slice16(const u32* tab, u32 w0, u32 w1, u32 w2, u32 w3) {
+  u32 c = xor3(tlook(tab, 15, w0 & 0xFF), tlook(tab, 14, (w0 >> 8) & 0xFF), tlook(tab, 13, (w0 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 12, w0 >> 24), tlook(tab, 11, w1 & 0xFF));
+  c = xor3(c, tlook(tab, 10, (w1 >> 8) & 0xFF), tlook(tab, 9, (w1 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 8, w1 >> 24), tlook(tab, 7, w2 & 0xFF));
+  c = xor3(c, tlook(tab, 6, (w2 >> 8) & 0xFF), tlook(tab, 5, (w2 >> 16) & 0xFF));
+  c = xor3(c, tlook(tab, 4, w2 >> 24), tlook(tab, 3, w3 & 0xFF));
+  c = xor3(c, tlook(tab, 2, (w3 >> 8) & 0xFF), tlook(tab, 1, (w3 >> 16) & 0xFF));
+  return c ^ tlook(tab, 0, w3 >> 24);
+}
+template <int J>
+__device__ __forceinline__ u32 crc_shift(const u32* tab, u32 a) {
+  constexpr int b0 = 16 + 4 * J;
+  return xor3(tlook(tab, b0, a & 0xFF), tlook(tab, b0 + 1, (a >> 8) & 0xFF),
+              tlook(tab, b0 + 2, (a >> 16) & 0xFF)) ^ tlook(tab, b0 + 3, a >> 24);
+}
+// Un-feed k zero bytes (the inverse of appending them; the top byte of T_0[b] determines b).
+__device__ __forceinline__ u32 crc_unshift_small(const u32* tab, u32 r, u32 k) {
+  for (u32 i = 0; i < k; i++) {
+    const u32 b = tlook(tab, kCrcInvTable, r >> 24);
+    r = ((r ^ tlook(tab, 0, b)) << 8) | b;
+  }
+  return r;
+}
+// a * b mod P, reflected (bit 31 = x^0): shifts a super-round's CRC to the block end.
+__device__ __forceinline__ u32 gf_mul(u32 a, u32 b) {
+  u32 p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    p ^= (a & (0x80000000u >> i)) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
+  }
+  return p;
+}
+// The lanes' run CRCs (lane l's run ends 80 l bytes before the end) as one R0: a lane tree of
+// shift-by-80*2^k lookups and DPP row shifts (tpz_decode.hip crc_combine).
+__device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
+  const u32 lane = lane_id();
+  if ((lane & 1u) == 1u) A = crc_shift<0>(tab, A);
+  A ^= dpp<kRowShl + 1>(A);
+  if ((lane & 3u) == 2u) A = crc_shift<1>(tab, A);
+  A ^= dpp<kRowShl + 2>(A);
+  if ((lane & 7u) == 4u) A = crc_shift<2>(tab, A);
+  A ^= dpp<kRowShl + 4>(A);
+  if ((lane & 15u) == 8u) A = crc_shift<3>(tab, A);
+  A ^= dpp<kRowShl + 8>(A);
+  if ((lane & 31u) == 16u) A = crc_shift<4>(tab, A);
+  if ((lane & 47u) == 32u) A = crc_shift<5>(tab, A);
+  return readlane(A, 0) ^ readlane(A, 16) ^ readlane(A, 32) ^ readlane(A, 48);
+}
+// R0 of super-round r of the LDS range [pb, pb + Pa) (pb + Pa 16-byte aligned; 5120-B rounds
+// counted from the end, 80-B lane runs end-aligned; bytes before pb read from zeroed LDS).
+__device__ __forceinline__ u32 round_crc(const u32* tab, const uint8_t* win, int pb, u32 Pa, u32 r) {
+  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+  const int seg = (int)Pa - 5120 * (int)r - kCrcLaneBytes * (int)(lane_id() + 1);
+  u32 c = 0;
+  if (seg + kCrcLaneBytes > 0) {
+#pragma unroll
+    for (int t = 0; t < kCrcLaneBytes / 16; t++) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(win + pb + seg + 16 * t);
+      c = slice16(tab, w.x ^ c, w.y, w.z, w.w);
+    }
+  }
+  return crc_combine(tab, c);
+}
+
+// ------------------------------------------------------------------ LDS byte assembly
+// The window is zeroed first and every byte is OR-ed in exactly once, so lanes writing bytes of
+// one dword need no ordering between them (entries can be 5 bytes long).
+__device__ __forceinline__ void lds_or64(uint8_t* W, u32 g, u64 v) {
+  __hip_atomic_fetch_or(reinterpret_cast<u64*>(W + g), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_xor64(uint8_t* W, u32 g, u64 v) {
+  __hip_atomic_fetch_xor(reinterpret_cast<u64*>(W + g), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// OR the low nb (<= 8) bytes of v into W[d ..)
+__device__ __forceinline__ void or_bytes(uint8_t* W, u32 d, u64 v, u32 nb) {
+  const u32 g = d & ~7u, sh = d & 7u;
+  lds_or64(W, g, v << (8 * sh));
+  if (sh + nb > 8) lds_or64(W, g + 8, v >> (64 - 8 * sh));
+}
+__device__ __forceinline__ void xor_bytes(uint8_t* W, u32 d, u64 v, u32 nb) {
+  const u32 g = d & ~7u, sh = d & 7u;
+  lds_xor64(W, g, v << (8 * sh));
+  if (sh + nb > 8) lds_xor64(W, g + 8, v >> (64 - 8 * sh));
+}
+// OR 16 bytes (lo, hi) into W[d .. d + 16)
+__device__ __forceinline__ void or16(uint8_t* W, u32 d, u64 lo, u64 hi) {
+  const u32 g = d & ~7u, sh = d & 7u;
+  if (sh == 0) {
+    lds_or64(W, g, lo);
+    lds_or64(W, g + 8, hi);
+  } else {
+    lds_or64(W, g, lo << (8 * sh));
+    lds_or64(W, g + 8, (lo >> (64 - 8 * sh)) | (hi << (8 * sh)));
+    lds_or64(W, g + 16, hi >> (64 - 8 * sh));
+  }
+}
+
+// 16 bytes of a global buffer of `size` bytes at offset a; bytes past the buffer read as 0.
+typedef u128 u128_u __attribute__((aligned(1)));
+__device__ __forceinline__ u128 ld16(const uint8_t* base, u64 size, u64 a) {
+  if (a + 16 <= size) return *reinterpret_cast<const u128_u*>(base + a);
+  u128 v = 0;
+  for (u32 i = 0; i < 16 && a + i < size; i++) v |= (u128)base[a + i] << (8 * i);
+  return v;
+}
+__device__ __forceinline__ u128 keep_low(u128 v, u32 m) {   // the low m (<= 16) bytes
+  return m >= 16 ? v : (v & (((u128)1 << (8 * m)) - 1));
+}
+// OR src[0 .. len) (global) into W[d ..): lane-private, 16 bytes per step
+__device__ __forceinline__ void copy_in(uint8_t* W, u32 d, const uint8_t* base, u64 size, u64 s,
+                                        u32 len) {
+  for (u32 t = 0; t < len; t += 16) {
+    const u128 v = keep_low(ld16(base, size, s + t), len - t);
+    or16(W, d + t, (u64)v, (u64)(v >> 64));
+  }
+}
+
+// ------------------------------------------------------------------ parameters
+struct PlanParams {
+  const u64* kpos;
+  const u64* vpos;
+  u32 n;             // entries
+  u32 T;             // block_size - 2: an entry fits while size + encode_len <= T
+  u32 span;          // max(1, T / 5): a block holds at most this many entries (each >= 5 B)
+  u32* nx;           // n
+  u32* info;         // [0] max nx (w), [1] first bad entry (~0u: none), zeroed/set by the host
+  int* tab_a;        // chunk transfer tables, K x w
+  int* tab_b;
+  u32 C;             // entries per chunk (>= w)
+  u32 K;             // chunks
+  u32 w;
+  u32* cnt;          // K: blocks per chunk, then their exclusive prefix
+  u32* first;        // n + 1: block starts
+  u64* ext;          // n + 1: encoded byte extents
+  u32* n_blocks;     // one u32
+};
+
+__device__ __forceinline__ u64 S_at(const u64* kpos, const u64* vpos, u64 k0, u64 v0, u32 x) {
+  return 4ull * x + (kpos[x] - k0) + (vpos[x] - v0);
+}
+
+// ------------------------------------------------------------------ plan kernels
+constexpr u32 kNextWG = 256, kNextWin = 4096;
+
+__global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
+  __shared__ u64 sw[kNextWin];
+  const u32 a0 = blockIdx.x * kNextWG;
+  const u64 k0 = p.kpos[0], v0 = p.vpos[0];
+  const u64 hiw = min((u64)p.n, (u64)a0 + kNextWG - 1 + p.span);   // highest index probed
+  const u32 wn = (u32)(hiw - a0 + 1);
+  const bool in_lds = wn <= kNextWin;
+  if (in_lds)
+    for (u32 i = threadIdx.x; i < wn; i += kNextWG) sw[i] = S_at(p.kpos, p.vpos, k0, v0, a0 + i);
+  __syncthreads();
+  const u32 a = a0 + threadIdx.x;
+  u32 len = 0, bad = ~0u;
+  if (a < p.n) {
+    auto S = [&](u32 x) -> u64 { return in_lds ? sw[x - a0] : S_at(p.kpos, p.vpos, k0, v0, x); };
+    const u64 kl = p.kpos[a + 1] - p.kpos[a], vl = p.vpos[a + 1] - p.vpos[a];
+    if (kl == 0 || 4 + kl + vl > p.T) {   // builder.rs:27 assert / an entry no block holds
+      bad = a;
+      len = 1;
+    } else {
+      const u64 lim = S(a) + p.T;
+      u32 lo = a + 1, hi = (u32)min((u64)p.n, (u64)a + p.span);   // S(lo) <= lim
+      if (S(hi) <= lim) {
+        lo = hi;
+      } else {
+        while (hi - lo > 1) {
+          const u32 mid = lo + (hi - lo) / 2;
+          if (S(mid) <= lim) lo = mid; else hi = mid;
+        }
+      }
+      len = lo - a;
+    }
+    p.nx[a] = len;
+  }
+  for (int o = 32; o; o >>= 1) {
+    len = max(len, (u32)__shfl_xor((int)len, o));
+    bad = min(bad, (u32)__shfl_xor((int)bad, o));
+  }
+  if (lane_id() == 0) {
+    if (len) atomicMax(&p.info[0], len);
+    if (bad != ~0u) atomicMin(&p.info[1], bad);
+  }
+}
+
+// tab_a[k w + j] = where the chain entering chunk k at entry k C + j leaves it: the entry
+// offset into chunk k + 1, or -1 when it reaches the end of the entries first.
+__global__ __launch_bounds__(256) void plan_table_kernel(PlanParams p) {
+  const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (u64)p.K * p.w) return;
+  const u32 k = (u32)(t / p.w), j = (u32)(t % p.w);
+  const u64 c1 = (u64)(k + 1) * p.C;
+  u64 a = (u64)k * p.C + j;
+  int F = -1;
+  if (a < p.n) {
+    const u64 end = min((u64)p.n, c1);
+    while (a < end) a += p.nx[a];
+    F = a >= p.n ? -1 : (int)(a - c1);
+  }
+  p.tab_a[t] = F;
+}
+
+// One Hillis-Steele round: A_k <- A_k o A_{k-d} (tab_a -> tab_b).
+__global__ __launch_bounds__(256) void plan_round_kernel(PlanParams p, u32 d) {
+  const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (u64)p.K * p.w) return;
+  const u32 k = (u32)(t / p.w), j = (u32)(t % p.w);
+  int v = p.tab_a[t];
+  if (k >= d) {
+    const int x = p.tab_a[(u64)(k - d) * p.w + j];
+    v = x < 0 ? -1 : p.tab_a[(u64)k * p.w + x];
+  }
+  p.tab_b[t] = v;
+}
+
+// The chain's entry into chunk k (absolute entry index), or ~0u if it ended before.
+__device__ __forceinline__ u64 chunk_entry(const PlanParams& p, u32 k) {
+  if (k == 0) return 0;
+  const int e = p.tab_a[(u64)(k - 1) * p.w];
+  return e < 0 ? ~0ull : (u64)k * p.C + (u32)e;
+}
+
+__global__ __launch_bounds__(256) void plan_count_kernel(PlanParams p) {
+  const u32 k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= p.K) return;
+  u64 a = chunk_entry(p, k);
+  u32 c = 0;
+  if (a != ~0ull) {
+    const u64 end = min((u64)p.n, (u64)(k + 1) * p.C);
+    for (; a < end; a += p.nx[a]) c++;
+  }
+  p.cnt[k] = c;
+}
+
+// Exclusive prefix of cnt in place (one workgroup); the total goes to *n_blocks.
+__global__ __launch_bounds__(1024) void plan_scan_kernel(PlanParams p) {
+  __shared__ u32 part[1024 / kWave];
+  __shared__ u32 carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const u32 lane = lane_id(), wid = threadIdx.x / kWave;
+  for (u32 base = 0; base < p.K; base += 1024) {
+    const u32 k = base + threadIdx.x;
+    const u32 v = k < p.K ? p.cnt[k] : 0u;
+    u32 x = v;                                   // inclusive wave scan
+    for (int o = 1; o < kWave; o <<= 1) {
+      const u32 y = (u32)__shfl_up((int)x, o);
+      if (lane >= (u32)o) x += y;
+    }
+    if (lane == kWave - 1) part[wid] = x;
+    __syncthreads();
+    u32 before = carry_s;
+    for (u32 w = 0; w < wid; w++) before += part[w];
+    if (k < p.K) p.cnt[k] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *p.n_blocks = carry_s;
+}
+
+__global__ __launch_bounds__(256) void plan_write_kernel(PlanParams p) {
+  const u32 k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= p.K) return;
+  const u64 k0 = p.kpos[0], v0 = p.vpos[0];
+  u64 a = chunk_entry(p, k);
+  u32 b = p.cnt[k];
+  if (a != ~0ull) {
+    const u64 end = min((u64)p.n, (u64)(k + 1) * p.C);
+    for (; a < end; a += p.nx[a], b++) {
+      p.first[b] = (u32)a;
+      p.ext[b] = S_at(p.kpos, p.vpos, k0, v0, (u32)a) + 2 * a + 7ull * b;   // SsTableBuilder data.len()
+    }
+  }
+  if (k + 1 == p.K) {
+    const u32 nb = *p.n_blocks;
+    p.first[nb] = p.n;
+    p.ext[nb] = S_at(p.kpos, p.vpos, k0, v0, p.n) + 2ull * p.n + 7ull * nb;
+  }
+}
+
+// ------------------------------------------------------------------ encode kernels
+struct EncParams {
+  const uint8_t* keys;
+  const u64* kpos;
+  u64 key_bytes;     // readable bytes of keys (kpos[n])
+  const uint8_t* vals;
+  const u64* vpos;
+  u64 val_bytes;
+  const u32* first;  // n_blocks + 1
+  const u64* ext;    // n_blocks + 1
+  u32 n_blocks;
+  const u32* crc_tables;
+  uint8_t* out;      // 16-byte aligned
+  u32* big_list;     // workspace: blocks for encode_big_kernel
+  u32* big_count;    // zeroed before the launch
+  u32 xp[kBigSuper]; // x^(8 * 5120 r) mod P: super-round r's shift to the block end
+};
+
+// Stores W[A, A + len) to out[o0, o0 + len) (o0 & 15 == A): whole 16-byte pieces for the lines
+// inside the block, byte-exact stores for the pieces it shares with its neighbours.
+__device__ __forceinline__ void store_block(const uint8_t* W, uint8_t* out, u64 o0, u32 A, u32 len,
+                                            u32 t0, u32 nt) {
+  const u32 end = A + len, npieces = (end + 15) / 16;
+  uint8_t* g = out + (o0 & ~15ull);
+  for (u32 q = t0; q < npieces; q += nt) {
+    const bool edge = (q == 0 && A != 0) || (q + 1 == npieces && (end & 15u) != 0);
+    const uint4 v = *reinterpret_cast<const uint4*>(W + 16 * q);
+    if (!edge) {
+      *reinterpret_cast<uint4*>(g + 16 * q) = v;
+    } else {
+      const u32 lo = q == 0 ? A : 0u, hi = min(16u, end - 16 * q);
+      for (u32 i = lo; i < hi; i++) g[16 * q + i] = W[16 * q + i];
+    }
+  }
+}
+
+// One block's entries: n (BE u16), the offsets and Entry::encode of each entry, OR-ed into W.
+// Threads t0, t0 + nt, ... take the offsets; entry copies go per thread (wave path).
+__device__ __forceinline__ void put_offsets(const EncParams& p, uint8_t* W, u32 A, u32 a, u32 nb,
+                                            u64 kp0, u64 vp0, u32 t0, u32 nt) {
+  for (u32 i = t0; i < nb; i += nt) {
+    const u32 x = a + i;
+    const u64 off = 4ull * i + (p.kpos[x] - kp0) + (p.vpos[x] - vp0);
+    or_bytes(W, A + 2 + 2 * i, be16((u32)off & 0xFFFFu), 2);   // builder.rs:37 (size as u16)
+  }
+}
+
+constexpr int kEncLds = kTableBytes + kEncWaves * kEncSlot;
+constexpr int kBigEncLds = kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves;
+
+__global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncLds];
+  u32* tab = reinterpret_cast<u32*>(lds);
+  const u32 lane = lane_id(), wid = threadIdx.x / kWave;
+  uint8_t* slot = lds + kTableBytes + wid * kEncSlot;
+  uint8_t* W = slot + kEncGuard;
+  for (int i = threadIdx.x; i < kTableBytes / 16; i += kEncThreads)
+    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(p.crc_tables)[i];
+  for (int i = lane; i < kEncGuard / 16; i += kWave) reinterpret_cast<uint4*>(slot)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const u32 nwaves = gridDim.x * kEncWaves;
+  for (u32 b = blockIdx.x * kEncWaves + wid; b < p.n_blocks; b += nwaves) {
+    const u32 a = p.first[b], e = p.first[b + 1], nb = e - a;
+    const u64 o0 = p.ext[b], len = p.ext[b + 1] - o0;
+    const u32 A = (u32)(o0 & 15);
+    const u32 P = (u32)(len - 5);
+    if (P + A > kEncMaxP) {                              // longer block: the big kernel
+      if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
+      continue;
+    }
+    const u32 kpad = (16 - ((A + P) & 15)) & 15;         // zero bytes up to the 16-byte boundary
+    const u32 zn = (A + P + 5 + 24 + 15) / 16;
+    for (u32 q = lane; q < zn; q += kWave) reinterpret_cast<uint4*>(W)[q] = make_uint4(0, 0, 0, 0);
+    wave_sync();
+    const u64 kp0 = uni64(p.kpos[a]), vp0 = uni64(p.vpos[a]);
+    if (lane == 0) or_bytes(W, A, be16(nb & 0xFFFFu), 2);           // block.rs:35 (n as u16)
+    put_offsets(p, W, A, a, nb, kp0, vp0, lane, kWave);
+    for (u32 i = lane; i < nb; i += kWave) {                        // Entry::encode, builder.rs:72-81
+      const u32 x = a + i;
+      const u64 kp = p.kpos[x], kl = p.kpos[x + 1] - kp, vp = p.vpos[x], vl = p.vpos[x + 1] - vp;
+      const u32 pos = A + 2 + 2 * nb + (u32)(4ull * i + (kp - kp0) + (vp - vp0));
+      or_bytes(W, pos, be16((u32)kl & 0xFFFFu), 2);
+      copy_in(W, pos + 2, p.keys, p.key_bytes, kp, (u32)kl);
+      or_bytes(W, pos + 2 + (u32)kl, be16((u32)vl & 0xFFFFu), 2);
+      copy_in(W, pos + 4 + (u32)kl, p.vals, p.val_bytes, vp, (u32)vl);
+    }
+    wave_sync();
+    // checksum::calculate_checksum over the payload: init 0xFFFFFFFF folded into its first four
+    // bytes, raw CRC of payload || 0^kpad, un-shifted, complemented
+    if (lane == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
+    wave_sync();
+    const u32 R = round_crc(tab, slot, kEncGuard + (int)A, P + kpad, 0);
+    wave_sync();
+    const u32 crc = ~crc_unshift_small(tab, R, kpad);
+    if (lane == 0) {
+      xor_bytes(W, A, 0xFFFFFFFFull, 4);
+      or_bytes(W, A + P, __builtin_bswap32(crc), 4);               // block.rs:42 (put_u32, BE)
+      or_bytes(W, A + P + 4, 1, 1);                                 // compress.rs:87 Uncompress tag
+    }
+    wave_sync();
+    store_block(W, p.out, o0, A, P + 5, lane, kWave);
+    wave_sync();
+  }
+}
+
+__global__ __launch_bounds__(kBigThreads) void encode_big_kernel(EncParams p) {
+  const u32 cnt = uni(*p.big_count);
+  if (cnt == 0) return;                                  // before loading the tables
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kBigEncLds];
+  u32* tab = reinterpret_cast<u32*>(lds);
+  uint8_t* slot = lds + kTableBytes;
+  uint8_t* W = slot + kEncGuard;
+  u32* wcrc = reinterpret_cast<u32*>(W + kBigWin);
+  const u32 lane = lane_id(), wid = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < kTableBytes / 16; i += kBigThreads)
+    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(p.crc_tables)[i];
+  for (int i = threadIdx.x; i < kEncGuard / 16; i += kBigThreads) reinterpret_cast<uint4*>(slot)[i] = make_uint4(0, 0, 0, 0);
+  for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const u32 b = p.big_list[it];
+    const u32 a = p.first[b], e = p.first[b + 1], nb = e - a;
+    const u64 o0 = p.ext[b], len = p.ext[b + 1] - o0;
+    const u32 A = (u32)(o0 & 15);
+    const u32 P = (u32)(len - 5);
+    if (P + A > kBigMaxP) continue;                      // rejected by tpz_plan_blocks (block_size)
+    const u32 kpad = (16 - ((A + P) & 15)) & 15;
+    const u32 zn = (A + P + 5 + 24 + 15) / 16;
+    __syncthreads();                                     // the previous block's store read W
+    for (u32 q = threadIdx.x; q < zn; q += kBigThreads) reinterpret_cast<uint4*>(W)[q] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const u64 kp0 = p.kpos[a], vp0 = p.vpos[a];
+    if (threadIdx.x == 0) or_bytes(W, A, be16(nb & 0xFFFFu), 2);
+    put_offsets(p, W, A, a, nb, kp0, vp0, threadIdx.x, kBigThreads);
+    for (u32 i = wid; i < nb; i += kBigWaves) {          // one wave per entry, 16-B pieces per lane
+      const u32 x = a + i;
+      const u64 kp = p.kpos[x], kl = p.kpos[x + 1] - kp, vp = p.vpos[x], vl = p.vpos[x + 1] - vp;
+      const u32 pos = A + 2 + 2 * nb + (u32)(4ull * i + (kp - kp0) + (vp - vp0));
+      if (lane == 0) {
+        or_bytes(W, pos, be16((u32)kl & 0xFFFFu), 2);
+        or_bytes(W, pos + 2 + (u32)kl, be16((u32)vl & 0xFFFFu), 2);
+      }
+      for (u32 t = 16 * lane; t < kl; t += 16 * kWave) {
+        const u128 v = keep_low(ld16(p.keys, p.key_bytes, kp + t), (u32)kl - t);
+        or16(W, pos + 2 + t, (u64)v, (u64)(v >> 64));
+      }
+      for (u32 t = 16 * lane; t < vl; t += 16 * kWave) {
+        const u128 v = keep_low(ld16(p.vals, p.val_bytes, vp + t), (u32)vl - t);
+        or16(W, pos + 4 + (u32)kl + t, (u64)v, (u64)(v >> 64));
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
+    __syncthreads();
+    const u32 Pa = P + kpad, Sr = (Pa + 5119) / 5120;
+    u32 acc = 0;
+    for (u32 r = wid; r < Sr; r += kBigWaves) acc ^= gf_mul(p.xp[r], round_crc(tab, slot, kEncGuard + (int)A, Pa, r));
+    if (lane == 0) wcrc[wid] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u32 R = 0;
+      for (int w = 0; w < kBigWaves; w++) R ^= wcrc[w];
+      const u32 crc = ~crc_unshift_small(tab, R, kpad);
+      xor_bytes(W, A, 0xFFFFFFFFull, 4);
+      or_bytes(W, A + P, __builtin_bswap32(crc), 4);
+      or_bytes(W, A + P + 4, 1, 1);
+    }
+    __syncthreads();
+    store_block(W, p.out, o0, A, P + 5, threadIdx.x, kBigThreads);
+  }
+}
+
+// ------------------------------------------------------------------ host side
+u32 gf_mul_host(u32 a, u32 b) {
+  u32 p = 0;
+  for (int i = 0; i < 32; i++) {
+    if (a & (0x80000000u >> i)) p ^= b;
+    b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
+  }
+  return p;
+}
+u32 x8n_host(u64 n) {                    // x^(8n) mod P, reflected
+  u32 r = 0x80000000u, sq = 0x00800000u;  // x^0, x^8
+  for (; n; n >>= 1) {
+    if (n & 1u) r = gf_mul_host(r, sq);
+    sq = gf_mul_host(sq, sq);
+  }
+  return r;
+}
+
+}  // namespace
+
+hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
+  PlanParams p{};
+  p.kpos = a.kpos;
+  p.vpos = a.vpos;
+  p.n = a.n;
+  p.T = a.block_size - 2;
+  p.span = p.T / 5 ? p.T / 5 : 1;
+  p.nx = a.nx;
+  p.info = a.info;
+  p.first = a.first;
+  p.ext = a.ext;
+  p.n_blocks = a.n_blocks;
+  p.cnt = a.cnt;
+  p.C = a.chunk ? a.chunk : 1;
+  p.K = (u32)(((u64)a.n + p.C - 1) / p.C);
+  hipError_t e;
+  if (a.phase == 0) {
+    plan_next_kernel<<<(a.n + kNextWG - 1) / kNextWG, kNextWG, 0, s>>>(p);
+    return hipGetLastError();
+  }
+  p.w = a.w;
+  const u64 tn = (u64)p.K * p.w;
+  const u32 tg = (u32)((tn + 255) / 256);
+  p.tab_a = a.tab_a;
+  p.tab_b = a.tab_b;
+  plan_table_kernel<<<tg, 256, 0, s>>>(p);
+  for (u32 d = 1; d < p.K; d <<= 1) {
+    plan_round_kernel<<<tg, 256, 0, s>>>(p, d);
+    int* t = p.tab_a;
+    p.tab_a = p.tab_b;
+    p.tab_b = t;
+  }
+  const u32 kg = (p.K + 255) / 256;
+  plan_count_kernel<<<kg, 256, 0, s>>>(p);
+  plan_scan_kernel<<<1, 1024, 0, s>>>(p);
+  plan_write_kernel<<<kg, 256, 0, s>>>(p);
+  e = hipGetLastError();
+  return e;
+}
+
+hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
+  EncParams p{};
+  p.keys = a.keys;
+  p.kpos = a.kpos;
+  p.key_bytes = a.key_bytes;
+  p.vals = a.vals;
+  p.vpos = a.vpos;
+  p.val_bytes = a.val_bytes;
+  p.first = a.first;
+  p.ext = a.ext;
+  p.n_blocks = a.n_blocks;
+  p.crc_tables = a.crc_tables;
+  p.out = a.out;
+  p.big_list = a.big_list;
+  p.big_count = a.big_count;
+  for (int r = 0; r < kBigSuper; r++) p.xp[r] = x8n_host(5120ull * r);
+  hipError_t e = hipMemsetAsync(a.big_count, 0, 4, s);
+  if (e != hipSuccess) return e;
+  const u32 grid = a.num_cus;
+  encode_wave_kernel<<<grid, kEncThreads, 0, s>>>(p);
+  encode_big_kernel<<<grid, kBigThreads, 0, s>>>(p);
+  return hipGetLastError();
+}
+
+u32 encode_max_payload() { return kBigMaxP; }
+
+}  // namespace tpz

@@ -200,4 +200,44 @@ struct CodecLaunch {
 void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream);
 void launch_decompress(const CodecLaunch& a, hipStream_t stream);
 
+// The write side (tpz_encode.hip): block cuts (phase 0: nx + info; phase 1: the chain) and the
+// block encode.
+struct PlanLaunch {
+  int phase;
+  const uint64_t* kpos;
+  const uint64_t* vpos;
+  uint32_t n;
+  uint32_t block_size;
+  uint32_t* nx;        // workspace: n
+  uint32_t* info;      // workspace: {max nx, first bad entry}
+  uint32_t w;          // phase 1: info[0]
+  uint32_t chunk;      // phase 1: entries per chunk (>= w)
+  int* tab_a;          // phase 1 workspace: 2 x K x w
+  int* tab_b;
+  uint32_t* cnt;       // phase 1 workspace: K
+  uint32_t* first;
+  uint64_t* ext;
+  uint32_t* n_blocks;  // workspace: one u32
+};
+hipError_t launch_plan(const PlanLaunch& a, hipStream_t stream);
+constexpr uint32_t kPlanChunk = 2048;  // minimum entries per plan chunk
+
+struct EncodeLaunch {
+  const uint8_t* keys;
+  const uint64_t* kpos;
+  uint64_t key_bytes;
+  const uint8_t* vals;
+  const uint64_t* vpos;
+  uint64_t val_bytes;
+  const uint32_t* first;
+  const uint64_t* ext;
+  uint32_t n_blocks;
+  const uint32_t* crc_tables;
+  uint8_t* out;
+  uint32_t* big_list;   // workspace: n_blocks
+  uint32_t* big_count;  // workspace: one u32
+  uint32_t num_cus;
+};
+hipError_t launch_encode(const EncodeLaunch& a, hipStream_t stream);
+
 }  // namespace tpz
