@@ -492,6 +492,43 @@ def codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, steps: int = 
             "gib_s_uncompressed": round(int(ext[nb]) / t / GIB, 1)}
 
 
+def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, block_size: int,
+                dev, steps: int = 10) -> dict:
+    """The device write side (SURVEY.md §8f row 4's alternative, compaction output) on the
+    shard's own entries: tpz_plan_blocks (BlockBuilder's fill rule, synchronous: host wall
+    clock) and tpz_encode_blocks (Block::encode + CRC + tag, HIP events). The encoded region
+    must equal the shard's blocks byte for byte. Algorithmic bytes: keys + values + kpos/vpos
+    (16 B per entry) + first/ext (12 B per block) read, the region written. Not the metric."""
+    from topazdb_amd.encode import DeviceEntries, encode_blocks, plan_blocks
+    keys, kpos, vals, vpos = gen
+    etot = int(n_ent.sum())
+    nb = len(ext) - 1
+    ent = DeviceEntries(keys, kpos[:etot + 1], vals, vpos[:etot + 1], dev.index)
+    first, dext, nb2 = plan_blocks(ctx, ent, block_size)
+    assert nb2 == nb and np.array_equal(dext[:nb + 1].cpu().numpy().view(np.uint64), ext)
+    out = torch.empty(int(ext[-1]) + 16, dtype=torch.uint8, device=dev)
+    encode_blocks(ctx, ent, first, dext, nb, out=out)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(out[:int(ext[-1])].cpu(), torch.from_numpy(src[:int(ext[-1])])), "encoded bytes"
+    t0 = time.perf_counter()
+    for _ in range(3):
+        plan_blocks(ctx, ent, block_size)
+    ms_plan = (time.perf_counter() - t0) / 3 * 1e3
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        encode_blocks(ctx, ent, first, dext, nb, out=out)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    alg = int(kpos[etot] - kpos[0]) + int(vpos[etot] - vpos[0]) + 16 * etot + 12 * nb + int(ext[-1])
+    return {"entries": etot, "blocks": nb, "ms_plan": round(ms_plan, 3), "ms_encode": round(ms, 4),
+            "gib_s_encoded": round(int(ext[-1]) / (ms * 1e-3) / GIB, 1),
+            "algorithmic_bytes": alg, "achieved_gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
+            "frac_of_8tb": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 DEFAULT_BLOCKS = {"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}
 
 
@@ -634,6 +671,7 @@ def main():
     ap.add_argument("--no-snappy", action="store_true")
     ap.add_argument("--no-lz4", action="store_true")
     ap.add_argument("--no-seek", action="store_true")
+    ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -731,6 +769,13 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"seek measurement failed: {ex}")
 
+    encode = None
+    if side and not args.no_encode:
+        try:
+            encode = encode_rate(ctx, src, ext, gen, n_ent, synth.CONFIGS[args.config]["block_size"], dev)
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"encode measurement failed: {ex}")
+
     snappy = lz4 = None
     if side and not args.no_snappy:
         try:
@@ -800,6 +845,7 @@ def main():
             "seek": seek,
             "snappy": snappy,
             "lz4": lz4,
+            "encode": encode,
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -424,15 +424,18 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filt
 }
 
 namespace {
-// Device scratch of one write-side call, freed on every exit path.
+// Device scratch of one write-side call: stream-ordered (the pool keeps the memory between
+// calls), freed on every exit path.
 struct DevScratch {
+  hipStream_t s;
   std::vector<void*> p;
+  explicit DevScratch(hipStream_t st) : s(st) {}
   ~DevScratch() {
-    for (void* x : p) (void)hipFree(x);
+    for (void* x : p) (void)hipFreeAsync(x, s);
   }
   hipError_t get(void* out, size_t bytes) {  // out: a T** for any T
     void* d = nullptr;
-    hipError_t e = hipMalloc(&d, bytes ? bytes : 16);
+    hipError_t e = hipMallocAsync(&d, bytes ? bytes : 16, s);
     if (e == hipSuccess) p.push_back(d);
     std::memcpy(out, &d, sizeof d);
     return e;
@@ -458,9 +461,9 @@ tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, 
     return TPZ_SUCCESS;
   }
   if (!en->d_kpos || !en->d_vpos) return TPZ_ERR_INVALID_ARG;
-  DevScratch sc;
+  DevScratch sc(s);
   uint32_t *nx = nullptr, *info = nullptr;
-  TPZ_HIP(sc.get(&nx, (size_t)n * 4));
+  TPZ_HIP(sc.get(&nx, ((size_t)n + n / 2048 + 2) * 4));   // nx, then per-workgroup maxima
   TPZ_HIP(sc.get(&info, 16));
   uint32_t h_info[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
   TPZ_HIP(hipMemcpyAsync(info, h_info, 16, hipMemcpyHostToDevice, s));

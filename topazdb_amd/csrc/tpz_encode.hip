@@ -217,6 +217,7 @@ struct PlanParams {
   u32 span;          // max(1, T / 5): a block holds at most this many entries (each >= 5 B)
   u32* nx;           // n
   u32* info;         // [0] max nx (w), [1] first bad entry (~0u: none), zeroed/set by the host
+  u32* wgmax;        // phase 0: per-workgroup max nx
   int* tab_a;        // chunk transfer tables, K x w
   int* tab_b;
   u32 C;             // entries per chunk (>= w)
@@ -233,25 +234,30 @@ __device__ __forceinline__ u64 S_at(const u64* kpos, const u64* vpos, u64 k0, u6
 }
 
 // ------------------------------------------------------------------ plan kernels
-constexpr u32 kNextWG = 256, kNextWin = 4096;
+// A workgroup takes kNextPer consecutive entries; the prefix sums its binary searches probe
+// (its entries + span) are staged in LDS once. The longest block (w) is reduced per workgroup into
+// wgmax[] (a single-address atomic per wave saturated at ~88 per microsecond: 6.4 ms for 2^20
+// blocks), then by plan_reduce_kernel.
+constexpr u32 kNextWG = 256, kNextPer = 2048, kNextWin = 4096;
 
 __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
   __shared__ u64 sw[kNextWin];
-  const u32 a0 = blockIdx.x * kNextWG;
+  __shared__ u32 wmax[kNextWG / kWave];
+  const u32 a0 = blockIdx.x * kNextPer;
   const u64 k0 = p.kpos[0], v0 = p.vpos[0];
-  const u64 hiw = min((u64)p.n, (u64)a0 + kNextWG - 1 + p.span);   // highest index probed
+  const u64 hiw = min((u64)p.n, (u64)a0 + kNextPer - 1 + p.span);   // highest index probed
   const u32 wn = (u32)(hiw - a0 + 1);
   const bool in_lds = wn <= kNextWin;
   if (in_lds)
     for (u32 i = threadIdx.x; i < wn; i += kNextWG) sw[i] = S_at(p.kpos, p.vpos, k0, v0, a0 + i);
   __syncthreads();
-  const u32 a = a0 + threadIdx.x;
-  u32 len = 0, bad = ~0u;
-  if (a < p.n) {
-    auto S = [&](u32 x) -> u64 { return in_lds ? sw[x - a0] : S_at(p.kpos, p.vpos, k0, v0, x); };
+  auto S = [&](u32 x) -> u64 { return in_lds ? sw[x - a0] : S_at(p.kpos, p.vpos, k0, v0, x); };
+  u32 mx = 0, bad = ~0u;
+  for (u32 a = a0 + threadIdx.x; a < min((u64)p.n, (u64)a0 + kNextPer); a += kNextWG) {
     const u64 kl = p.kpos[a + 1] - p.kpos[a], vl = p.vpos[a + 1] - p.vpos[a];
+    u32 len;
     if (kl == 0 || 4 + kl + vl > p.T) {   // builder.rs:27 assert / an entry no block holds
-      bad = a;
+      bad = min(bad, a);
       len = 1;
     } else {
       const u64 lim = S(a) + p.T;
@@ -267,14 +273,36 @@ __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
       len = lo - a;
     }
     p.nx[a] = len;
+    mx = max(mx, len);
   }
   for (int o = 32; o; o >>= 1) {
-    len = max(len, (u32)__shfl_xor((int)len, o));
+    mx = max(mx, (u32)__shfl_xor((int)mx, o));
     bad = min(bad, (u32)__shfl_xor((int)bad, o));
   }
-  if (lane_id() == 0) {
-    if (len) atomicMax(&p.info[0], len);
-    if (bad != ~0u) atomicMin(&p.info[1], bad);
+  const u32 lane = lane_id(), wid = threadIdx.x / kWave;
+  if (lane == 0) {
+    wmax[wid] = mx;
+    if (bad != ~0u) atomicMin(&p.info[1], bad);    // only for inputs the reference rejects
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 m = 0;
+    for (u32 w = 0; w < kNextWG / kWave; w++) m = max(m, wmax[w]);
+    p.wgmax[blockIdx.x] = m;
+  }
+}
+
+// info[0] = the longest block in entries (max over wgmax), one workgroup.
+__global__ __launch_bounds__(1024) void plan_reduce_kernel(PlanParams p, u32 n_wg) {
+  __shared__ u32 part[1024 / kWave];
+  u32 m = 0;
+  for (u32 i = threadIdx.x; i < n_wg; i += 1024) m = max(m, p.wgmax[i]);
+  for (int o = 32; o; o >>= 1) m = max(m, (u32)__shfl_xor((int)m, o));
+  if (lane_id() == 0) part[threadIdx.x / kWave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (u32 w = 0; w < 1024 / kWave; w++) m = max(m, part[w]);
+    p.info[0] = m;
   }
 }
 
@@ -582,7 +610,10 @@ hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
   p.K = (u32)(((u64)a.n + p.C - 1) / p.C);
   hipError_t e;
   if (a.phase == 0) {
-    plan_next_kernel<<<(a.n + kNextWG - 1) / kNextWG, kNextWG, 0, s>>>(p);
+    const u32 nwg = (u32)(((u64)a.n + kNextPer - 1) / kNextPer);
+    p.wgmax = a.nx + a.n;                 // the caller sizes nx for n + n / 2048 + 1 words
+    plan_next_kernel<<<nwg, kNextWG, 0, s>>>(p);
+    plan_reduce_kernel<<<1, 1024, 0, s>>>(p, nwg);
     return hipGetLastError();
   }
   p.w = a.w;

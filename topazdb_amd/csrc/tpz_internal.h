@@ -208,7 +208,7 @@ struct PlanLaunch {
   const uint64_t* vpos;
   uint32_t n;
   uint32_t block_size;
-  uint32_t* nx;        // workspace: n
+  uint32_t* nx;        // workspace: n + n / 2048 + 2 (nx, then per-workgroup maxima)
   uint32_t* info;      // workspace: {max nx, first bad entry}
   uint32_t w;          // phase 1: info[0]
   uint32_t chunk;      // phase 1: entries per chunk (>= w)

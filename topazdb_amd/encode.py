@@ -83,13 +83,13 @@ def plan_blocks(ctx: Context, ent: DeviceEntries, block_size: int,
 def encode_blocks(ctx: Context, ent: DeviceEntries, first: torch.Tensor, ext: torch.Tensor,
                   n_blocks: int, out: torch.Tensor | None = None,
                   stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """tpz_encode_blocks (asynchronous): the data region, ext[n_blocks] bytes (uint8 tensor)."""
+    """tpz_encode_blocks (asynchronous): the data region, ext[n_blocks] bytes (uint8 tensor;
+    `out`, if given, must hold ext[n_blocks] bytes)."""
     dev = _dev(ctx.device)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
-    total = int(ext[n_blocks]) if n_blocks else 0
-    if out is None:
+    if out is None:   # (a caller that passes `out` avoids this device read of the length)
+        total = int(ext[n_blocks]) if n_blocks else 0
         out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
-    assert out.numel() >= total
     ctx.encode_blocks_ptrs(ent.struct(), first.data_ptr(), ext.data_ptr(), n_blocks,
                            out.data_ptr(), s.cuda_stream)
     return out
