@@ -66,10 +66,6 @@ static_assert(kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves <= 163840, "big 
 // ------------------------------------------------------------------ small helpers
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ u64 uni64(u64 x) {
-  const u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
-  return ((u64)hi << 32) | lo;
-}
 __device__ __forceinline__ u32 readlane(u32 x, int l) { return __builtin_amdgcn_readlane(x, l); }
 template <int CTRL>
 __device__ __forceinline__ u32 dpp(u32 x) {
@@ -452,6 +448,55 @@ __device__ __forceinline__ void put_offsets(const EncParams& p, uint8_t* W, u32 
 constexpr int kEncLds = kTableBytes + kEncWaves * kEncSlot;
 constexpr int kBigEncLds = kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves;
 
+// The wave path keeps three blocks in flight per wave: block i is assembled from pieces loaded
+// during block i - 1, the pieces of block i + 1 are issued as soon as block i's are in LDS (their
+// kpos/vpos arrived during block i - 1), and block i + 2's kpos/vpos are issued at the start of
+// block i; the blocks' first/ext come 64 blocks at a time (lane l: the wave's block g*64 + l).
+constexpr int kPre = 8;                      // prefetched 16-B pieces per lane (key, then value)
+
+struct EntryRegs {                           // the lane's entry in a block's first 64
+  u64 kp, vp;                                // kpos[x], vpos[x]
+  u32 kl, vl;                                // its key and value lengths (< 2^16 in any block)
+};
+
+__device__ __forceinline__ EntryRegs load_entry(const EncParams& p, u32 a, u32 e, bool live) {
+  const u32 x = a + lane_id();
+  EntryRegs r{0, 0, 0, 0};
+  if (live && x < e) {
+    r.kp = p.kpos[x];
+    r.kl = (u32)(p.kpos[x + 1] - r.kp);
+    r.vp = p.vpos[x];
+    r.vl = (u32)(p.vpos[x + 1] - r.vp);
+  }
+  return r;
+}
+
+// piece k of the lane's entry: key pieces (nk of them), then value pieces
+__device__ __forceinline__ u128 load_piece(const EncParams& p, const EntryRegs& r, u32 nk, u32 k) {
+  return k < nk ? ld16(p.keys, p.key_bytes, r.kp + 16ull * k)
+                : ld16(p.vals, p.val_bytes, r.vp + 16ull * (k - nk));
+}
+
+__device__ __forceinline__ void issue_pieces(const EncParams& p, const EntryRegs& r, u128 (&pf)[kPre]) {
+  const u32 nk = (r.kl + 15) / 16, nt = nk + (r.vl + 15) / 16;
+#pragma unroll
+  for (int k = 0; k < kPre; k++) pf[k] = (u32)k < nt ? load_piece(p, r, nk, k) : (u128)0;
+}
+
+// OR piece k (value v) of an entry whose klen field sits at W[pos] into the window
+__device__ __forceinline__ void emit_piece(uint8_t* W, u32 pos, u64 kl, u64 vl, u32 nk, u32 k, u128 v) {
+  const bool key = k < nk;
+  const u32 j = key ? k : k - nk;
+  const u32 rem = (u32)((key ? kl : vl) - 16ull * j);
+  v = keep_low(v, rem);
+  or16(W, pos + (key ? 2u : 4u + (u32)kl) + 16 * j, (u64)v, (u64)(v >> 64));
+}
+
+struct BlockMeta {
+  u32 a, e;
+  u64 o0, o1;
+};
+
 __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncLds];
   u32* tab = reinterpret_cast<u32*>(lds);
@@ -464,47 +509,114 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
   __syncthreads();
 
   const u32 nwaves = gridDim.x * kEncWaves;
-  for (u32 b = blockIdx.x * kEncWaves + wid; b < p.n_blocks; b += nwaves) {
-    const u32 a = p.first[b], e = p.first[b + 1], nb = e - a;
-    const u64 o0 = p.ext[b], len = p.ext[b + 1] - o0;
+  const u32 wv = blockIdx.x * kEncWaves + wid;
+  if (wv >= p.n_blocks) return;
+  const u32 nmine = (p.n_blocks - 1 - wv) / nwaves + 1;     // blocks wv + i * nwaves
+
+  auto load_group = [&](u32 g, BlockMeta& m) {
+    const u32 i = g * kWave + lane;
+    if (i < nmine) {
+      const u32 b = wv + i * nwaves;
+      m.a = p.first[b];
+      m.e = p.first[b + 1];
+      m.o0 = p.ext[b];
+      m.o1 = p.ext[b + 1];
+    }
+  };
+  auto pick = [&](const BlockMeta& m, u32 l) {
+    BlockMeta r;
+    r.a = readlane(m.a, (int)l);
+    r.e = readlane(m.e, (int)l);
+    r.o0 = ((u64)readlane((u32)(m.o0 >> 32), (int)l) << 32) | readlane((u32)m.o0, (int)l);
+    r.o1 = ((u64)readlane((u32)(m.o1 >> 32), (int)l) << 32) | readlane((u32)m.o1, (int)l);
+    return r;
+  };
+  BlockMeta gA{0, 0, 0, 0}, gB{0, 0, 0, 0};                 // groups i / 64 and i / 64 + 1
+  load_group(0, gA);
+  load_group(1, gB);
+  auto meta_of = [&](u32 j, u32 g) { return (j / kWave == g) ? pick(gA, j & 63) : pick(gB, j & 63); };
+
+  BlockMeta m0 = meta_of(0, 0), m1 = meta_of(1 < nmine ? 1 : 0, 0);
+  EntryRegs cur = load_entry(p, m0.a, m0.e, true);
+  EntryRegs nxt = load_entry(p, m1.a, m1.e, 1 < nmine);
+  u128 pf[kPre];
+  issue_pieces(p, cur, pf);
+
+  for (u32 i = 0; i < nmine; i++) {
+    const u32 g = i / kWave;
+    if (i && (i & 63) == 0) {
+      gA = gB;
+      load_group(g + 1, gB);
+    }
+    const BlockMeta m = meta_of(i, g);
+    const bool has2 = i + 2 < nmine;
+    const BlockMeta m2 = meta_of(has2 ? i + 2 : i, g);
+    const EntryRegs nn = load_entry(p, m2.a, m2.e, has2);   // block i + 2's kpos / vpos
+
+    const u32 b = wv + i * nwaves;
+    const u32 a = m.a, nb = m.e - m.a;
+    const u64 o0 = m.o0;
     const u32 A = (u32)(o0 & 15);
-    const u32 P = (u32)(len - 5);
-    if (P + A > kEncMaxP) {                              // longer block: the big kernel
+    const u32 P = (u32)(m.o1 - o0 - 5);
+    const bool small = P + A <= kEncMaxP;
+    if (small) {
+      const u32 kpad = (16 - ((A + P) & 15)) & 15;       // zero bytes up to the 16-byte boundary
+      const u32 zn = (A + P + 5 + 24 + 15) / 16;
+      for (u32 q = lane; q < zn; q += kWave) reinterpret_cast<uint4*>(W)[q] = make_uint4(0, 0, 0, 0);
+      wave_sync();
+      const u64 kp0 = ((u64)readlane((u32)(cur.kp >> 32), 0) << 32) | readlane((u32)cur.kp, 0);
+      const u64 vp0 = ((u64)readlane((u32)(cur.vp >> 32), 0) << 32) | readlane((u32)cur.vp, 0);
+      if (lane == 0) or_bytes(W, A, be16(nb & 0xFFFFu), 2);         // block.rs:35 (n as u16)
+      {                                                              // entries 0..63 from registers
+        const u64 kl = cur.kl, vl = cur.vl;
+        if (lane < nb) {
+          const u64 off = 4ull * lane + (cur.kp - kp0) + (cur.vp - vp0);
+          or_bytes(W, A + 2 + 2 * lane, be16((u32)off & 0xFFFFu), 2);   // builder.rs:37
+          const u32 pos = A + 2 + 2 * nb + (u32)off;
+          or_bytes(W, pos, be16((u32)kl & 0xFFFFu), 2);               // Entry::encode
+          or_bytes(W, pos + 2 + (u32)kl, be16((u32)vl & 0xFFFFu), 2);
+          const u32 nk = (u32)((kl + 15) / 16), nt = nk + (u32)((vl + 15) / 16);
+#pragma unroll
+          for (int k = 0; k < kPre; k++)
+            if ((u32)k < nt) emit_piece(W, pos, kl, vl, nk, k, pf[k]);
+          for (u32 k = kPre; k < nt; k++) emit_piece(W, pos, kl, vl, nk, k, load_piece(p, cur, nk, k));
+        }
+      }
+      if (nb > kWave) {                                              // entries 64.. (tiny entries)
+        put_offsets(p, W, A, a, nb, kp0, vp0, kWave + lane, kWave);
+        for (u32 i2 = kWave + lane; i2 < nb; i2 += kWave) {
+          const u32 x = a + i2;
+          const u64 kp = p.kpos[x], kl = p.kpos[x + 1] - kp, vp = p.vpos[x], vl = p.vpos[x + 1] - vp;
+          const u32 pos = A + 2 + 2 * nb + (u32)(4ull * i2 + (kp - kp0) + (vp - vp0));
+          or_bytes(W, pos, be16((u32)kl & 0xFFFFu), 2);
+          copy_in(W, pos + 2, p.keys, p.key_bytes, kp, (u32)kl);
+          or_bytes(W, pos + 2 + (u32)kl, be16((u32)vl & 0xFFFFu), 2);
+          copy_in(W, pos + 4 + (u32)kl, p.vals, p.val_bytes, vp, (u32)vl);
+        }
+      }
+      wave_sync();
+      issue_pieces(p, nxt, pf);                                      // block i + 1's pieces
+      // checksum::calculate_checksum over the payload: init 0xFFFFFFFF folded into its first
+      // four bytes, raw CRC of payload || 0^kpad, un-shifted, complemented
+      if (lane == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
+      wave_sync();
+      const u32 R = round_crc(tab, slot, kEncGuard + (int)A, P + kpad, 0);
+      wave_sync();
+      const u32 crc = ~crc_unshift_small(tab, R, kpad);
+      if (lane == 0) {
+        xor_bytes(W, A, 0xFFFFFFFFull, 4);
+        or_bytes(W, A + P, __builtin_bswap32(crc), 4);               // block.rs:42 (put_u32, BE)
+        or_bytes(W, A + P + 4, 1, 1);                                 // compress.rs:87 tag
+      }
+      wave_sync();
+      store_block(W, p.out, o0, A, P + 5, lane, kWave);
+      wave_sync();
+    } else {                                                         // longer block: big kernel
       if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
-      continue;
+      issue_pieces(p, nxt, pf);
     }
-    const u32 kpad = (16 - ((A + P) & 15)) & 15;         // zero bytes up to the 16-byte boundary
-    const u32 zn = (A + P + 5 + 24 + 15) / 16;
-    for (u32 q = lane; q < zn; q += kWave) reinterpret_cast<uint4*>(W)[q] = make_uint4(0, 0, 0, 0);
-    wave_sync();
-    const u64 kp0 = uni64(p.kpos[a]), vp0 = uni64(p.vpos[a]);
-    if (lane == 0) or_bytes(W, A, be16(nb & 0xFFFFu), 2);           // block.rs:35 (n as u16)
-    put_offsets(p, W, A, a, nb, kp0, vp0, lane, kWave);
-    for (u32 i = lane; i < nb; i += kWave) {                        // Entry::encode, builder.rs:72-81
-      const u32 x = a + i;
-      const u64 kp = p.kpos[x], kl = p.kpos[x + 1] - kp, vp = p.vpos[x], vl = p.vpos[x + 1] - vp;
-      const u32 pos = A + 2 + 2 * nb + (u32)(4ull * i + (kp - kp0) + (vp - vp0));
-      or_bytes(W, pos, be16((u32)kl & 0xFFFFu), 2);
-      copy_in(W, pos + 2, p.keys, p.key_bytes, kp, (u32)kl);
-      or_bytes(W, pos + 2 + (u32)kl, be16((u32)vl & 0xFFFFu), 2);
-      copy_in(W, pos + 4 + (u32)kl, p.vals, p.val_bytes, vp, (u32)vl);
-    }
-    wave_sync();
-    // checksum::calculate_checksum over the payload: init 0xFFFFFFFF folded into its first four
-    // bytes, raw CRC of payload || 0^kpad, un-shifted, complemented
-    if (lane == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
-    wave_sync();
-    const u32 R = round_crc(tab, slot, kEncGuard + (int)A, P + kpad, 0);
-    wave_sync();
-    const u32 crc = ~crc_unshift_small(tab, R, kpad);
-    if (lane == 0) {
-      xor_bytes(W, A, 0xFFFFFFFFull, 4);
-      or_bytes(W, A + P, __builtin_bswap32(crc), 4);               // block.rs:42 (put_u32, BE)
-      or_bytes(W, A + P + 4, 1, 1);                                 // compress.rs:87 Uncompress tag
-    }
-    wave_sync();
-    store_block(W, p.out, o0, A, P + 5, lane, kWave);
-    wave_sync();
+    cur = nxt;
+    nxt = nn;
   }
 }
 
