@@ -1104,7 +1104,7 @@ __global__ __launch_bounds__(256) void codec_lane_kernel(CodecParams p) {
 __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u32& elems) {
   if (b >= p.n_blocks) return;
 #ifndef TPZ_CODEC_LANE_SNAPPY
-  if (p.status[b] != kLeftForWaveKernel) return;              // decoded by snappy_ring_kernel
+  if (p.status[b] != kLeftForWaveKernel) return;              // decoded by a ring kernel
 #endif
   const u64 s = p.ext[b], e = p.ext[b + 1], len = e - s;
   const u64 D0 = p.dst_ext[b], dn = p.dst_ext[b + 1] - D0;
@@ -1211,7 +1211,10 @@ __device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst,
   }
 }
 
-__global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
+// The ring body for snappy (kCodec 2) and LZ4 (kCodec 3) blocks: they differ only in how an
+// element is decoded (an LZ4 sequence is a literal element, then a copy element).
+template <int kCodec>
+__device__ __forceinline__ void ring_body(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kRingWG * kRing];
   __shared__ u32 fl_addr[kRingWG / kWave][kWave];
   __shared__ u32 fl_lane[kRingWG / kWave][kWave];
@@ -1231,12 +1234,25 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
     const u64 s64 = p.ext[b], e64 = p.ext[b + 1], len = e64 - s64;
     const u64 D064 = p.dst_ext[b], dn64 = p.dst_ext[b + 1] - D064;
     const u32 tag = len ? p.src[e64 - 1] : 0u;
-    live = len > 1 && tag == 2 && dn64 >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
+    live = len > 1 && tag == (u32)kCodec && dn64 >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
            dst_bytes < 0x7FFFFFF0ull && p.src_bytes < 0x7FFFFFF0ull;
+    if constexpr (kCodec == 3)   // the snappy pass left it (every non-snappy block is 0xFF)
+      live = live && p.status[b] == kLeftForWaveKernel;
     if (live) {
       u64 want64 = 0;
-      const u32 h = snappy_header(p.src + s64, len - 1, want64);
-      live = h != 0 && want64 + 1 == dn64;
+      u32 h = 0;
+      if constexpr (kCodec == 2) {
+        h = snappy_header(p.src + s64, len - 1, want64);
+        live = h != 0 && want64 + 1 == dn64;
+      } else {
+        // u32 LE size prefix, then the block stream (compress.rs:108-111); the sizes pass ran
+        // liblz4's acceptance walk: dn - 1 is the exact decoded length of an accepted stream
+        // (dn = 1 for an Err). A stream this pass finds anything unusual in is left to the
+        // lane kernel, which decodes it with liblz4's own control flow.
+        want64 = dn64 - 1;
+        h = 4;
+        live = lz4_prefix(p.src + s64, len - 1) >= 0 && len - 1 > 4;
+      }
       s = (u32)s64;
       ip = h;
       n = (u32)(len - 1);
@@ -1244,7 +1260,9 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
       D0 = (u32)D064;
       dn = (u32)dn64;
     }
-    if (!live) p.status[b] = kLeftForWaveKernel;
+    if constexpr (kCodec == 2) {
+      if (!live) p.status[b] = kLeftForWaveKernel;
+    }
   }
   const u32 src_bytes = live ? (u32)p.src_bytes : 0u;
   u32 d = 0;                                  // bytes produced
@@ -1255,6 +1273,8 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
   u128 acc = 0;                               // the ring slot holding the frontier D0 + d
   u32 ek = 0;                                 // element: 0 literal, 1 copy
   u32 erem = 0, esrc = 0, eoff = 0;
+  bool need_off = false;                      // LZ4: the next header is a match's offset part
+  u32 mln = 0;                                // LZ4: the match-length nibble of the token
 #ifdef TPZ_CODEC_STAMPS
   const u64 t0 = __builtin_amdgcn_s_memtime();
   u64 trips = 0, gtrips = 0, elems = 0;
@@ -1268,6 +1288,71 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
     if (live && erem == 0) {
       if (ip >= n) {
         finish = true;
+      } else if constexpr (kCodec == 3) {
+        // LZ4 sequence (lz4 block format): token = literal length (high nibble) | match length
+        // - 4 (low nibble); 15 continues with bytes until one is not 255; literals; u16 LE
+        // offset; match-length continuation bytes. Decoded from the 16 header bytes in hv.
+        auto hb = [&](u32 i) -> u32 { return (u32)(hv >> (8 * i)) & 0xFFu; };
+        u32 o = 0, len = 0, off = 0;
+        bool bad = false, is_lit = false;
+        if (!need_off) {
+          const u32 t = hb(0);
+          u32 lit = t >> 4;
+          mln = t & 15u;
+          o = 1;
+          if (lit == 15) {
+            u32 x;
+            do {
+              bad = bad || o >= hvv;
+              x = bad ? 0u : hb(o);
+              lit += x;
+              o++;
+            } while (x == 255 && !bad);
+          }
+          if (lit) {
+            is_lit = true;
+            len = lit;
+          }
+        }
+        if (!is_lit && !bad) {                // the offset part (right after the token when no
+          bad = o + 2 > hvv;                  // literal precedes it)
+          off = bad ? 0u : hb(o) | hb(o + 1) << 8;
+          o += 2;
+          u32 ml = mln;
+          if (ml == 15 && !bad) {
+            u32 x;
+            do {
+              bad = bad || o >= hvv;
+              x = bad ? 0u : hb(o);
+              ml += x;
+              o++;
+            } while (x == 255 && !bad);
+          }
+          len = ml + 4;
+        }
+        const u32 next = ip + o + (is_lit ? len : 0u);
+        if (bad || d + len > want || next > n || next < ip || (!is_lit && (off == 0 || off > d))) {
+          fail = true;
+        } else {
+          ek = is_lit ? 0u : 1u;
+          erem = len;
+          esrc = s + ip + o;
+          eoff = off;
+          need_off = is_lit;
+          ip = next;
+          const u32 used = is_lit ? o + len : o;
+          hv = used < hvv ? hv >> (8 * used) : (u128)0;
+          hvv = used < hvv ? hvv - used : 0u;
+          if (hvv < 8 && next < n) {          // the next header, in flight during the element
+            hv = s + next + 16 <= src_bytes
+                     ? __builtin_bit_cast(u128, __builtin_amdgcn_raw_buffer_load_b128(srs, s + next, 0, 0))
+                     : ld16c(p.src, p.src_bytes, s + next);
+            hvv = 16;
+          }
+#ifdef TPZ_CODEC_STAMPS
+          elems++;
+#endif
+        }
       } else {
         const u32 h0 = (u32)hv, x = (u32)(hv >> 8);
         const u32 tag = h0 & 0xFF, kind = tag & 3, t6 = tag >> 2;
@@ -1358,7 +1443,7 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
 #pragma unroll
           for (int j = 0; j < 4; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
         esrc += c;
-        if (c == erem && hvv == 0) {
+        if (kCodec == 2 && c == erem && hvv == 0) {
           const u32 r16 = c & 15, last = (c - 1) >> 4;
           const u128 lp = last == 0 ? v[0] : last == 1 ? v[1] : last == 2 ? v[2] : v[3];
           hv = lp >> (8 * r16);
@@ -1448,6 +1533,9 @@ __global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
 #endif
 }
 
+__global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) { ring_body<2>(p); }
+__global__ __launch_bounds__(kRingWG) void lz4_ring_kernel(CodecParams p) { ring_body<3>(p); }
+
 __global__ __launch_bounds__(kWave) void codec_big_kernel(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kGuard + kBigIn + kBigOut];
   const u32 cnt = uni(*p.defer_count);
@@ -1526,6 +1614,10 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
 #ifndef TPZ_CODEC_LANE_SNAPPY
     hipLaunchKernelGGL(snappy_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),
                        0, stream, p);
+#ifndef TPZ_CODEC_NO_LZ4_RING
+    hipLaunchKernelGGL(lz4_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),
+                       0, stream, p);
+#endif
 #endif
     hipLaunchKernelGGL(codec_lane_kernel, dim3((a.n_blocks + 255) / 256), dim3(256), 0, stream, p);
   }
