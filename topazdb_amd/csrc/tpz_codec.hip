@@ -305,6 +305,42 @@ struct Lz4WaveOut {              // wave-wide copies into the LDS output window
   }
 };
 
+typedef unsigned __int128 u128;
+
+__device__ __forceinline__ u128 ld16u(const uint8_t* p) {    // unaligned 16-byte load
+  u128 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16u(uint8_t* p, u128 v) { __builtin_memcpy(p, &v, 16); }
+
+// 16 bytes at base[a ..] of a buffer of size >= 16 bytes: the load is clamped inside the buffer
+// and the bytes past its end read as zero (branch-free, so the waits on a lane's loads stay exact)
+__device__ __forceinline__ u128 ld16c(const uint8_t* base, u64 size, u64 a) {
+  const u64 ac = a + 16 <= size ? a : size - 16;
+  const u128 v = ld16u(base + ac);
+  const u64 sh = a - ac;
+  return sh == 0 ? v : (sh >= 16 ? (u128)0 : v >> (8 * sh));
+}
+
+// per thread through a 16-byte register window (one 16-byte load per window instead of a
+// dependent byte load per header byte)
+// cpos starts 2^62 before base, so the first byte read always loads a window (a start of ~0
+// made the window look valid for addresses below 15, reading zeros)
+struct Lz4LaneSrc {
+  const uint8_t* src;
+  u64 src_bytes, base;          // in[0] is src[base]
+  mutable u64 cpos;
+  mutable u128 cv;
+  __device__ u32 byte(int64_t i) const {
+    const u64 a = base + (u64)i;
+    if (a - cpos >= 16) {
+      cpos = a;
+      cv = ld16c(src, src_bytes, a);
+    }
+    return (u32)(cv >> (8 * (a - cpos))) & 0xFFu;
+  }
+};
 template <class Src, class Out>
 __device__ int64_t lz4_walk(const Src& in, int64_t iend, const Out& out, int64_t oend) {
   if (oend == 0) return (iend == 1 && in.byte(0) == 0) ? 0 : -1;
@@ -513,7 +549,17 @@ struct Lz4GlobalOut {            // wave-wide copies into global memory
 
 // The whole decode decision of a tag-3 block from global memory (per thread): its decoded
 // length, or -1 (the codec's Err).
-__device__ __forceinline__ int64_t lz4_block_length(const uint8_t* blk, u64 len) {
+__device__ __forceinline__ int64_t lz4_block_length(const uint8_t* src, u64 src_bytes, u64 s, u64 len) {
+  const int64_t size = lz4_prefix(src + s, len - 1);
+  if (size < 0) return -1;
+#ifdef TPZ_CODEC_SIZES_BYTES
+  return lz4_walk(Lz4GlobalSrc{src + s + 4}, (int64_t)len - 5, Lz4NoOut{}, size);
+#else
+  return lz4_walk(Lz4LaneSrc{src, src_bytes, s + 4, s + 4 - (1ull << 62), 0}, (int64_t)len - 5, Lz4NoOut{}, size);
+#endif
+}
+
+__device__ __forceinline__ int64_t lz4_block_length_bytes(const uint8_t* blk, u64 len) {
   const int64_t size = lz4_prefix(blk, len - 1);
   if (size < 0) return -1;
   return lz4_walk(Lz4GlobalSrc{blk + 4}, (int64_t)len - 5, Lz4NoOut{}, size);
@@ -528,7 +574,8 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
   if (tag == 3) {
     // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err
     // leaves a lone tag byte
-    const int64_t r = lz4_block_length(p.src + s, len);
+    const int64_t r = p.src_bytes >= 16 ? lz4_block_length(p.src, p.src_bytes, s, len)
+                                        : lz4_block_length_bytes(p.src + s, len);
     p.size[i] = r < 0 ? 1 : (u64)r + 1;
     return;
   }
@@ -566,7 +613,8 @@ __device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const Blo
   if (dn < 2) {
     // an Err (the sizes pass gave it 1 byte) or an empty output: the decision again, from
     // global memory
-    const int64_t r = lz4_block_length(p.src + s, len);
+    const int64_t r = p.src_bytes >= 16 ? lz4_block_length(p.src, p.src_bytes, s, len)
+                                        : lz4_block_length_bytes(p.src + s, len);
     ok = r == 0 && dn == 1;
   } else if (!fits) {
     const int64_t size = lz4_prefix(p.src + s, len - 1);     // valid: dn >= 2
@@ -885,24 +933,6 @@ __global__ __launch_bounds__(kWave * kGroupWaves) void snappy_group_kernel(Codec
 // that later elements overwrite (the lane's stores land in program order), and no store passes the
 // block's `want` bytes, so neighbouring blocks are never touched. Back-references read the lane's
 // own earlier output (single-thread read-after-write through memory).
-typedef unsigned __int128 u128;
-
-__device__ __forceinline__ u128 ld16u(const uint8_t* p) {    // unaligned 16-byte load
-  u128 v;
-  __builtin_memcpy(&v, p, 16);
-  return v;
-}
-__device__ __forceinline__ void st16u(uint8_t* p, u128 v) { __builtin_memcpy(p, &v, 16); }
-
-// 16 bytes at base[a ..] of a buffer of size >= 16 bytes: the load is clamped inside the buffer
-// and the bytes past its end read as zero (branch-free, so the waits on a lane's loads stay exact)
-__device__ __forceinline__ u128 ld16c(const uint8_t* base, u64 size, u64 a) {
-  const u64 ac = a + 16 <= size ? a : size - 16;
-  const u128 v = ld16u(base + ac);
-  const u64 sh = a - ac;
-  return sh == 0 ? v : (sh >= 16 ? (u128)0 : v >> (8 * sh));
-}
-
 // Stores whose piece does not belong to the block go here instead (never read).
 __device__ u128 g_store_sink[1024];
 __device__ __forceinline__ uint8_t* sink_for_lane() {
@@ -1049,20 +1079,6 @@ __device__ bool snappy_lane(const uint8_t* src, u64 src_bytes, u64 s, u64 n, u64
 
 // LZ4 through lz4_walk, one block per lane: input bytes from a 16-byte register window that is
 // reloaded when the walk leaves it; copies as above.
-struct Lz4LaneSrc {
-  const uint8_t* src;
-  u64 src_bytes, base;          // in[0] is src[base]
-  mutable u64 cpos;
-  mutable u128 cv;
-  __device__ u32 byte(int64_t i) const {
-    const u64 a = base + (u64)i;
-    if (a - cpos >= 16) {
-      cpos = a;
-      cv = ld16c(src, src_bytes, a);
-    }
-    return (u32)(cv >> (8 * (a - cpos))) & 0xFFu;
-  }
-};
 struct Lz4LaneOut {
   const uint8_t* src;
   u64 src_bytes, ibase;         // in[0] is src[ibase]
@@ -1126,7 +1142,7 @@ __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u3
     const int64_t size = lz4_prefix(p.src + s, len - 1);
     ok = size >= 0;
     if (ok) {
-      Lz4LaneSrc in{p.src, p.src_bytes, s + 4, ~0ull, 0};
+      Lz4LaneSrc in{p.src, p.src_bytes, s + 4, s + 4 - (1ull << 62), 0};
       const int64_t r = lz4_walk(in, (int64_t)len - 5,
                                  Lz4LaneOut{p.src, p.src_bytes, s + 4, p.dst, dst_bytes, D0, dn - 1},
                                  size);
