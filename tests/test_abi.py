@@ -189,6 +189,7 @@ def test_c_example_compiles_against_the_header(tmp_path):
     against libtpz_gpu.so with gcc, no C++ and no torch types."""
     assert os.path.exists(_build_c_example(tmp_path))
     assert os.path.exists(_build_c_example(tmp_path, "c_host_decode"))
+    assert os.path.exists(_build_c_example(tmp_path, "c_encode"))
 
 
 def test_unaligned_src_is_rejected():

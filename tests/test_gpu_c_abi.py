@@ -28,3 +28,14 @@ def test_c_host_pipeline(tmp_path, chunk, pinned):
                        timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("ok ") and r.stdout.split()[2] == "30000"
+
+
+@pytest.mark.parametrize("n,block_size", [(50000, 4096), (3000, 65536), (20000, 128)])
+def test_c_device_encode(tmp_path, n, block_size):
+    """The device write side from plain C (examples/c_encode.c): tpz_plan_blocks +
+    tpz_encode_blocks against the host restatement tpz_build_blocks (every byte and block
+    offset), the encoded region decoded back by tpz_decode_blocks, an empty key refused."""
+    exe = _build_c_example(tmp_path, "c_encode")
+    r = subprocess.run([exe, str(n), str(block_size)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok ") and r.stdout.split()[1] == str(n)
