@@ -1172,8 +1172,14 @@ __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u3
 // source bytes or a far copy's stored lines (one set instead of one per descriptor: 1.351 ->
 // 1.314 ms per 2^18 4kc blocks).
 constexpr u32 kRingWG = 256;                                 // blocks (threads) per workgroup
-constexpr u32 kRing = 128, kRingLine = 64, kRingStep = 64;
-static_assert(kRingWG * kRing + (kRingWG / kWave) * kWave * 12 <= 81920, "ring LDS");
+#ifdef TPZ_CODEC_RING256
+constexpr u32 kRing = 256;                                   // 2 workgroups (8 waves) per CU
+#else
+constexpr u32 kRing = 128;                                   // 4 workgroups (16 waves) per CU
+#endif
+constexpr u32 kRingLine = 64, kRingStep = 64;
+static_assert(kRingWG * kRing + (kRingWG / kWave) * kWave * 12 <= (kRing == 128 ? 40960 : 81920),
+              "ring LDS");
 
 __device__ __forceinline__ u128 lds16(const uint8_t* q) {
   return *reinterpret_cast<const u128*>(q);                  // aligned
@@ -1428,7 +1434,16 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     const bool lit = ek == 0, far = !lit && eoff >= 16;
     if (prod && far && eoff < c) c = eoff;
     const u32 Pl = P & ~(kRingLine - 1);
-    const u32 ring_lo = Pl >= kRingLine ? Pl - kRingLine : 0u;        // previous line: intact
+    // The ring holds [roundup16(P) - kRing, P) intact: no write passes the frontier's slot, so
+    // the slots past it still hold the bytes kRing before (a far copy of an entry ~120 bytes
+    // back is served from the ring about half the time instead of never). Everything below
+    // Pl is stored (the lines completed before this step).
+#ifdef TPZ_CODEC_RINGLO_LINE
+    const u32 ring_lo = Pl >= kRing - kRingLine ? Pl - (kRing - kRingLine) : 0u;
+#else
+    const u32 Pr = (P + 15) & ~15u;
+    const u32 ring_lo = Pr >= kRing ? Pr - kRing : 0u;
+#endif
     const u32 q0 = P - eoff;                                          // a copy's first source byte
     const bool gcopy = prod && far && q0 < ring_lo;
     // the 16-byte pieces this step loads from memory (a prefix of the step's four): a literal's,

@@ -485,6 +485,10 @@ __device__ __forceinline__ void issue_pieces(const EncParams& p, const EntryRegs
 
 // OR piece k (value v) of an entry whose klen field sits at W[pos] into the window
 __device__ __forceinline__ void emit_piece(uint8_t* W, u32 pos, u64 kl, u64 vl, u32 nk, u32 k, u128 v) {
+#ifdef TPZ_ENC_ABL_NOASM   // diagnostic (timing only, wrong bytes): the pieces are loaded, not placed
+  asm volatile("" ::"v"((u32)v), "v"((u32)(v >> 32)), "v"((u32)(v >> 64)), "v"((u32)(v >> 96)));
+  return;
+#endif
   const bool key = k < nk;
   const u32 j = key ? k : k - nk;
   const u32 rem = (u32)((key ? kl : vl) - 16ull * j);
@@ -600,7 +604,11 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
       // four bytes, raw CRC of payload || 0^kpad, un-shifted, complemented
       if (lane == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
       wave_sync();
+#ifdef TPZ_ENC_ABL_NOCRC   // diagnostic (timing only, wrong CRCs)
+      const u32 R = kpad;
+#else
       const u32 R = round_crc(tab, slot, kEncGuard + (int)A, P + kpad, 0);
+#endif
       wave_sync();
       const u32 crc = ~crc_unshift_small(tab, R, kpad);
       if (lane == 0) {
@@ -609,7 +617,9 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
         or_bytes(W, A + P + 4, 1, 1);                                 // compress.rs:87 tag
       }
       wave_sync();
+#ifndef TPZ_ENC_ABL_NOSTORE   // diagnostic (timing only): nothing written
       store_block(W, p.out, o0, A, P + 5, lane, kWave);
+#endif
       wave_sync();
     } else {                                                         // longer block: big kernel
       if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
