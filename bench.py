@@ -523,7 +523,12 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     alg = int(kpos[etot] - kpos[0]) + int(vpos[etot] - vpos[0]) + 16 * etot + 12 * nb + int(ext[-1])
+    # the host builder beside it (tpz_build_blocks, one thread: SsTableBuilder's loop restated)
+    t0 = time.perf_counter()
+    synth.build_blocks(keys, kpos[:etot + 1], vals, vpos[:etot + 1], block_size)
+    cpu_s = time.perf_counter() - t0
     return {"entries": etot, "blocks": nb, "ms_plan": round(ms_plan, 3), "ms_encode": round(ms, 4),
+            "cpu_host_builder_ms_1_thread": round(cpu_s * 1e3, 1),
             "gib_s_encoded": round(int(ext[-1]) / (ms * 1e-3) / GIB, 1),
             "algorithmic_bytes": alg, "achieved_gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
             "frac_of_8tb": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}

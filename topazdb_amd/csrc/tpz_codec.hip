@@ -1212,12 +1212,25 @@ __device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (
 #endif
   const u32 m = P & 15, K = (m + c + 15) >> 4, Kn = (m + c) >> 4;
   const u32 A = P & ~15u;
+#ifndef TPZ_CODEC_SLOT16
+  // the new frontier's slot keeps its upper half when the frontier is in its lower half: the
+  // ring then holds [roundup8(P) - kRing, P) intact (a copy 120 bytes back always from LDS)
+  const bool half = ((P + c) & 15u) != 0 && ((P + c) & 15u) <= 8;
+#endif
   u128 carry = m ? lowbytes(acc, m) : (u128)0, nacc = acc;
 #pragma unroll
   for (int k = 0; k < 5; k++) {
     const u128 cur = k < 4 ? v[k < 4 ? k : 0] : (u128)0;
     const u128 slot = m ? carry | (cur << (8 * m)) : cur;
+#ifndef TPZ_CODEC_SLOT16
+    if ((u32)k < K) {
+      uint8_t* q = R + ((A + 16 * k) & (kRing - 1));
+      if ((u32)k == Kn && half) *reinterpret_cast<u64*>(q) = (u64)slot;
+      else lds16w(q, slot);
+    }
+#else
     if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), slot);
+#endif
     if ((u32)k == Kn) nacc = slot;
     carry = m ? cur >> (8 * (16 - m)) : (u128)0;
   }
@@ -1434,14 +1447,18 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     const bool lit = ek == 0, far = !lit && eoff >= 16;
     if (prod && far && eoff < c) c = eoff;
     const u32 Pl = P & ~(kRingLine - 1);
-    // The ring holds [roundup16(P) - kRing, P) intact: no write passes the frontier's slot, so
-    // the slots past it still hold the bytes kRing before (a far copy of an entry ~120 bytes
-    // back is served from the ring about half the time instead of never). Everything below
-    // Pl is stored (the lines completed before this step).
+    // The ring holds [roundup8(P) - kRing, P) intact: no write passes the frontier's 8-byte
+    // half-slot, so the bytes past it still hold the bytes kRing before (a far copy of an
+    // entry 120 bytes back is served from the ring; with whole 16-byte slots only about half
+    // of them were). Everything below Pl is stored (the lines completed before this step).
 #ifdef TPZ_CODEC_RINGLO_LINE
     const u32 ring_lo = Pl >= kRing - kRingLine ? Pl - (kRing - kRingLine) : 0u;
 #else
+#ifdef TPZ_CODEC_SLOT16
     const u32 Pr = (P + 15) & ~15u;
+#else
+    const u32 Pr = (P + 7) & ~7u;
+#endif
     const u32 ring_lo = Pr >= kRing ? Pr - kRing : 0u;
 #endif
     const u32 q0 = P - eoff;                                          // a copy's first source byte
