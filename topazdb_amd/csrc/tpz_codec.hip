@@ -1178,6 +1178,27 @@ constexpr u32 kRing = 256;                                   // 2 workgroups (8 
 constexpr u32 kRing = 128;                                   // 4 workgroups (16 waves) per CU
 #endif
 constexpr u32 kRingLine = 64, kRingStep = 64;
+// 16-byte pieces a step can take. A literal's steps are 64 bytes, but its final step may take up
+// to 16 kPieces bytes as long as it ends by Pl + 128 (every line it completes is then still
+// intact in the ring when the step's stores read it): a 65-80 byte literal is one step instead
+// of two. (Per 2^18 4kc blocks: 4 pieces 1.22 ms, 5 pieces 1.15 ms, steps of up to two whole
+// lines with 8 pieces 1.22-1.24 ms; profiles/r2/codec_ring.jsonl.)
+#ifndef TPZ_CODEC_PIECES
+#define TPZ_CODEC_PIECES 5
+#endif
+constexpr u32 kPieces = TPZ_CODEC_PIECES;
+static_assert(kPieces >= 4 && kPieces <= 7, "a step ends by Pl + 128");
+// bytes a literal step starting at P takes of the `rem` left
+__device__ __forceinline__ u32 lit_step(u32 P, u32 rem) {
+  const u32 lim = min(16 * kPieces, 128u - (P & 63u));
+  return rem <= lim ? rem : kRingStep;
+}
+// the length of the final step of a literal of len bytes whose first step starts at P (steps of
+// 64 keep P mod 64, and with it the limit, the same)
+__device__ __forceinline__ u32 lit_final(u32 P, u32 len) {
+  const u32 lim = min(16 * kPieces, 128u - (P & 63u));
+  return len <= lim ? len : len - 64 * ((len - lim + 63) / 64);
+}
 static_assert(kRingWG * kRing + (kRingWG / kWave) * kWave * 12 <= (kRing == 128 ? 40960 : 81920),
               "ring LDS");
 
@@ -1196,15 +1217,15 @@ __device__ __forceinline__ u128 ring_read(const uint8_t* R, u32 a) {
   return m ? (s0 >> (8 * m)) | (s1 << (8 * (16 - m))) : s0;
 }
 
-// Writes the step's output bytes [P, P + c) (c <= 64; v[j] = bytes [P + 16 j, P + 16 j + 16))
-// into the ring's aligned slots. acc holds the slot containing P (its bytes below P are the
+// Writes the step's output bytes [P, P + c) (c <= 16 kPieces; v[j] = bytes [P + 16 j, P + 16 j +
+// 16)) into the ring's aligned slots. acc holds the slot containing P (its bytes below P are the
 // output); on return it holds the slot containing P + c.
-__device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (&v)[4], u128& acc) {
+__device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (&v)[kPieces], u128& acc) {
 #ifdef TPZ_CODEC_CHEAPEMIT
   {                                          // timing build only: no funnel (wrong bytes)
     const u32 A = P & ~15u, K = (c + 15) >> 4;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
+    for (int k = 0; k < (int)kPieces; k++)
       if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), v[k]);
     acc = v[0];
     return;
@@ -1219,8 +1240,8 @@ __device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (
 #endif
   u128 carry = m ? lowbytes(acc, m) : (u128)0, nacc = acc;
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const u128 cur = k < 4 ? v[k < 4 ? k : 0] : (u128)0;
+  for (int k = 0; k <= (int)kPieces; k++) {
+    const u128 cur = k < (int)kPieces ? v[k < (int)kPieces ? k : 0] : (u128)0;
     const u128 slot = m ? carry | (cur << (8 * m)) : cur;
 #ifndef TPZ_CODEC_SLOT16
     if ((u32)k < K) {
@@ -1423,7 +1444,7 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
           hvv = hvv > used ? hvv - used : 0u;
           // a literal whose final step's last piece ends 5..15 bytes past the literal carries the
           // next header: taken from that piece when the literal completes (hvv = 0 until then)
-          const u32 rf = kind == 0 ? ((len - 1) % kRingStep + 1) & 15 : 0u;
+          const u32 rf = kind == 0 ? lit_final(D0 + d, len) & 15 : 0u;
           const bool from_lit = kind == 0 && hvv < 5 && rf >= 1 && rf <= 11 &&
                                 s + next + 5 <= src_bytes;
           if (from_lit) hvv = 0;
@@ -1443,8 +1464,8 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     // so every source byte precedes the step)
     const bool prod = live && !finish && !fail && erem > 0;
     const u32 P = D0 + d;
-    u32 c = prod ? (erem < kRingStep ? erem : kRingStep) : 0u;
     const bool lit = ek == 0, far = !lit && eoff >= 16;
+    u32 c = !prod ? 0u : lit ? lit_step(P, erem) : (erem < kRingStep ? erem : kRingStep);
     if (prod && far && eoff < c) c = eoff;
     const u32 Pl = P & ~(kRingLine - 1);
     // The ring holds [roundup8(P) - kRing, P) intact: no write passes the frontier's 8-byte
@@ -1465,7 +1486,7 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     const bool gcopy = prod && far && q0 < ring_lo;
     // the 16-byte pieces this step loads from memory (a prefix of the step's four): a literal's,
     // or a far copy's pieces that start below the ring (the others come from the ring)
-    const bool tail = lit && esrc + kRingStep + 16 > src_bytes;
+    const bool tail = lit && esrc + 16 * kPieces + 16 > src_bytes;
     const u32 cp = (c + 15) >> 4;
     const u32 np = !prod ? 0u : lit ? (tail ? 0u : cp)
                  : !gcopy ? 0u : min(cp, (ring_lo - q0 + 15) >> 4);
@@ -1479,21 +1500,23 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
       // One set of four 16-byte global loads serves every lane: a literal's source bytes, or the
       // stored lines a far copy reads (the wave's own stores: same CU, visible after the vmcnt
       // wait above). Pieces a lane does not need are exec-masked off.
-      u128 v[4];
+      u128 v[kPieces];
       const uint8_t* base = lit ? p.src + esrc : p.dst + q0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) v[j] = 0;
+      for (int j = 0; j < (int)kPieces; j++) v[j] = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++)
+      for (int j = 0; j < (int)kPieces; j++)
         if ((u32)j < np) v[j] = *reinterpret_cast<const u128 __attribute__((aligned(1)))*>(base + 16 * j);
       if (lit) {
         if (tail)
 #pragma unroll
-          for (int j = 0; j < 4; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
+          for (int j = 0; j < (int)kPieces; j++) v[j] = ld16c(p.src, p.src_bytes, esrc + 16 * j);
         esrc += c;
         if (kCodec == 2 && c == erem && hvv == 0) {
           const u32 r16 = c & 15, last = (c - 1) >> 4;
-          const u128 lp = last == 0 ? v[0] : last == 1 ? v[1] : last == 2 ? v[2] : v[3];
+          u128 lp = v[0];
+#pragma unroll
+          for (int j = 1; j < (int)kPieces; j++) lp = last == (u32)j ? v[j] : lp;
           hv = lp >> (8 * r16);
           hvv = 16 - r16;
         }
