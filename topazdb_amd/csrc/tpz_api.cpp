@@ -124,6 +124,10 @@ struct tpz_workspace {
   uint64_t* d_big_scratch = nullptr;
   uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
   uint32_t acc_cap = 0;
+  void* d_plan0 = nullptr;      // tpz_plan_blocks: nx + per-workgroup maxima + info
+  size_t plan0_cap = 0;
+  void* d_plan1 = nullptr;      // tpz_plan_blocks: the transfer tables + chunk counts
+  size_t plan1_cap = 0;
 };
 
 struct tpz_ctx {
@@ -142,6 +146,8 @@ void free_workspace(tpz_workspace& w) {
   if (w.d_defer) (void)hipFree(w.d_defer);
   if (w.d_big_scratch) (void)hipFree(w.d_big_scratch);
   if (w.d_acc) (void)hipFree(w.d_acc);
+  if (w.d_plan0) (void)hipFree(w.d_plan0);
+  if (w.d_plan1) (void)hipFree(w.d_plan1);
   w = tpz_workspace{};
 }
 
@@ -159,6 +165,21 @@ tpz_err get_acc(tpz_ctx* c, void* stream, uint32_t n, uint32_t** out) {
     w.acc_cap = n;
   }
   *out = w.d_acc;
+  return TPZ_SUCCESS;
+}
+
+// A grow-only device buffer of the stream's workspace (the stream is idle or only uses it in
+// order: a buffer is replaced after the stream's pending work is done). Caller holds c->mu.
+tpz_err grow(void* stream, void** buf, size_t* cap, size_t bytes) {
+  if (*buf && *cap >= bytes) return TPZ_SUCCESS;
+  void* d = nullptr;
+  TPZ_HIP(hipMalloc(&d, bytes));
+  if (*buf) {
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    (void)hipFree(*buf);
+  }
+  *buf = d;
+  *cap = bytes;
   return TPZ_SUCCESS;
 }
 
@@ -423,25 +444,6 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filt
   return TPZ_SUCCESS;
 }
 
-namespace {
-// Device scratch of one write-side call: stream-ordered (the pool keeps the memory between
-// calls), freed on every exit path.
-struct DevScratch {
-  hipStream_t s;
-  std::vector<void*> p;
-  explicit DevScratch(hipStream_t st) : s(st) {}
-  ~DevScratch() {
-    for (void* x : p) (void)hipFreeAsync(x, s);
-  }
-  hipError_t get(void* out, size_t bytes) {  // out: a T** for any T
-    void* d = nullptr;
-    hipError_t e = hipMallocAsync(&d, bytes ? bytes : 16, s);
-    if (e == hipSuccess) p.push_back(d);
-    std::memcpy(out, &d, sizeof d);
-    return e;
-  }
-};
-}  // namespace
 
 tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, uint32_t* d_first,
                         uint64_t* d_ext, uint32_t* h_n_blocks, uint64_t* h_bad_entry,
@@ -461,10 +463,18 @@ tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, 
     return TPZ_SUCCESS;
   }
   if (!en->d_kpos || !en->d_vpos) return TPZ_ERR_INVALID_ARG;
-  DevScratch sc(s);
-  uint32_t *nx = nullptr, *info = nullptr;
-  TPZ_HIP(sc.get(&nx, ((size_t)n + n / 2048 + 2) * 4));   // nx, then per-workgroup maxima
-  TPZ_HIP(sc.get(&info, 16));
+  // the stream's grow-only plan buffers (one plan per stream at a time: the call is synchronous)
+  std::unique_lock<std::mutex> lk(c->mu);
+  tpz_workspace& w = c->ws[stream];
+  lk.unlock();
+  const size_t nx_words = (size_t)n + n / 2048 + 2;        // nx, then per-workgroup maxima
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = grow(stream, &w.d_plan0, &w.plan0_cap, (nx_words + 4) * 4);
+    if (r != TPZ_SUCCESS) return r;
+  }
+  uint32_t* nx = static_cast<uint32_t*>(w.d_plan0);
+  uint32_t* info = nx + nx_words;
   uint32_t h_info[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
   TPZ_HIP(hipMemcpyAsync(info, h_info, 16, hipMemcpyHostToDevice, s));
   tpz::PlanLaunch a{};
@@ -489,9 +499,14 @@ tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, 
   a.w = h_info[0];
   a.chunk = a.w > tpz::kPlanChunk ? a.w : tpz::kPlanChunk;
   const uint64_t K = (n + (uint64_t)a.chunk - 1) / a.chunk;
-  TPZ_HIP(sc.get(&a.tab_a, K * a.w * 4));
-  TPZ_HIP(sc.get(&a.tab_b, K * a.w * 4));
-  TPZ_HIP(sc.get(&a.cnt, K * 4));
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = grow(stream, &w.d_plan1, &w.plan1_cap, (2 * K * a.w + K + 4) * 4);
+    if (r != TPZ_SUCCESS) return r;
+  }
+  a.tab_a = static_cast<int*>(w.d_plan1);
+  a.tab_b = a.tab_a + K * a.w;
+  a.cnt = reinterpret_cast<uint32_t*>(a.tab_b + K * a.w);
   a.n_blocks = info + 2;
   TPZ_HIP(tpz::launch_plan(a, s));
   TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
@@ -509,8 +524,12 @@ tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_f
     return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
-  void* ws = nullptr;  // the big-block worklist: stream-ordered, freed behind the kernels
-  TPZ_HIP(hipMallocAsync(&ws, (size_t)n_blocks * 4 + 16, s));
+  tpz_workspace* w = nullptr;    // the big-block worklist: the stream's decode worklist
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = get_workspace(c, stream, n_blocks, &w);
+    if (r != TPZ_SUCCESS) return r;
+  }
   tpz::EncodeLaunch a{};
   a.keys = en->d_keys;
   a.kpos = en->d_kpos;
@@ -523,12 +542,10 @@ tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_f
   a.n_blocks = n_blocks;
   a.crc_tables = c->d_tables;
   a.out = d_out;
-  a.big_count = static_cast<uint32_t*>(ws);
-  a.big_list = static_cast<uint32_t*>(ws) + 4;
+  a.big_count = w->d_defer;
+  a.big_list = w->d_defer + 4;
   a.num_cus = c->num_cus;
-  const hipError_t e = tpz::launch_encode(a, s);
-  (void)hipFreeAsync(ws, s);
-  TPZ_HIP(e);
+  TPZ_HIP(tpz::launch_encode(a, s));
   return TPZ_SUCCESS;
 }
 
