@@ -339,7 +339,9 @@ uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len);
  *     return TPZ_ERR_INVALID_ARG with *h_bad_entry = the first such entry (UINT64_MAX otherwise).
  *     block_size must be in (2, 65536]: past 64 KiB the reference's u16 offsets wrap.
  *   tpz_encode_blocks: writes block b to d_out[d_ext[b] .. d_ext[b+1]) (d_out 16-byte aligned,
- *     d_ext[n_blocks] bytes; no byte outside the blocks is written). Asynchronous on `stream`.
+ *     d_ext[n_blocks] bytes; no byte outside the blocks is written) for d_first / d_ext /
+ *     n_blocks exactly as tpz_plan_blocks returned them for these entries and block_size.
+ *     Asynchronous on `stream`; uses the stream's workspace (like tpz_decode_blocks).
  * BlockMeta::first_key of block b is entry d_first[b]'s key. */
 typedef struct {
   const uint8_t* d_keys;
