@@ -19,6 +19,8 @@
  *   tpz_decompress_blocks   compress::decode's codec step: snappy (src/block/compress.rs:104-107)
  *                           and lz4 (:108-111) blocks to their Uncompress form
  *   tpz_format_block_error  the reference's error strings (checksum.rs:18-21, compress.rs:97,102)
+ *   tpz_plan_blocks +       the write side for compaction output: SsTableBuilder::add +
+ *   tpz_encode_blocks       block_build (src/table/builder.rs:49-85) over entries in HBM
  *
  * Plain pointers and sizes only. Pointers named d_* are device (HBM) pointers of the context's
  * device; h_* are host pointers. `stream` is a hipStream_t passed as void* (NULL = default).
