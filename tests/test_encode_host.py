@@ -109,3 +109,32 @@ def test_oracle_builder_rejects_what_the_reference_cannot_take():
     assert struct.unpack(">H", region[:2].tobytes())[0] == 1
     region, ext, first = O.build_blocks(*pack([]), 64)
     assert len(region) == 0 and ext.tolist() == [0] and first.tolist() == [0]
+
+
+@pytest.mark.parametrize("n,fpp", [(1, 0.1), (3, 0.01), (100, 0.1), (1000, 0.3), (5000, 0.001)])
+def test_bloom_from_keys_matches_the_restatement(n, fpp):
+    """The facade's Bloom::from_keys (topazdb_amd/table.py, bloom.rs:48-70) against the golden
+    generator's independent restatement (make_golden.bloom_from_keys), which the golden SSTs'
+    filters pin against the reference's test expectations (table/tests.rs:140-155)."""
+    from topazdb_amd.table import Bloom
+    rng = random.Random(n * 7 + 1)
+    hs = [rng.getrandbits(64) for _ in range(n)]
+    assert Bloom.from_keys(hs, fpp).encode() == MG.bloom_from_keys(hs, fpp)
+
+
+def test_bloom_of_no_keys():
+    """bloom.rs:48-70 with no keys: m = 0 bits, k = ceil(0/0) = NaN cast to 0, clamped to 1: the
+    filter is the lone k byte."""
+    from topazdb_amd.table import Bloom
+    assert Bloom.from_keys([], 0.1).encode() == b"\x01"
+
+
+def test_golden_blooms_rebuilt_from_their_keys():
+    """Every golden SST's filter equals Bloom::from_keys over xxh3_64 of its keys (fpp 0.1)."""
+    from topazdb_amd import _lib
+    from topazdb_amd.table import Bloom
+    for name in sorted(GOLDEN_SSTS):
+        f, exp, kvs = golden_entries(name)
+        bloom_off = struct.unpack(">I", f[-8:-4])[0]
+        filt = f[bloom_off:len(f) - 8]
+        assert Bloom.from_keys([_lib.xxh3_64(k) for k, _ in kvs], 0.1).encode() == filt, name

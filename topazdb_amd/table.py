@@ -21,6 +21,7 @@ BlockError("decompression failed"). There is no CPU fallback.
 from __future__ import annotations
 
 import bisect
+import math
 import os
 import struct
 
@@ -409,11 +410,49 @@ class BlockMeta:
         return metas
 
 
+def _sat_cast(x: float, hi: int) -> int:
+    """Rust's saturating float -> unsigned cast (`as u8` / `as usize`): NaN -> 0."""
+    if x != x:
+        return 0
+    return 0 if x <= 0 else (hi if x >= hi else int(x))
+
+
 class Bloom:
-    """src/bloom.rs:37-95 (decode + may_contain)."""
+    """src/bloom.rs:37-95 (from_keys, encode, decode, may_contain)."""
 
     def __init__(self, filt: bytes):
         self.filter = bytes(filt)
+
+    @staticmethod
+    def from_keys(hashes, fpp: float) -> "Bloom":
+        """Bloom::from_keys (bloom.rs:48-70): m = -n ln(fpp) / ln2^2 bits, k = ceil(m / n ln2^2)
+        probes clamped to [1, 15] (stored in the last byte), probe i of hash h at
+        (h + i * rotr(h, 34)) mod limit."""
+        if not (0.0 <= fpp < 1.0):
+            raise ReferencePanic("assertion failed: (0.0..1.0).contains(&fpp)")
+        n = float(len(hashes))
+        ln2sq = math.log(2.0) * math.log(2.0)           # LN_2.powi(2)
+        lnf = math.log(fpp) if fpp > 0.0 else -math.inf
+        num = n * lnf
+        m = -num / ln2sq if num == num else math.nan
+        k = (m / n * ln2sq) if n > 0 else math.nan
+        k = max(1, min(15, _sat_cast(math.ceil(k) if k == k and abs(k) != math.inf else k, 255)))
+        nbits = _sat_cast(math.ceil(m) if m == m and abs(m) != math.inf else m, 1 << 64)
+        filt = bytearray((nbits + 7) // 8 + 1)
+        filt[-1] = k
+        limit = (len(filt) - 1) * 8
+        mask = (1 << 64) - 1
+        for h in hashes:
+            h = int(h) & mask
+            delta = ((h >> 34) | (h << 30)) & mask     # Bloom::delta
+            for _ in range(k):
+                pos = h % limit
+                filt[pos // 8] |= 1 << (pos % 8)
+                h = (h + delta) & mask
+        return Bloom(bytes(filt))
+
+    def encode(self) -> bytes:
+        return self.filter
 
     def may_contain(self, h: int) -> bool:
         mask = (1 << 64) - 1
@@ -580,3 +619,59 @@ class SsTableIterator:
         if not self.block_iter.is_valid() and self.idx < self.table.num_of_blocks() - 1:
             self.idx += 1
             self.block_iter = self._seek_to_first_inner(self.table, self.idx)
+
+
+class SsTableBuilder:
+    """SsTableBuilder (src/table/builder.rs:17-141) with the block loop on the device: add()
+    collects the entries (the key-hash list of the bloom filter included, :49-64), and
+    build_image() runs BlockBuilder's fill rule, Block::encode and the CRCs for every block on the
+    GPU (tpz_plan_blocks + tpz_encode_blocks), then appends the block metas (encode_block_meta,
+    table.rs:33-46), the meta offset, the bloom filter and its offset (:97-130, :132-141) exactly
+    as the reference lays them out. build() writes the file (FileObject::create appends the
+    whole-file CRC, file_object.rs:33-48) and opens it as an SsTable."""
+
+    def __init__(self, ctx: Context, block_size: int = 4096, false_positive_rate: float = 0.1):
+        self.ctx = ctx
+        self.block_size = block_size
+        self.fpp = false_positive_rate
+        self.keys: list[bytes] = []
+        self.values: list[bytes] = []
+
+    def add(self, key: bytes, value: bytes) -> None:
+        if not key:
+            raise ReferencePanic("key must not be empty")       # builder.rs:27
+        self.keys.append(bytes(key))
+        self.values.append(bytes(value))
+
+    def build_image(self) -> bytes:
+        from .encode import DeviceEntries, EntryError, encode_blocks, plan_blocks
+        kl = np.fromiter((len(k) for k in self.keys), np.uint64, len(self.keys))
+        vl = np.fromiter((len(v) for v in self.values), np.uint64, len(self.values))
+        kpos = np.zeros(len(kl) + 1, np.uint64)
+        vpos = np.zeros(len(vl) + 1, np.uint64)
+        np.cumsum(kl, out=kpos[1:])
+        np.cumsum(vl, out=vpos[1:])
+        ent = DeviceEntries(np.frombuffer(b"".join(self.keys), np.uint8),
+                            kpos, np.frombuffer(b"".join(self.values), np.uint8), vpos,
+                            self.ctx.device)
+        try:
+            first, ext, nb = plan_blocks(self.ctx, ent, self.block_size)
+        except EntryError as e:   # an entry no block holds: SsTableBuilder::add never returns
+            raise ReferencePanic(str(e)) from e
+        region = encode_blocks(self.ctx, ent, first, ext, nb)
+        torch.cuda.synchronize(torch.device("cuda", self.ctx.device))
+        e = ext[:nb + 1].cpu().numpy().astype(np.int64)
+        f = first[:nb + 1].cpu().numpy().astype(np.int64)
+        data = bytearray(region[:int(e[-1])].cpu().numpy().tobytes() if nb else b"")
+        meta_off = len(data)
+        data += BlockMeta.encode_block_meta(
+            [BlockMeta(int(e[b]), self.keys[int(f[b])]) for b in range(nb)])
+        data += struct.pack(">I", meta_off & 0xFFFFFFFF)
+        if math.copysign(1.0, self.fpp) > 0:                    # is_sign_positive
+            bloom_off = len(data)
+            data += Bloom.from_keys([_lib.xxh3_64(k) for k in self.keys], self.fpp).encode()
+            data += struct.pack(">I", bloom_off & 0xFFFFFFFF)
+        return bytes(data)
+
+    def build(self, id: int, path: str) -> "SsTable":
+        return SsTable.open(id, FileObject.create(path, self.build_image(), self.ctx), self.ctx)
