@@ -323,6 +323,17 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* ctx, const uint8_t* d_filter, uint64_t fi
 /* xxh3_64 (seed 0) on the host: the hash the reference's bloom uses (xxhash-rust 0.8.5). */
 uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len);
 
+/* Bloom::from_keys (src/bloom.rs:48-70) for keys in HBM (SsTableBuilder::build_bloom,
+ * src/table/builder.rs:132-141, over xxh3_64 of every added key):
+ *   tpz_bloom_geometry (host): the filter's length in bytes (bit array + the k byte) and k for
+ *     n_keys keys and false-positive rate fpp, with the reference's f64 arithmetic and saturating
+ *     casts; TPZ_ERR_INVALID_ARG unless 0 <= fpp < 1 (bloom.rs:49 asserts).
+ *   tpz_bloom_build: writes the filter (Bloom::encode) to d_filter[0 .. filter_len). d_filter must
+ *     be 4-byte aligned with room for (filter_len + 3) & ~3 bytes. Asynchronous on `stream`. */
+tpz_err tpz_bloom_geometry(uint64_t n_keys, double fpp, uint64_t* filter_len, uint32_t* k);
+tpz_err tpz_bloom_build(tpz_ctx* ctx, const uint8_t* d_keys, const uint64_t* d_key_pos,
+                        uint32_t n_keys, double fpp, uint8_t* d_filter, void* stream);
+
 /* ---- device write side (SURVEY.md §8f row 4's alternative: compaction output) ------------
  * A run of sorted entries in HBM becomes SST data-region blocks, byte for byte what
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) writes with

@@ -5,6 +5,7 @@ device encode is compared with it (tests/test_gpu_encode.py): against the commit
 builder on random entry sets, and against the product's host builder (tpz_build_blocks)."""
 import importlib.util
 import json
+import math
 import os
 import random
 import struct
@@ -138,3 +139,29 @@ def test_golden_blooms_rebuilt_from_their_keys():
         bloom_off = struct.unpack(">I", f[-8:-4])[0]
         filt = f[bloom_off:len(f) - 8]
         assert Bloom.from_keys([_lib.xxh3_64(k) for k, _ in kvs], 0.1).encode() == filt, name
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 17, 1000, 123457, 10 ** 7])
+@pytest.mark.parametrize("fpp", [0.0, 1e-300, 1e-9, 0.001, 0.1, 0.5, 0.999999, 1.0, -0.1, float("nan")])
+def test_bloom_geometry_matches_the_restatement(n, fpp):
+    """tpz_bloom_geometry (the C ABI's Bloom::from_keys sizing, bloom.rs:48-57) against the
+    facade's restatement: filter length and k agree, and both refuse the same inputs."""
+    from topazdb_amd import _lib
+    from topazdb_amd.table import Bloom, ReferencePanic
+    geo = _lib.bloom_geometry(n, fpp)
+    try:
+        b = Bloom.from_keys([0] * min(n, 3), fpp) if n <= 3 else None
+    except ReferencePanic:
+        assert geo is None
+        return
+    if b is not None:
+        assert geo == (len(b.filter), b.filter[-1])
+        return
+    # large n: the restatement's sizing without hashing n keys
+    if not (0.0 <= fpp < 1.0) or fpp == 0.0:
+        assert geo is None
+        return
+    ln2sq = math.log(2.0) ** 2
+    m = -(n * math.log(fpp)) / ln2sq
+    k = max(1, min(15, math.ceil(m / n * ln2sq)))
+    assert geo == ((math.ceil(m) + 7) // 8 + 1, k)

@@ -189,3 +189,39 @@ def test_sstable_builder_refuses_what_the_reference_cannot_take(ctx):
     b.add(b"k", b"v" * 100)                                    # fits no 64-byte block
     with pytest.raises(ReferencePanic):
         b.build_image()
+
+
+@pytest.mark.parametrize("n,fpp,kmax", [(1, 0.1, 8), (7, 0.9, 3), (1000, 0.1, 40), (5000, 0.01, 16),
+                                        (60000, 0.001, 24), (200000, 0.3, 64)])
+def test_device_bloom_build(ctx, n, fpp, kmax):
+    """tpz_bloom_build (SsTableBuilder::build_bloom, builder.rs:132-141, over Bloom::from_keys,
+    bloom.rs:48-70) against the restatement table.Bloom.from_keys over xxh3_64 of the same keys,
+    byte for byte, then every key found by the device probe (tpz_bloom_may_contain)."""
+    from topazdb_amd.encode import bloom_build
+    from topazdb_amd.table import Bloom
+    rng = random.Random(n ^ 0x5EED)
+    kvs = [(bytes(rng.getrandbits(8) for _ in range(rng.randint(1, kmax))), b"")
+           for _ in range(min(n, 3000))]
+    if n > len(kvs):   # big cases: bulk random keys (duplicates allowed, as the builder allows)
+        kl = np.random.default_rng(n).integers(1, kmax + 1, n - len(kvs))
+        buf = np.random.default_rng(n + 1).integers(0, 256, int(kl.sum()), dtype=np.uint8).tobytes()
+        ends = np.cumsum(kl)
+        kvs += [(buf[e - l:e], b"") for e, l in zip(ends.tolist(), kl.tolist())]
+    keys, kpos, vals, vpos = pack(kvs)
+    ent = DeviceEntries(keys, kpos, vals, vpos)
+    got = bloom_build(ctx, ent, fpp)
+    want = Bloom.from_keys([_lib.xxh3_64(k) for k, _ in kvs], fpp).encode()
+    assert len(got) == len(want)
+    if got != want:
+        bad = next(i for i in range(len(got)) if got[i] != want[i])
+        raise AssertionError(f"first differing filter byte {bad} of {len(got)}")
+
+
+def test_device_bloom_build_edges(ctx):
+    from topazdb_amd.encode import bloom_build
+    keys, kpos, vals, vpos = pack([])
+    assert bloom_build(ctx, DeviceEntries(keys, kpos, vals, vpos), 0.1) == b"\x01"
+    ent = DeviceEntries(*pack([(b"a", b"")]))
+    for fpp in (0.0, 1.0, -0.5, float("nan")):    # assert!((0.0..1.0)) or a zero `% limit`
+        with pytest.raises(ValueError):
+            bloom_build(ctx, ent, fpp)

@@ -126,6 +126,12 @@ def lib() -> C.CDLL:
         L.tpz_encode_blocks.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_void_p, C.c_void_p,
                                         C.c_uint32, C.c_void_p, C.c_void_p]
         L.tpz_encode_blocks.restype = C.c_int
+        L.tpz_bloom_geometry.argtypes = [C.c_uint64, C.c_double, C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint32)]
+        L.tpz_bloom_geometry.restype = C.c_int
+        L.tpz_bloom_build.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_double,
+                                      C.c_void_p, C.c_void_p]
+        L.tpz_bloom_build.restype = C.c_int
         L.tpz_host_xxh3_64.argtypes = [C.c_char_p, C.c_uint64]
         L.tpz_host_xxh3_64.restype = C.c_uint64
         L.tpz_layout_spill_stream.argtypes = [C.c_uint64]
@@ -299,6 +305,14 @@ def _pack_ends(ctx, d_ext: int, n_blocks: int, src_bytes: int, cols: dict, d_fir
     c = Columns(*[cols[f] for f in COLUMN_FIELDS])
     check(lib().tpz_pack_ends(ctx.handle, C.byref(b), C.byref(c), C.c_void_p(d_first),
                               C.c_void_p(d_dense), C.c_void_p(stream)), "tpz_pack_ends")
+
+
+def bloom_geometry(n_keys: int, fpp: float):
+    """tpz_bloom_geometry: (filter length in bytes, k) of Bloom::from_keys (bloom.rs:48-70), or
+    None where the reference asserts (fpp outside [0, 1)) or divides by zero (fpp 0 with keys)."""
+    ln, k = C.c_uint64(), C.c_uint32()
+    rc = lib().tpz_bloom_geometry(n_keys, fpp, C.byref(ln), C.byref(k))
+    return None if rc != SUCCESS else (int(ln.value), int(k.value))
 
 
 def xxh3_64(b: bytes) -> int:

@@ -1,6 +1,7 @@
 // tpz_api.cpp — the C ABI of include/tpz_gpu.h: context, workspace, launches, error text.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -428,6 +429,43 @@ tpz_err tpz_seek_keys(tpz_ctx* c, const tpz_table* t, const uint8_t* d_keys,
                     t->d_ends, t->d_count, t->d_status, t->d_spill, t->d_spill_off, d_keys,
                     d_key_pos, n_keys, d_block, d_entry, d_status, d_valid};
   tpz::launch_seek(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+// Rust's saturating float-to-unsigned cast (`as u8`, `as usize`): NaN -> 0.
+static uint64_t sat_cast(double x, double hi) {
+  if (!(x == x) || x <= 0.0) return 0;
+  return x >= hi ? (uint64_t)hi : (uint64_t)x;
+}
+
+tpz_err tpz_bloom_geometry(uint64_t n_keys, double fpp, uint64_t* filter_len, uint32_t* k) {
+  if (!filter_len || !k || !(fpp >= 0.0 && fpp < 1.0)) return TPZ_ERR_INVALID_ARG;  // bloom.rs:49
+  const double n = (double)n_keys;
+  const double ln2sq = 0.6931471805599453 * 0.6931471805599453;   // LN_2.powi(2)
+  const double m = -(n * std::log(fpp)) / ln2sq;
+  if (std::isinf(m)) return TPZ_ERR_INVALID_ARG;   // fpp 0: the reference's `% limit` divides by 0
+  uint64_t kk = sat_cast(std::ceil(m / n * ln2sq), 255.0);
+  kk = kk < 1 ? 1 : (kk > 15 ? 15 : kk);
+  *k = (uint32_t)kk;
+  *filter_len = (sat_cast(std::ceil(m), 18446744073709549568.0) + 7) / 8 + 1;
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_bloom_build(tpz_ctx* c, const uint8_t* d_keys, const uint64_t* d_key_pos,
+                        uint32_t n_keys, double fpp, uint8_t* d_filter, void* stream) {
+  if (!c || !d_filter || (n_keys && !d_key_pos) || (reinterpret_cast<uintptr_t>(d_filter) & 3u))
+    return TPZ_ERR_INVALID_ARG;
+  uint64_t len = 0;
+  uint32_t k = 0;
+  tpz_err r = tpz_bloom_geometry(n_keys, fpp, &len, &k);
+  if (r != TPZ_SUCCESS) return r;
+  TPZ_HIP(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  TPZ_HIP(hipMemsetAsync(d_filter, 0, (len + 3) & ~(uint64_t)3, s));
+  TPZ_HIP(hipMemsetAsync(d_filter + len - 1, (int)k, 1, s));        // the last byte is k
+  tpz::BloomBuildLaunch a{d_keys, d_key_pos, n_keys, k, (len - 1) * 8, d_filter};
+  tpz::launch_bloom_build(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
 }

@@ -167,6 +167,16 @@ struct BloomLaunch {
 };
 void launch_bloom(const BloomLaunch& a, hipStream_t stream);
 
+struct BloomBuildLaunch {
+  const uint8_t* keys;
+  const uint64_t* key_pos;
+  uint32_t n_keys;
+  uint32_t k;
+  uint64_t limit;       // bits in the array: (filter_len - 1) * 8
+  uint8_t* filter;      // zeroed bit array, 4-byte aligned, padded to whole words
+};
+void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream);
+
 struct PackLaunch {
   const uint64_t* ext;
   uint32_t n_blocks;

@@ -177,6 +177,23 @@ __global__ __launch_bounds__(256) void bloom_kernel(BloomParams p) {
   p.out[i] = hit;
 }
 
+// Bloom::from_keys (src/bloom.rs:48-70) for keys on the device: one thread per key sets its k
+// probe bits (h + j * rotr(h, 34) mod limit) with 32-bit atomic ORs into the zeroed bit array
+// (the geometry, limit and k, comes from the host: tpz_bloom_geometry).
+__global__ __launch_bounds__(256) void bloom_build_kernel(BloomBuildLaunch a) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_keys) return;
+  const u64 s = a.key_pos[i];
+  u64 h = xxh3::hash64(a.keys + s, a.key_pos[i + 1] - s);
+  const u64 delta = (h >> 34) | (h << 30);                  // Bloom::delta
+  u32* words = reinterpret_cast<u32*>(a.filter);
+  for (u32 j = 0; j < a.k; j++) {
+    const u64 bit = h % a.limit;
+    atomicOr(&words[bit >> 5], 1u << (bit & 31));           // bit_set: byte bit/8, bit bit%8
+    h += delta;
+  }
+}
+
 // Dense entry ends: block b's count[b] {kend, vend} pairs (status OK: from its worst-case-sized
 // slot, tpz_entry_base; OK_SPILLED: from its spill record; zeros otherwise) moved to
 // dense[2 * first[b] ..]. One wave per block.
@@ -239,6 +256,11 @@ void launch_seek(const SeekLaunch& a, hipStream_t stream) {
                a.spill, a.spill_off, a.q, a.q_pos, a.n_q, a.out_block, a.out_entry,
                a.out_status, a.out_valid};
   hipLaunchKernelGGL(seek_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
+}
+
+void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream) {
+  if (a.n_keys && a.limit)
+    hipLaunchKernelGGL(bloom_build_kernel, dim3((a.n_keys + 255) / 256), dim3(256), 0, stream, a);
 }
 
 void launch_bloom(const BloomLaunch& a, hipStream_t stream) {

@@ -9,6 +9,8 @@ the tag src/block/compress.rs:85-89), through tpz_plan_blocks / tpz_encode_block
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -104,3 +106,22 @@ def build_region(ctx: Context, keys, kpos, vals, vpos, block_size: int):
     torch.cuda.synchronize(_dev(ctx.device))
     e = ext[:nb + 1].cpu().numpy().view(np.uint64)
     return out[:int(e[-1])].cpu().numpy(), e.copy(), first[:nb + 1].cpu().numpy().astype(np.int64)
+
+
+def bloom_build(ctx: Context, ent: DeviceEntries, fpp: float,
+                stream: torch.cuda.Stream | None = None) -> bytes:
+    """tpz_bloom_build: Bloom::from_keys (src/bloom.rs:48-70) over xxh3_64 of every entry's key,
+    built on the device (SsTableBuilder::build_bloom, src/table/builder.rs:132-141); returns
+    Bloom::encode's bytes. Raises ValueError where the reference asserts or divides by zero."""
+    geo = _lib.bloom_geometry(ent.n, fpp)
+    if geo is None:
+        raise ValueError(f"no bloom filter for {ent.n} keys at fpp {fpp}")
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    filt = torch.empty((geo[0] + 3) // 4, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().tpz_bloom_build(ctx.handle, C.c_void_p(ent.keys.data_ptr()),
+                                          C.c_void_p(ent.kpos.data_ptr()), ent.n, fpp,
+                                          C.c_void_p(filt.data_ptr()), C.c_void_p(s.cuda_stream)),
+               "tpz_bloom_build")
+    torch.cuda.synchronize(dev)
+    return filt.cpu().numpy().view(np.uint8)[:geo[0]].tobytes()

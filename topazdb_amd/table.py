@@ -435,6 +435,8 @@ class Bloom:
         lnf = math.log(fpp) if fpp > 0.0 else -math.inf
         num = n * lnf
         m = -num / ln2sq if num == num else math.nan
+        if m == math.inf:                     # fpp 0 with keys: `% limit` divides by zero
+            raise ReferencePanic("attempt to calculate the remainder with a divisor of zero")
         k = (m / n * ln2sq) if n > 0 else math.nan
         k = max(1, min(15, _sat_cast(math.ceil(k) if k == k and abs(k) != math.inf else k, 255)))
         nbits = _sat_cast(math.ceil(m) if m == m and abs(m) != math.inf else m, 1 << 64)
@@ -644,7 +646,7 @@ class SsTableBuilder:
         self.values.append(bytes(value))
 
     def build_image(self) -> bytes:
-        from .encode import DeviceEntries, EntryError, encode_blocks, plan_blocks
+        from .encode import DeviceEntries, EntryError, bloom_build, encode_blocks, plan_blocks
         kl = np.fromiter((len(k) for k in self.keys), np.uint64, len(self.keys))
         vl = np.fromiter((len(v) for v in self.values), np.uint64, len(self.values))
         kpos = np.zeros(len(kl) + 1, np.uint64)
@@ -669,7 +671,9 @@ class SsTableBuilder:
         data += struct.pack(">I", meta_off & 0xFFFFFFFF)
         if math.copysign(1.0, self.fpp) > 0:                    # is_sign_positive
             bloom_off = len(data)
-            data += Bloom.from_keys([_lib.xxh3_64(k) for k in self.keys], self.fpp).encode()
+            if _lib.bloom_geometry(len(self.keys), self.fpp) is None:
+                Bloom.from_keys([0] * min(1, len(self.keys)), self.fpp)  # raises the panic
+            data += bloom_build(self.ctx, ent, self.fpp)             # on the device
             data += struct.pack(">I", bloom_off & 0xFFFFFFFF)
         return bytes(data)
 
