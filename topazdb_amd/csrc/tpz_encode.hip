@@ -6,8 +6,9 @@
 //          size + encode_len + 2 <= block_size (size = the block's entry bytes so far);
 //          SsTableBuilder::add (src/table/builder.rs:49-64) starts the next block with the entry
 //          that did not fit. The block starts are the chain 0 -> nx[0] -> ... over entries:
-//            plan_next_kernel   nx[a] = entries of a block that starts at entry a (binary search
-//                               over the entries' prefix sums S, closed form from kpos/vpos)
+//            plan_next_kernel   nx[a] = entries of a block that starts at entry a (galloping
+//                               search over the entries' prefix sums S staged in LDS, closed
+//                               form from kpos/vpos)
 //            plan_table_kernel  per chunk of C entries (C = max(2048, w)), the chain's exit offset into the
 //                               next chunk for every entry offset it can enter at (< w, the
 //                               longest block in entries)
@@ -15,6 +16,8 @@
 //                               composition, log2(chunks) rounds): the entry offset of every chunk
 //            plan_count_kernel + plan_scan_kernel + plan_write_kernel: one walk per chunk counts
 //                               and then writes its block starts and byte extents
+//            (chunks of <= 8192 entries: plan_table_lds_kernel and plan_walk_lds_kernel do the
+//             table and the walks with the chunk's nx staged in LDS, a workgroup per chunk)
 //  encode  Block::encode (src/block.rs:31-44) + Entry::encode (src/block/builder.rs:72-81) +
 //          checksum::calculate_checksum (src/checksum.rs:6-10) + compress::encode Uncompress
 //          (src/block/compress.rs:85-89): block b = [u16 n][n x u16 offset][entries][u32 crc]
@@ -30,6 +33,7 @@
 //                                the waves and shifted to the end with GF(2) multiplies
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "tpz_internal.h"
@@ -223,6 +227,7 @@ struct PlanParams {
   u32* first;        // n + 1: block starts
   u64* ext;          // n + 1: encoded byte extents
   u32* n_blocks;     // one u32
+  u32 guess;         // plan_next_kernel: gallop from the mean entry size (0: bisect only)
 };
 
 __device__ __forceinline__ u64 S_at(const u64* kpos, const u64* vpos, u64 k0, u64 v0, u32 x) {
@@ -236,31 +241,84 @@ __device__ __forceinline__ u64 S_at(const u64* kpos, const u64* vpos, u64 k0, u6
 // blocks), then by plan_reduce_kernel.
 constexpr u32 kNextWG = 256, kNextPer = 2048, kNextWin = 4096;
 
+// The window is staged as {kpos, vpos} relative to the workgroup's first entry (u32 pairs: one
+// ds_read_b64 per probe, and each entry's own lengths come from LDS too); a window whose bytes do
+// not fit u32 takes global probes. A probe sequence starts at the window's mean entry size and
+// gallops (4k config: 3 probes per entry instead of 11 for a bisection over span entries).
 __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
-  __shared__ u64 sw[kNextWin];
+  __shared__ uint2 sw[kNextWin];
   __shared__ u32 wmax[kNextWG / kWave];
   const u32 a0 = blockIdx.x * kNextPer;
-  const u64 k0 = p.kpos[0], v0 = p.vpos[0];
-  const u64 hiw = min((u64)p.n, (u64)a0 + kNextPer - 1 + p.span);   // highest index probed
-  const u32 wn = (u32)(hiw - a0 + 1);
-  const bool in_lds = wn <= kNextWin;
-  if (in_lds)
-    for (u32 i = threadIdx.x; i < wn; i += kNextWG) sw[i] = S_at(p.kpos, p.vpos, k0, v0, a0 + i);
+  const u64 k0 = p.kpos[a0], v0 = p.vpos[a0];
+  const u32 hiw = (u32)min((u64)p.n, (u64)a0 + kNextPer - 1 + p.span);   // highest index probed
+  const u32 wn = hiw - a0 + 1;
+  const bool in_lds = wn <= kNextWin && (p.kpos[hiw] - k0) + (p.vpos[hiw] - v0) + 4ull * wn < (1ull << 32);
+  if (in_lds) {
+    // all of a thread's loads issued before the first LDS write: a loop that stores each pair
+    // as it arrives waits out one memory latency per pair
+    constexpr u32 kR = kNextWin / kNextWG;
+    u64 kk[kR], vv[kR];
+#pragma unroll
+    for (u32 r = 0; r < kR; r++) {
+      const u32 i = threadIdx.x + r * kNextWG;
+      if (i < wn) {
+        kk[r] = p.kpos[a0 + i];
+        vv[r] = p.vpos[a0 + i];
+      }
+    }
+#pragma unroll
+    for (u32 r = 0; r < kR; r++) {
+      const u32 i = threadIdx.x + r * kNextWG;
+      if (i < wn) sw[i] = make_uint2((u32)(kk[r] - k0), (u32)(vv[r] - v0));
+    }
+  }
   __syncthreads();
-  auto S = [&](u32 x) -> u64 { return in_lds ? sw[x - a0] : S_at(p.kpos, p.vpos, k0, v0, x); };
+  // mean encoded entry size over the window (>= 5 B), rounded up: the gallop's first probe
+  const u64 wbytes = 4ull * (wn - 1) + (p.kpos[hiw] - k0) + (p.vpos[hiw] - v0);
+  const u64 mean = wn > 1 ? max((u64)5, (wbytes + wn - 2) / (wn - 1)) : 5;
+  const bool guess = p.guess;
   u32 mx = 0, bad = ~0u;
   for (u32 a = a0 + threadIdx.x; a < min((u64)p.n, (u64)a0 + kNextPer); a += kNextWG) {
-    const u64 kl = p.kpos[a + 1] - p.kpos[a], vl = p.vpos[a + 1] - p.vpos[a];
+    u64 kl, vl, sa;
+    if (in_lds) {
+      const uint2 e0 = sw[a - a0], e1 = sw[a + 1 - a0];
+      kl = e1.x - e0.x;
+      vl = e1.y - e0.y;
+      sa = 4ull * (a - a0) + e0.x + e0.y;
+    } else {
+      kl = p.kpos[a + 1] - p.kpos[a];
+      vl = p.vpos[a + 1] - p.vpos[a];
+      sa = 4ull * (a - a0) + (p.kpos[a] - k0) + (p.vpos[a] - v0);
+    }
     u32 len;
     if (kl == 0 || 4 + kl + vl > p.T) {   // builder.rs:27 assert / an entry no block holds
       bad = min(bad, a);
       len = 1;
     } else {
-      const u64 lim = S(a) + p.T;
+      const u64 lim = sa + p.T;
+      auto S = [&](u32 x) -> u64 {
+        if (!in_lds) return 4ull * (x - a0) + (p.kpos[x] - k0) + (p.vpos[x] - v0);
+        const uint2 e = sw[x - a0];
+        return 4ull * (x - a0) + e.x + e.y;
+      };
       u32 lo = a + 1, hi = (u32)min((u64)p.n, (u64)a + p.span);   // S(lo) <= lim
       if (S(hi) <= lim) {
         lo = hi;
-      } else {
+      } else {   // S(lo) <= lim < S(hi): gallop from the window's mean entry size, then bisect
+        if (guess && hi - lo > 1) {
+          const u32 g = (u32)min((u64)hi - 1, max((u64)lo, (u64)a + p.T / mean));
+          if (S(g) <= lim) {
+            lo = g;
+            u32 d = 1;
+            while (d < hi - lo && S(lo + d) <= lim) { lo += d; d <<= 1; }
+            if (d < hi - lo) hi = lo + d;
+          } else {
+            hi = g;
+            u32 d = 1;
+            while (d < hi - lo && S(hi - d) > lim) { hi -= d; d <<= 1; }
+            if (d < hi - lo) lo = hi - d;
+          }
+        }
         while (hi - lo > 1) {
           const u32 mid = lo + (hi - lo) / 2;
           if (S(mid) <= lim) lo = mid; else hi = mid;
@@ -392,6 +450,84 @@ __global__ __launch_bounds__(256) void plan_write_kernel(PlanParams p) {
     }
   }
   if (k + 1 == p.K) {
+    const u32 nb = *p.n_blocks;
+    p.first[nb] = p.n;
+    p.ext[nb] = S_at(p.kpos, p.vpos, k0, v0, p.n) + 2ull * p.n + 7ull * nb;
+  }
+}
+
+// The same three chain walks with the chunk's nx staged in LDS (chunks of <= kWalkMaxC entries):
+// a step is an LDS read instead of a dependent global load, and the write kernel no longer waits
+// on its own first/ext stores between steps (vmcnt counts stores too). One workgroup per chunk.
+constexpr u32 kWalkMaxC = 8192;
+
+__device__ __forceinline__ u32 stage_chunk_nx(const PlanParams& p, u32 k, u32* snx) {
+  const u64 c0 = (u64)k * p.C;
+  const u32 len = (u32)(min((u64)p.n, c0 + p.C) - c0);
+  // eight loads in flight per thread before their LDS writes (one latency per eight words)
+  for (u32 i0 = threadIdx.x; i0 < len; i0 += 8 * blockDim.x) {
+    u32 v[8];
+#pragma unroll
+    for (u32 r = 0; r < 8; r++) {
+      const u32 i = i0 + r * blockDim.x;
+      if (i < len) v[r] = p.nx[c0 + i];
+    }
+#pragma unroll
+    for (u32 r = 0; r < 8; r++) {
+      const u32 i = i0 + r * blockDim.x;
+      if (i < len) snx[i] = v[r];
+    }
+  }
+  __syncthreads();
+  return len;
+}
+
+__global__ __launch_bounds__(256) void plan_table_lds_kernel(PlanParams p) {
+  extern __shared__ u32 snx[];
+  const u32 k = blockIdx.x;
+  const u32 len = stage_chunk_nx(p, k, snx);
+  for (u32 j = threadIdx.x; j < p.w; j += blockDim.x) {
+    int F = -1;
+    if (j < len) {
+      u32 r = j;
+      while (r < len) r += snx[r];
+      const u64 a = (u64)k * p.C + r;
+      F = a >= p.n ? -1 : (int)(r - p.C);
+    }
+    p.tab_a[(u64)k * p.w + j] = F;
+  }
+}
+
+template <bool kWrite>
+__global__ __launch_bounds__(256) void plan_walk_lds_kernel(PlanParams p) {
+  extern __shared__ u32 snx[];
+  uint16_t* st = reinterpret_cast<uint16_t*>(snx + p.C);     // the chunk's block starts, chunk-relative
+  __shared__ u32 s_count;
+  const u32 k = blockIdx.x;
+  const u64 c0 = (u64)k * p.C;
+  const u32 len = stage_chunk_nx(p, k, snx);
+  if (threadIdx.x == 0) {
+    const u64 a = chunk_entry(p, k);
+    u32 c = 0;
+    if (a != ~0ull)
+      for (u32 r = (u32)(a - c0); r < len; r += snx[r]) st[c++] = (uint16_t)r;
+    s_count = c;
+  }
+  __syncthreads();
+  const u32 c = s_count;
+  if (!kWrite) {
+    if (threadIdx.x == 0) p.cnt[k] = c;
+    return;
+  }
+  const u64 k0 = p.kpos[0], v0 = p.vpos[0];
+  const u32 b0 = p.cnt[k];
+  for (u32 i = threadIdx.x; i < c; i += blockDim.x) {
+    const u32 a = (u32)(c0 + st[i]);
+    const u64 b = (u64)b0 + i;
+    p.first[b] = a;
+    p.ext[b] = S_at(p.kpos, p.vpos, k0, v0, a) + 2ull * a + 7ull * b;   // SsTableBuilder data.len()
+  }
+  if (k + 1 == p.K && threadIdx.x == 0) {
     const u32 nb = *p.n_blocks;
     p.first[nb] = p.n;
     p.ext[nb] = S_at(p.kpos, p.vpos, k0, v0, p.n) + 2ull * p.n + 7ull * nb;
@@ -734,6 +870,8 @@ hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
   if (a.phase == 0) {
     const u32 nwg = (u32)(((u64)a.n + kNextPer - 1) / kNextPer);
     p.wgmax = a.nx + a.n;                 // the caller sizes nx for n + n / 2048 + 1 words
+    static const bool bisect = std::getenv("TPZ_PLAN_BISECT") != nullptr;   // A/B probe
+    p.guess = bisect ? 0u : 1u;
     plan_next_kernel<<<nwg, kNextWG, 0, s>>>(p);
     plan_reduce_kernel<<<1, 1024, 0, s>>>(p, nwg);
     return hipGetLastError();
@@ -743,7 +881,12 @@ hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
   const u32 tg = (u32)((tn + 255) / 256);
   p.tab_a = a.tab_a;
   p.tab_b = a.tab_b;
-  plan_table_kernel<<<tg, 256, 0, s>>>(p);
+  static const bool global_walk = std::getenv("TPZ_PLAN_GLOBAL_WALK") != nullptr;   // A/B probe
+  const bool lds = p.C <= kWalkMaxC && !global_walk;
+  if (lds)
+    plan_table_lds_kernel<<<p.K, 256, p.C * 4, s>>>(p);
+  else
+    plan_table_kernel<<<tg, 256, 0, s>>>(p);
   for (u32 d = 1; d < p.K; d <<= 1) {
     plan_round_kernel<<<tg, 256, 0, s>>>(p, d);
     int* t = p.tab_a;
@@ -751,9 +894,15 @@ hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
     p.tab_b = t;
   }
   const u32 kg = (p.K + 255) / 256;
-  plan_count_kernel<<<kg, 256, 0, s>>>(p);
-  plan_scan_kernel<<<1, 1024, 0, s>>>(p);
-  plan_write_kernel<<<kg, 256, 0, s>>>(p);
+  if (lds) {
+    plan_walk_lds_kernel<false><<<p.K, 256, p.C * 6, s>>>(p);
+    plan_scan_kernel<<<1, 1024, 0, s>>>(p);
+    plan_walk_lds_kernel<true><<<p.K, 256, p.C * 6, s>>>(p);
+  } else {
+    plan_count_kernel<<<kg, 256, 0, s>>>(p);
+    plan_scan_kernel<<<1, 1024, 0, s>>>(p);
+    plan_write_kernel<<<kg, 256, 0, s>>>(p);
+  }
   e = hipGetLastError();
   return e;
 }
