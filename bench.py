@@ -523,6 +523,7 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     alg = int(kpos[etot] - kpos[0]) + int(vpos[etot] - vpos[0]) + 16 * etot + 12 * nb + int(ext[-1])
+    bloom = bloom_build_rate(ctx, ent, stream, dev)
     # the host builder beside it (tpz_build_blocks, one thread: SsTableBuilder's loop restated)
     t0 = time.perf_counter()
     synth.build_blocks(keys, kpos[:etot + 1], vals, vpos[:etot + 1], block_size)
@@ -531,7 +532,38 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
             "cpu_host_builder_ms_1_thread": round(cpu_s * 1e3, 1),
             "gib_s_encoded": round(int(ext[-1]) / (ms * 1e-3) / GIB, 1),
             "algorithmic_bytes": alg, "achieved_gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
-            "frac_of_8tb": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            "frac_of_8tb": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bloom": bloom}
+
+
+def bloom_build_rate(ctx, ent, stream, dev, fpp: float = 0.1, steps: int = 5) -> dict:
+    """SsTableBuilder::build_bloom on the device (tpz_bloom_build: xxh3_64 of every key, k probe
+    bits set with atomics; table/builder.rs:132-141, bloom.rs:48-70) over the shard's keys, HIP
+    events; then every key probed (tpz_bloom_may_contain) must be found: a Bloom filter has no
+    false negatives. Byte parity with Bloom::from_keys is tests/test_gpu_encode.py's job."""
+    import ctypes as C
+    geo = _lib.bloom_geometry(ent.n, fpp)
+    filt = torch.empty((geo[0] + 3) // 4, dtype=torch.int32, device=dev)
+    L = _lib.lib()
+
+    def build():
+        _lib.check(L.tpz_bloom_build(ctx.handle, C.c_void_p(ent.keys.data_ptr()),
+                                     C.c_void_p(ent.kpos.data_ptr()), ent.n, fpp,
+                                     C.c_void_p(filt.data_ptr()), C.c_void_p(stream.cuda_stream)),
+                   "tpz_bloom_build")
+    build()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        build()
+    e1.record(stream)
+    out = torch.empty(ent.n, dtype=torch.uint8, device=dev)
+    ctx.bloom_ptrs(filt.data_ptr(), geo[0], ent.keys.data_ptr(), ent.kpos.data_ptr(), ent.n,
+                   out.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    assert bool((out == 1).all()), "bloom: a key of the filter not found"
+    return {"keys": ent.n, "fpp": fpp, "filter_bytes": geo[0], "k": geo[1], "ms_build": round(ms, 4),
+            "gkeys_s": round(ent.n / (ms * 1e-3) / 1e9, 2)}
 
 
 DEFAULT_BLOCKS = {"4k": 1 << 20, "zipf": 1 << 20, "64k": 65536}

@@ -329,7 +329,9 @@ uint64_t tpz_host_xxh3_64(const uint8_t* h_buf, uint64_t len);
  *     n_keys keys and false-positive rate fpp, with the reference's f64 arithmetic and saturating
  *     casts; TPZ_ERR_INVALID_ARG unless 0 <= fpp < 1 (bloom.rs:49 asserts).
  *   tpz_bloom_build: writes the filter (Bloom::encode) to d_filter[0 .. filter_len). d_filter must
- *     be 4-byte aligned with room for (filter_len + 3) & ~3 bytes. Asynchronous on `stream`. */
+ *     be 4-byte aligned with room for (filter_len + 3) & ~3 bytes. Asynchronous on `stream`;
+ *     uses the stream's grow-only workspace (4 B per probe: n_keys * k * 4 bytes plus slice
+ *     histograms), so one build at a time per stream, as with the other workspace users. */
 tpz_err tpz_bloom_geometry(uint64_t n_keys, double fpp, uint64_t* filter_len, uint32_t* k);
 tpz_err tpz_bloom_build(tpz_ctx* ctx, const uint8_t* d_keys, const uint64_t* d_key_pos,
                         uint32_t n_keys, double fpp, uint8_t* d_filter, void* stream);

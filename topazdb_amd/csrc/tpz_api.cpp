@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -129,6 +130,8 @@ struct tpz_workspace {
   size_t plan0_cap = 0;
   void* d_plan1 = nullptr;      // tpz_plan_blocks: the transfer tables + chunk counts
   size_t plan1_cap = 0;
+  void* d_bloom = nullptr;      // tpz_bloom_build: probe buckets + slice histograms
+  size_t bloom_cap = 0;
 };
 
 struct tpz_ctx {
@@ -149,6 +152,7 @@ void free_workspace(tpz_workspace& w) {
   if (w.d_acc) (void)hipFree(w.d_acc);
   if (w.d_plan0) (void)hipFree(w.d_plan0);
   if (w.d_plan1) (void)hipFree(w.d_plan1);
+  if (w.d_bloom) (void)hipFree(w.d_bloom);
   w = tpz_workspace{};
 }
 
@@ -463,10 +467,21 @@ tpz_err tpz_bloom_build(tpz_ctx* c, const uint8_t* d_keys, const uint64_t* d_key
   TPZ_HIP(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   TPZ_HIP(hipMemsetAsync(d_filter, 0, (len + 3) & ~(uint64_t)3, s));
-  TPZ_HIP(hipMemsetAsync(d_filter + len - 1, (int)k, 1, s));        // the last byte is k
-  tpz::BloomBuildLaunch a{d_keys, d_key_pos, n_keys, k, (len - 1) * 8, d_filter};
+  static const bool atomic_only = std::getenv("TPZ_BLOOM_ATOMIC") != nullptr;   // A/B probe
+  const uint64_t work = atomic_only ? 0 : tpz::bloom_build_work_bytes(n_keys, k, (len - 1) * 8);
+  void* d_work = nullptr;
+  if (work && n_keys) {   // the stream's grow-only scratch (stream-ordered reuse)
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_workspace& w = c->ws[stream];
+    tpz_err r2 = grow(stream, &w.d_bloom, &w.bloom_cap, work);
+    if (r2 != TPZ_SUCCESS) return r2;
+    d_work = w.d_bloom;
+  }
+  tpz::BloomBuildLaunch a{d_keys, d_key_pos, n_keys, k, (len - 1) * 8, d_filter, (len + 3) / 4,
+                          d_work};
   tpz::launch_bloom_build(a, s);
   TPZ_HIP(hipGetLastError());
+  TPZ_HIP(hipMemsetAsync(d_filter + len - 1, (int)k, 1, s));        // the last byte is k
   return TPZ_SUCCESS;
 }
 

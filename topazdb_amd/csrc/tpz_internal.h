@@ -174,7 +174,11 @@ struct BloomBuildLaunch {
   uint32_t k;
   uint64_t limit;       // bits in the array: (filter_len - 1) * 8
   uint8_t* filter;      // zeroed bit array, 4-byte aligned, padded to whole words
+  uint64_t filter_words;  // (filter_len + 3) / 4
+  void* work;           // bloom_build_work_bytes() of device scratch (the partitioned build)
 };
+// Scratch for the partitioned build (0: the filter is too big for it and the atomic kernel runs).
+uint64_t bloom_build_work_bytes(uint32_t n_keys, uint32_t k, uint64_t limit);
 void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream);
 
 struct PackLaunch {

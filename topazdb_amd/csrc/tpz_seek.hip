@@ -15,6 +15,9 @@
 // whose block did not decode gets that block's status (the reference's read_block_cached Err, or
 // its panic for MALFORMED); OK_SPILLED blocks are read from their spill records and report OK.
 
+#if defined(TPZ_BLOOM_ABL_BLOOMBYTES)   // diagnostic: the byte-load xxh3 reads
+#define TPZ_XXH3_BYTEREADS
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -189,9 +192,201 @@ __global__ __launch_bounds__(256) void bloom_build_kernel(BloomBuildLaunch a) {
   u32* words = reinterpret_cast<u32*>(a.filter);
   for (u32 j = 0; j < a.k; j++) {
     const u64 bit = h % a.limit;
+#if defined(TPZ_BLOOM_ABL_BLOOMWG)      // diagnostic: workgroup-scope atomics (wrong across WGs)
+    __hip_atomic_fetch_or(&words[bit >> 5], 1u << (bit & 31), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+#elif defined(TPZ_BLOOM_ABL_BLOOMSTORE) // diagnostic: plain stores (wrong filter)
+    words[bit >> 5] = 1u << (bit & 31);
+#else
     atomicOr(&words[bit >> 5], 1u << (bit & 31));           // bit_set: byte bit/8, bit bit%8
+#endif
     h += delta;
   }
+}
+
+// The partitioned build (filters of <= kBloomMaxSlices slices of 2^19 bits, 64 MiB): the probes are
+// bucketed by slice (count, scan, scatter: LDS histograms and LDS rank counters, no global
+// atomics), then a workgroup per slice ORs its bucket into a 64 KiB LDS slice and writes it out
+// with plain stores. The atomic kernel above spends ~4 ms on 107 M device-scope atomics for
+// 35.6 M keys; this moves ~2.6 GB instead.
+constexpr uint32_t kBloomSliceLog = 19, kBloomSliceBits = 1u << kBloomSliceLog;   // 64 KiB
+constexpr uint32_t kBloomMaxSlices = 1024;          // scatter LDS: 2 S words + 48 KiB <= 64 KiB
+
+constexpr uint32_t kBloomWgProbes = 12288;         // a workgroup's probes staged in LDS (48 KiB)
+
+// keys per workgroup: as many as keep its probes within kBloomWgProbes
+__host__ __device__ inline uint32_t bloom_part_per_wg(uint32_t k) { return kBloomWgProbes / k; }
+__host__ __device__ inline uint32_t bloom_part_wgs(uint32_t n, uint32_t k) {
+  const uint32_t per = bloom_part_per_wg(k);
+  const uint32_t w = (n + per - 1) / per;
+  return w < 1 ? 1 : w;
+}
+
+struct BloomPart {
+  const uint8_t* keys;
+  const uint64_t* key_pos;
+  uint32_t n_keys, k;
+  uint64_t limit;
+  uint32_t S, nwg, per_wg;
+  uint32_t* hist;     // S x nwg, slice-major: the workgroups' probe counts
+  uint32_t* off;      // S x nwg: their exclusive prefix within the slice
+  uint32_t* tot;
+  uint32_t* base;
+  uint32_t* pos;
+  uint32_t* words;
+  uint64_t filter_words;
+};
+
+__device__ __forceinline__ void bloom_count_pass(const BloomPart& p, uint32_t* cnt) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * p.per_wg;
+  const uint64_t i1 = min((uint64_t)p.n_keys, i0 + p.per_wg);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint64_t s = p.key_pos[i];
+    uint64_t h = xxh3::hash64(p.keys + s, p.key_pos[i + 1] - s);
+    const uint64_t delta = (h >> 34) | (h << 30);   // Bloom::delta
+    for (uint32_t j = 0; j < p.k; j++) {
+      atomicAdd(&cnt[(uint32_t)((h % p.limit) >> kBloomSliceLog)], 1u);   // LDS
+      h += delta;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bloom_count_kernel(BloomPart p) {
+  extern __shared__ uint32_t cnt[];
+  for (uint32_t s = threadIdx.x; s < p.S; s += blockDim.x) cnt[s] = 0;
+  __syncthreads();
+  bloom_count_pass(p, cnt);
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < p.S; s += blockDim.x) p.hist[(uint64_t)s * p.nwg + blockIdx.x] = cnt[s];
+}
+
+// off[s][*] = exclusive prefix of hist[s][*] over the workgroups, tot[s] = the slice's probes.
+__global__ __launch_bounds__(256) void bloom_hist_scan_kernel(BloomPart p) {
+  __shared__ uint32_t part[256 / 64];
+  __shared__ uint32_t carry_s;
+  const uint32_t* row = p.hist + (uint64_t)blockIdx.x * p.nwg;
+  uint32_t* orow = p.off + (uint64_t)blockIdx.x * p.nwg;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < p.nwg; b += 256) {
+    const uint32_t w = b + threadIdx.x;
+    const uint32_t v = w < p.nwg ? row[w] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) part[wid] = x;
+    __syncthreads();
+    uint32_t before = carry_s;
+    for (uint32_t q = 0; q < wid; q++) before += part[q];
+    if (w < p.nwg) orow[w] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry_s = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) p.tot[blockIdx.x] = carry_s;
+}
+
+// base[s] = exclusive prefix of tot (one workgroup; S <= kBloomMaxSlices).
+__global__ __launch_bounds__(1024) void bloom_base_scan_kernel(BloomPart p) {
+  __shared__ uint32_t part[1024 / 64];
+  __shared__ uint32_t carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < p.S; b += 1024) {
+    const uint32_t s = b + threadIdx.x;
+    const uint32_t v = s < p.S ? p.tot[s] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) part[wid] = x;
+    __syncthreads();
+    uint32_t before = carry_s;
+    for (uint32_t q = 0; q < wid; q++) before += part[q];
+    if (s < p.S) p.base[s] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + x;
+    __syncthreads();
+  }
+}
+
+// The workgroup's probes are placed in LDS grouped by slice (local offsets from its own counts),
+// then written out in order: consecutive probes of one slice go to consecutive bucket slots, so
+// the stores come out as runs instead of one scattered 4-byte store per probe.
+__global__ __launch_bounds__(256) void bloom_scatter_kernel(BloomPart p) {
+  extern __shared__ uint32_t lds[];
+  uint32_t* loc = lds;                    // S: the local exclusive prefix (then the cursors)
+  uint32_t* gof = lds + p.S;              // S: global slot of the slice's first local probe
+  uint32_t* pr = lds + 2 * p.S;           // kBloomWgProbes: slice << 18 | bit in slice
+  __shared__ uint32_t part[256 / 64];
+  __shared__ uint32_t carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < p.S; b += 256) {       // block scan of this workgroup's counts
+    const uint32_t sl = b + threadIdx.x;
+    const uint64_t e = (uint64_t)sl * p.nwg + blockIdx.x;
+    const uint32_t v = sl < p.S ? p.hist[e] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) part[wid] = x;
+    __syncthreads();
+    uint32_t before = carry_s;
+    for (uint32_t q = 0; q < wid; q++) before += part[q];
+    if (sl < p.S) {
+      loc[sl] = before + x - v;
+      gof[sl] = p.base[sl] + p.off[e];
+    }
+    __syncthreads();
+    if (threadIdx.x == 255) carry_s = before + x;
+    __syncthreads();
+  }
+  const uint32_t total = carry_s;
+  const uint64_t i0 = (uint64_t)blockIdx.x * p.per_wg;
+  const uint64_t i1 = min((uint64_t)p.n_keys, i0 + p.per_wg);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint64_t s = p.key_pos[i];
+    uint64_t h = xxh3::hash64(p.keys + s, p.key_pos[i + 1] - s);
+    const uint64_t delta = (h >> 34) | (h << 30);   // Bloom::delta
+    for (uint32_t j = 0; j < p.k; j++) {
+      const uint64_t bit = h % p.limit;
+      const uint32_t sl = (uint32_t)(bit >> kBloomSliceLog);
+      const uint32_t r = atomicAdd(&loc[sl], 1u);   // LDS: loc[sl] ends at the next slice's start
+      pr[r] = sl << kBloomSliceLog | (uint32_t)(bit & (kBloomSliceBits - 1));
+      h += delta;
+    }
+  }
+  __syncthreads();
+  // loc[sl] is now the end of slice sl's local run; its start is loc[sl] - count
+  for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
+    const uint32_t v = pr[q], sl = v >> kBloomSliceLog;
+    const uint32_t start = loc[sl] - p.hist[(uint64_t)sl * p.nwg + blockIdx.x];
+    p.pos[(uint64_t)gof[sl] + (q - start)] = v & (kBloomSliceBits - 1);
+  }
+}
+
+// Slice s: OR its bucket into LDS, then store the slice's words (those below filter_words).
+__global__ __launch_bounds__(1024) void bloom_fill_kernel(BloomPart p) {
+  __shared__ uint32_t sl[kBloomSliceBits / 32];
+  for (uint32_t w = threadIdx.x; w < kBloomSliceBits / 32; w += blockDim.x) sl[w] = 0;
+  __syncthreads();
+  const uint32_t b0 = p.base[blockIdx.x], n = p.tot[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t b = p.pos[(uint64_t)b0 + i];
+    atomicOr(&sl[b >> 5], 1u << (b & 31));          // LDS
+  }
+  __syncthreads();
+  const uint64_t w0 = (uint64_t)blockIdx.x * (kBloomSliceBits / 32);
+  for (uint32_t w = threadIdx.x; w < kBloomSliceBits / 32; w += blockDim.x)
+    if (w0 + w < p.filter_words) p.words[w0 + w] = sl[w];
 }
 
 // Dense entry ends: block b's count[b] {kend, vend} pairs (status OK: from its worst-case-sized
@@ -258,9 +453,43 @@ void launch_seek(const SeekLaunch& a, hipStream_t stream) {
   hipLaunchKernelGGL(seek_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
 }
 
+uint64_t bloom_build_work_bytes(uint32_t n_keys, uint32_t k, uint64_t limit) {
+  const uint64_t S = (limit + kBloomSliceBits - 1) >> kBloomSliceLog;
+  if (S == 0 || S > kBloomMaxSlices || (uint64_t)n_keys * k >= (1ull << 32)) return 0;
+  const uint64_t nwg = bloom_part_wgs(n_keys, k);
+  return 4ull * ((uint64_t)n_keys * k + 2 * S * nwg + 2 * S + 64);
+}
+
 void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream) {
-  if (a.n_keys && a.limit)
+  if (!a.n_keys || !a.limit) return;
+  const uint64_t S = (a.limit + kBloomSliceBits - 1) >> kBloomSliceLog;
+  if (!a.work || S > kBloomMaxSlices) {
     hipLaunchKernelGGL(bloom_build_kernel, dim3((a.n_keys + 255) / 256), dim3(256), 0, stream, a);
+    return;
+  }
+  BloomPart p{};
+  p.keys = a.keys;
+  p.key_pos = a.key_pos;
+  p.n_keys = a.n_keys;
+  p.k = a.k;
+  p.limit = a.limit;
+  p.S = (uint32_t)S;
+  p.nwg = bloom_part_wgs(a.n_keys, a.k);
+  p.per_wg = bloom_part_per_wg(a.k);
+  uint32_t* w = static_cast<uint32_t*>(a.work);
+  p.hist = w;                                    // S x nwg, slice-major
+  p.off = w + (uint64_t)p.S * p.nwg;             // S x nwg
+  p.tot = p.off + (uint64_t)p.S * p.nwg;         // S slice totals
+  p.base = p.tot + p.S;                          // S slice bases
+  p.pos = p.base + p.S + 64;                     // n_keys x k in-slice bit offsets
+  p.words = reinterpret_cast<uint32_t*>(a.filter);
+  p.filter_words = a.filter_words;
+  hipLaunchKernelGGL(bloom_count_kernel, dim3(p.nwg), dim3(256), p.S * 4, stream, p);
+  hipLaunchKernelGGL(bloom_hist_scan_kernel, dim3(p.S), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(bloom_base_scan_kernel, dim3(1), dim3(1024), 0, stream, p);
+  hipLaunchKernelGGL(bloom_scatter_kernel, dim3(p.nwg), dim3(256), (2 * p.S + kBloomWgProbes) * 4,
+                     stream, p);
+  hipLaunchKernelGGL(bloom_fill_kernel, dim3(p.S), dim3(1024), 0, stream, p);
 }
 
 void launch_bloom(const BloomLaunch& a, hipStream_t stream) {

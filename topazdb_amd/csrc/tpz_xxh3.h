@@ -48,13 +48,27 @@ TPZ_HD inline uint64_t secret64(uint32_t off) {
 }
 TPZ_HD inline uint32_t secret32(uint32_t off) { return (uint32_t)secret64(off); }
 
+// Little-endian reads at any alignment: one (unaligned) dwordx2 / dword load on gfx950 instead of
+// eight / four byte loads (TPZ_XXH3_BYTEREADS keeps the byte loads, for A/B builds).
 TPZ_HD inline uint64_t rd64(const uint8_t* p) {
+#if defined(TPZ_XXH3_BYTEREADS)
   uint64_t v = 0;
   for (int i = 7; i >= 0; i--) v = (v << 8) | p[i];
   return v;
+#else
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+#endif
 }
 TPZ_HD inline uint32_t rd32(const uint8_t* p) {
+#if defined(TPZ_XXH3_BYTEREADS)
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+#else
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+#endif
 }
 TPZ_HD inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 TPZ_HD inline uint64_t swap64(uint64_t x) {
