@@ -20,6 +20,7 @@
 #endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "tpz_internal.h"
 #include "tpz_xxh3.h"
@@ -235,6 +236,7 @@ struct BloomPart {
   uint32_t* pos;
   uint32_t* words;
   uint64_t filter_words;
+  uint32_t* stage;    // gather path: nwg x kBloomWgProbes, each workgroup's probes grouped by slice
 };
 
 __device__ __forceinline__ void bloom_count_pass(const BloomPart& p, uint32_t* cnt) {
@@ -373,6 +375,88 @@ __global__ __launch_bounds__(256) void bloom_scatter_kernel(BloomPart p) {
   }
 }
 
+// The gather path (TPZ_BLOOM_GATHER, under evaluation): one pass over the keys. A workgroup counts its probes per slice,
+// scans the counts (hist / off = its per-slice counts and local offsets, slice-major), hashes its
+// keys again (L2-resident) to place the probes grouped by slice in LDS, and stores them as one
+// contiguous block of its own. A workgroup per slice then gathers the slice's run from every
+// workgroup's block (thread t takes runs t, t + 1024, ...; eight loads in flight per batch).
+__global__ __launch_bounds__(256) void bloom_stage_kernel(BloomPart p) {
+  extern __shared__ uint32_t lds[];
+  uint32_t* cnt = lds;                    // S
+  uint32_t* cur = lds + p.S;              // S
+  uint32_t* pr = lds + 2 * p.S;           // kBloomWgProbes
+  __shared__ uint32_t part[256 / 64];
+  __shared__ uint32_t carry_s;
+  for (uint32_t sl = threadIdx.x; sl < p.S; sl += blockDim.x) cnt[sl] = 0;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  bloom_count_pass(p, cnt);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  for (uint32_t b = 0; b < p.S; b += 256) {
+    const uint32_t sl = b + threadIdx.x;
+    const uint32_t v = sl < p.S ? cnt[sl] : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) part[wid] = x;
+    __syncthreads();
+    uint32_t before = carry_s;
+    for (uint32_t q = 0; q < wid; q++) before += part[q];
+    if (sl < p.S) {
+      cur[sl] = before + x - v;
+      const uint64_t e = (uint64_t)sl * p.nwg + blockIdx.x;
+      p.hist[e] = v;
+      p.off[e] = before + x - v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 255) carry_s = before + x;
+    __syncthreads();
+  }
+  const uint32_t total = carry_s;
+  const uint64_t i0 = (uint64_t)blockIdx.x * p.per_wg;
+  const uint64_t i1 = min((uint64_t)p.n_keys, i0 + p.per_wg);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint64_t s = p.key_pos[i];
+    uint64_t h = xxh3::hash64(p.keys + s, p.key_pos[i + 1] - s);
+    const uint64_t delta = (h >> 34) | (h << 30);   // Bloom::delta
+    for (uint32_t j = 0; j < p.k; j++) {
+      const uint64_t bit = h % p.limit;
+      const uint32_t r = atomicAdd(&cur[(uint32_t)(bit >> kBloomSliceLog)], 1u);   // LDS
+      pr[r] = (uint32_t)(bit & (kBloomSliceBits - 1));
+      h += delta;
+    }
+  }
+  __syncthreads();
+  uint32_t* dst = p.stage + (uint64_t)blockIdx.x * kBloomWgProbes;
+  for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) dst[q] = pr[q];
+}
+
+__global__ __launch_bounds__(1024) void bloom_gather_kernel(BloomPart p) {
+  __shared__ uint32_t sl[kBloomSliceBits / 32];
+  for (uint32_t w = threadIdx.x; w < kBloomSliceBits / 32; w += blockDim.x) sl[w] = 0;
+  __syncthreads();
+  const uint64_t row = (uint64_t)blockIdx.x * p.nwg;
+  for (uint32_t w = threadIdx.x; w < p.nwg; w += blockDim.x) {
+    const uint32_t c = p.hist[row + w], o = p.off[row + w];
+    const uint32_t* src = p.stage + (uint64_t)w * kBloomWgProbes + o;
+    for (uint32_t i = 0; i < c; i += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t r = 0; r < 8; r++) v[r] = i + r < c ? src[i + r] : 0u;
+#pragma unroll
+      for (uint32_t r = 0; r < 8; r++)
+        if (i + r < c) atomicOr(&sl[v[r] >> 5], 1u << (v[r] & 31));   // LDS
+    }
+  }
+  __syncthreads();
+  const uint64_t w0 = (uint64_t)blockIdx.x * (kBloomSliceBits / 32);
+  for (uint32_t w = threadIdx.x; w < kBloomSliceBits / 32; w += blockDim.x)
+    if (w0 + w < p.filter_words) p.words[w0 + w] = sl[w];
+}
+
 // Slice s: OR its bucket into LDS, then store the slice's words (those below filter_words).
 __global__ __launch_bounds__(1024) void bloom_fill_kernel(BloomPart p) {
   __shared__ uint32_t sl[kBloomSliceBits / 32];
@@ -457,7 +541,7 @@ uint64_t bloom_build_work_bytes(uint32_t n_keys, uint32_t k, uint64_t limit) {
   const uint64_t S = (limit + kBloomSliceBits - 1) >> kBloomSliceLog;
   if (S == 0 || S > kBloomMaxSlices || (uint64_t)n_keys * k >= (1ull << 32)) return 0;
   const uint64_t nwg = bloom_part_wgs(n_keys, k);
-  return 4ull * ((uint64_t)n_keys * k + 2 * S * nwg + 2 * S + 64);
+  return 4ull * (nwg * kBloomWgProbes + 2 * S * nwg + 2 * S + 64);   // >= n_keys * k probes
 }
 
 void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream) {
@@ -482,8 +566,16 @@ void launch_bloom_build(const BloomBuildLaunch& a, hipStream_t stream) {
   p.tot = p.off + (uint64_t)p.S * p.nwg;         // S slice totals
   p.base = p.tot + p.S;                          // S slice bases
   p.pos = p.base + p.S + 64;                     // n_keys x k in-slice bit offsets
+  p.stage = p.pos;                               // or nwg x kBloomWgProbes (gather path)
   p.words = reinterpret_cast<uint32_t*>(a.filter);
   p.filter_words = a.filter_words;
+  static const bool gather = std::getenv("TPZ_BLOOM_GATHER") != nullptr;   // A/B probe
+  if (gather) {
+    hipLaunchKernelGGL(bloom_stage_kernel, dim3(p.nwg), dim3(256), (2 * p.S + kBloomWgProbes) * 4,
+                       stream, p);
+    hipLaunchKernelGGL(bloom_gather_kernel, dim3(p.S), dim3(1024), 0, stream, p);
+    return;
+  }
   hipLaunchKernelGGL(bloom_count_kernel, dim3(p.nwg), dim3(256), p.S * 4, stream, p);
   hipLaunchKernelGGL(bloom_hist_scan_kernel, dim3(p.S), dim3(256), 0, stream, p);
   hipLaunchKernelGGL(bloom_base_scan_kernel, dim3(1), dim3(1024), 0, stream, p);
