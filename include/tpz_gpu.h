@@ -39,6 +39,17 @@
 extern "C" {
 #endif
 
+/* ---- ABI version -------------------------------------------------------------------------
+ * Bumped on every incompatible change of a status value, a struct layout or a record format:
+ *   1  round 1: statuses 0..7 with 6 = OVERLAP, 7 = TOO_LARGE (device limits); 5-field columns
+ *   2  6 = OK_SPILLED, 7 = SPILL_FULL, 8 = CODEC_ERROR; spill arena fields in tpz_columns
+ *   3  9 = BAD_ENTRY (a CRC-valid block with out-of-range entries decodes, with per-entry
+ *      classes in its spill record, instead of MALFORMED); MALFORMED is now only the block-level
+ *      panic of Block::decode; tpz_decode_blocks_host also takes snappy / lz4 blocks
+ * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
+#define TPZ_ABI_VERSION 3
+int tpz_abi_version(void);
+
 /* ---- API return codes ------------------------------------------------------------------- */
 typedef enum {
   TPZ_SUCCESS = 0,
@@ -57,26 +68,56 @@ typedef enum {
   TPZ_BLOCK_UNSUPPORTED_CODEC = 3, /* tag 2 (snappy) / 3 (lz4) given to tpz_decode_blocks
                                       without the codec step (tpz_decompress_blocks) first    */
   TPZ_BLOCK_CHECKSUM_MISMATCH = 4, /* Err("checksum: expected E, actual A") checksum.rs:18-21 */
-  TPZ_BLOCK_MALFORMED = 5,         /* CRC-valid, but the reference panics on it: payload too
-                                      short for n/offsets (block.rs:49-59) or an entry out of
-                                      range (iterator.rs:74-82)                              */
+  TPZ_BLOCK_MALFORMED = 5,         /* CRC-valid, but Block::decode itself panics on it: the
+                                      decompressed block is shorter than its CRC, or the payload
+                                      is too short for n / the n offsets (block.rs:49-59)      */
   TPZ_BLOCK_OK_SPILLED = 6,        /* Ok(Block); all entries decoded, into the spill arena
                                       (tpz_columns.d_spill) instead of the block's slot: the
                                       decoded bytes do not fit the slot (entries that overlap or
                                       repeat, which iterator.rs:63-83 accepts: 6*n > len or
-                                      value_start(K) + V > len + 2), or the block is longer than
-                                      TPZ_LDS_BLOCK_BYTES. Same answer as TPZ_BLOCK_OK.        */
+                                      value_start(K) + V > len + 2), or the block is too long
+                                      for the LDS paths (longer than TPZ_LDS_BLOCK_BYTES with
+                                      64+ entries, or longer than TPZ_BIGWAVE_BLOCK_BYTES).
+                                      Same answer as TPZ_BLOCK_OK.                             */
   TPZ_BLOCK_SPILL_FULL = 7,        /* Ok(Block) in the reference, but the caller's spill arena
                                       was too small for this block's record:
                                       d_spill_off[i] = the bytes it needs. Decode again with
                                       spill_cap >= *d_spill_used.                               */
-  TPZ_BLOCK_CODEC_ERROR = 8        /* Err of the codec: snap's decompress_vec rejects the
+  TPZ_BLOCK_CODEC_ERROR = 8,       /* Err of the codec: snap's decompress_vec rejects the
                                       stream (compress.rs:104-107)                           */
+  TPZ_BLOCK_BAD_ENTRY = 9          /* Ok(Block): Block::decode succeeds (block.rs:46-65 checks
+                                      no entry), but at least one entry lies out of range, and
+                                      BlockIterator panics when it reaches that entry
+                                      (iterator.rs:74-82, :91-109). Decoded into the spill arena
+                                      like OK_SPILLED, count[i] = n, with one class byte per
+                                      entry in the record (tpz_entry_class, below), so that a
+                                      reader fails exactly where the reference's iterator does:
+                                      a scan stopped by an empty key before the bad entry, a seek
+                                      whose bisection never touches it and SsTable::open's first
+                                      and last entry all succeed.                              */
 } tpz_block_status;
 
+/* Per-entry class of a TPZ_BLOCK_BAD_ENTRY block (its spill record), in the reference's terms
+ * for entry i at o = offsets[i] in data (L = data.len(), src/block/iterator.rs:74-82):
+ *   OK         the entry reads whole: key and value are in the record
+ *   BAD_VALUE  key readable (o + 2 + klen <= L), value not (o + 4 + klen + vlen > L): the key is
+ *              in the record, the value is empty; seek_to(i) panics, while seek_to_key's
+ *              bisection (which reads keys only, :95-98) may compare against the key
+ *   BAD_KEY    o + 2 > L or o + 2 + klen > L: key and value empty; any read of entry i panics */
+typedef enum {
+  TPZ_ENTRY_OK = 0,
+  TPZ_ENTRY_BAD_VALUE = 1,
+  TPZ_ENTRY_BAD_KEY = 2
+} tpz_entry_class;
+
 /* The largest block the LDS decode paths stage whole (every block a block_size <= 64 KiB
- * BlockBuilder emits fits); longer blocks are decoded by the spill path, straight from HBM. */
+ * BlockBuilder emits fits); longer blocks with 64 or more entries are decoded by the spill path,
+ * straight from HBM. */
 #define TPZ_LDS_BLOCK_BYTES 94192u
+/* Longer blocks with fewer than 64 entries are decoded one wave per block straight from HBM
+ * (the bigwave path, as OK) up to this length; past it by the spill path (OK_SPILLED). No block
+ * length limit exists: the spill path decodes any length the extents can express. */
+#define TPZ_BIGWAVE_BLOCK_BYTES 0x40000000u
 
 /* ---- batch input -------------------------------------------------------------------------
  * Encoded blocks back to back in one device buffer (an SST data region [0, meta_off), or the
@@ -108,21 +149,25 @@ typedef struct {
  *           vs = tpz_value_start(K):
  *             key_j   = data[s +      (j ? ends[2(e+j-1)]   : 0) .. s +      ends[2(e+j)]]
  *             value_j = data[s + vs + (j ? ends[2(e+j-1)+1] : 0) .. s + vs + ends[2(e+j)+1]]
- *   count[i]  : entries in block i (n) for OK, OK_SPILLED and SPILL_FULL, else 0
+ *   count[i]  : entries in block i (n) for OK, OK_SPILLED, BAD_ENTRY and SPILL_FULL, else 0
  *   status[i] : tpz_block_status
  *   crc[i]    : CRC-32 the device computed over the payload (valid for OK, OK_SPILLED,
- *               SPILL_FULL, MALFORMED, CHECKSUM_MISMATCH; the stored one is the payload's
- *               trailing u32)
+ *               BAD_ENTRY, SPILL_FULL, MALFORMED (n / offsets too short), CHECKSUM_MISMATCH;
+ *               the stored one is the payload's trailing u32)
  * Bytes of a slot beyond the block's own data are unspecified. A slot spans at most
  * len + 129 bytes (len = the block's encoded length), which never reaches the next slot.
  *
  * Spill arena. A block whose decoded bytes do not fit its slot (the reference iterator accepts
  * offsets that overlap or repeat, so n entries may materialise up to n * 65535 key and value
- * bytes each), or one longer than TPZ_LDS_BLOCK_BYTES, is decoded into the caller's spill arena
- * and reported TPZ_BLOCK_OK_SPILLED. Its record starts at r = d_spill_off[i] (128-aligned):
+ * bytes each), one too long for the LDS paths, or one with out-of-range entries is decoded into
+ * the caller's spill arena and reported TPZ_BLOCK_OK_SPILLED (TPZ_BLOCK_BAD_ENTRY for the last
+ * kind). Its record starts at r = d_spill_off[i] (128-aligned):
  *   u32 ends[2*count[i]] at d_spill[r ..]         {kend, vend} pairs, exactly as in the slot
  *   stream at d_spill[r + tpz_spill_stream(count[i]) ..]: keys, then values from
  *                                                 tpz_value_start(K), as in the slot
+ *   BAD_ENTRY only: count[i] class bytes (tpz_entry_class) at
+ *                   d_spill[r + tpz_spill_classes(count[i], K, V) ..], K / V = the last kend /
+ *                   vend; an entry's unreadable key or value is empty in ends and stream
  * (K and V each fit in 32 bits: at most 65535 entries of at most 65535 bytes.) Records are
  * placed by an atomic cursor; *d_spill_used = the bytes every spilled block of the call asked
  * for (the library zeroes it first). A record that does not fit spill_cap leaves the block
@@ -137,7 +182,7 @@ typedef struct {
   uint32_t* d_crc;          /* n_blocks */
   uint8_t* d_spill;         /* spill arena (see above), spill_cap bytes; may be NULL if 0   */
   uint64_t spill_cap;
-  uint64_t* d_spill_off;    /* n_blocks: written for OK_SPILLED and SPILL_FULL blocks only   */
+  uint64_t* d_spill_off;    /* n_blocks: written for OK_SPILLED, BAD_ENTRY, SPILL_FULL only   */
   uint64_t* d_spill_used;   /* one u64                                                      */
 } tpz_columns;
 
@@ -148,6 +193,11 @@ static inline uint64_t tpz_spill_stream(uint64_t n) {
 /* Bytes of a spilled record with n entries, K key and V value bytes (128-aligned). */
 static inline uint64_t tpz_spill_record_bytes(uint64_t n, uint64_t k, uint64_t v) {
   return tpz_spill_stream(n) + ((((k + 15u) & ~(uint64_t)15u) + v + 127u) & ~(uint64_t)127u);
+}
+/* Offset of a BAD_ENTRY record's class bytes from the record start (its ends and stream come
+ * first); the record then spans tpz_spill_classes(n, K, V) + n bytes, 128-aligned. */
+static inline uint64_t tpz_spill_classes(uint64_t n, uint64_t k, uint64_t v) {
+  return tpz_spill_record_bytes(n, k, v);
 }
 
 static inline uint64_t tpz_slot_base(uint64_t ext_i, uint64_t i) {
@@ -173,6 +223,7 @@ uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i);
 uint64_t tpz_layout_data_capacity(uint64_t src_bytes, uint64_t n_blocks);
 uint64_t tpz_layout_entry_capacity(uint64_t src_bytes, uint64_t n_blocks);
 uint64_t tpz_layout_spill_stream(uint64_t n);
+uint64_t tpz_layout_spill_classes(uint64_t n, uint64_t k, uint64_t v);
 
 /* ---- context ------------------------------------------------------------------------------ */
 typedef struct tpz_ctx tpz_ctx;
@@ -198,8 +249,8 @@ tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_column
  * ends reserve the worst case (a pair per 6 input bytes, ~1.33x the input) so that blocks need no
  * prefix pass; this packs the used pairs. d_first = exclusive prefix sums of out->d_count
  * (n_blocks + 1 entries, from the caller's device scan); block i's count[i] {kend, vend} pairs go
- * to d_dense[2*d_first[i] .. 2*d_first[i+1]) (for OK_SPILLED blocks from their spill records;
- * zeros for a block whose status is neither OK nor OK_SPILLED). */
+ * to d_dense[2*d_first[i] .. 2*d_first[i+1]) (for OK_SPILLED and BAD_ENTRY blocks from their
+ * spill records; zeros for a block whose status is none of OK, OK_SPILLED, BAD_ENTRY). */
 tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* cols,
                       const uint64_t* d_first, uint32_t* d_dense, void* stream);
 
@@ -217,7 +268,8 @@ tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* c
  *             exactly as tpz_decode_blocks writes it for this batch (slot bases from h_ext)
  *   h_ends    every decoded block's {kend, vend} pairs, dense in block order: block i's at
  *             h_ends[2*h_first[i] ..]; ends_cap = its capacity in u32
- *   h_first   n + 1 entries: h_first[i] = pairs before block i (OK and OK_SPILLED blocks only)
+ *   h_first   n + 1 entries: h_first[i] = pairs before block i (OK, OK_SPILLED and BAD_ENTRY
+ *             blocks only)
  *   h_count, h_status, h_crc    n each, as tpz_columns
  *   h_spill, spill_cap, h_spill_off, h_spill_used   as tpz_columns, in host memory: spilled
  *             blocks' records (the library's device arenas grow as needed)
@@ -294,7 +346,10 @@ tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_d
  *     d_block/d_entry = the position, d_valid = is_valid() (iterator.rs:50-52: the current key
  *     is non-empty), d_status = the status of the last block the seek read (non-OK: the
  *     reference's read_block_cached Err, or its panic for MALFORMED; a table with no blocks
- *     gives MALFORMED: block_metas[0] panics; OK_SPILLED blocks are read from their spill
+ *     gives MALFORMED: block_metas[0] panics; so does a seek whose bisection reads the key of
+ *     a BAD_KEY entry or which lands on a BAD_KEY / BAD_VALUE entry (iterator.rs:91-109, the
+ *     reference's panic; entries of a BAD_ENTRY block the seek does not touch do not matter);
+ *     OK_SPILLED and BAD_ENTRY blocks are read from their spill
  *     records and report OK).
  *   tpz_bloom_may_contain: SsTable::may_contain (src/table.rs:114-119) = Bloom::may_contain
  *     (src/bloom.rs:72-84) of xxh3_64(key) for every key; d_filter = Bloom::encode (the bit
@@ -310,7 +365,8 @@ typedef struct {
   const uint32_t* d_ends;
   const uint32_t* d_count;
   const uint8_t* d_status;
-  const uint8_t* d_spill;      /* the decode's spill arena and record offsets (OK_SPILLED) */
+  const uint8_t* d_spill;      /* the decode's spill arena and record offsets (OK_SPILLED,
+                                  BAD_ENTRY)                                               */
   const uint64_t* d_spill_off;
 } tpz_table;
 
@@ -406,7 +462,7 @@ uint32_t tpz_host_crc32(const uint8_t* h_buf, uint64_t len);
 /* Writes the reference's error text for a block outcome into buf (NUL-terminated):
  * "data is empty", "invaild data", "checksum: expected E, actual A" (decimal, as Rust's {}),
  * "unsupported codec", "malformed block", "spill arena too small", "decompression failed",
- * "" for OK and OK_SPILLED.
+ * "" for OK, OK_SPILLED and BAD_ENTRY (an Ok(Block); its bad entries panic on access).
  * Returns the text length. */
 int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actual, char* buf,
                            size_t cap);

@@ -181,26 +181,40 @@ static void block_decode(const uint8_t* b, size_t len, blockview* v) {
   v->status = TPZO_OK;
 }
 
-/* BlockIterator::seek_to (src/block/iterator.rs:63-83) for index i; returns 0 when the
+/* Entry i of a decoded block as BlockIterator reads it (src/block/iterator.rs:63-83 and the
+ * bisection's key read, :95-98): `&data[offset..]` and get_u16 need offset + 2 <= L, `buf[..klen]`
+ * needs offset + 2 + klen <= L (BAD_KEY otherwise), the second get_u16 and `buf[..vlen]` need
+ * offset + 4 + klen + vlen <= L (BAD_VALUE otherwise). The readable parts are returned: key and
+ * value for OK, the key for BAD_VALUE (with *vl = 0), nothing for BAD_KEY. */
+static int entry_class(const blockview* v, uint32_t i, const uint8_t** k, uint32_t* kl,
+                       const uint8_t** val, uint32_t* vl) {
+  *kl = *vl = 0;
+  *k = *val = v->data;
+  size_t o = be16(v->offs + 2 * (size_t)i);                      /* :74 */
+  if (o + 2 > v->data_len) return TPZO_ENTRY_BAD_KEY;            /* :75-77 */
+  uint32_t klen = be16(v->data + o);
+  if (o + 2 + klen > v->data_len) return TPZO_ENTRY_BAD_KEY;     /* :78 */
+  *k = v->data + o + 2;
+  *kl = klen;
+  if (o + 2 + klen + 2 > v->data_len) return TPZO_ENTRY_BAD_VALUE; /* :80 */
+  uint32_t vlen = be16(v->data + o + 2 + klen);
+  if (o + 4 + klen + vlen > v->data_len) return TPZO_ENTRY_BAD_VALUE; /* :81-82 */
+  *val = v->data + o + 4 + klen;
+  *vl = vlen;
+  return TPZO_ENTRY_OK;
+}
+
+/* BlockIterator::seek_to (src/block/iterator.rs:63-83) for index i < n; returns 0 when the
  * reference would panic (Buf::get_u16 underflow / slice out of range). */
 static int entry_at(const blockview* v, uint32_t i, const uint8_t** k, uint32_t* kl,
                     const uint8_t** val, uint32_t* vl) {
-  size_t o = be16(v->offs + 2 * (size_t)i);                      /* :74 */
-  if (o + 2 > v->data_len) return 0;                             /* :75-77 */
-  uint32_t klen = be16(v->data + o);
-  if (o + 2 + klen + 2 > v->data_len) return 0;                  /* :78-81 */
-  uint32_t vlen = be16(v->data + o + 2 + klen);
-  if (o + 4 + klen + vlen > v->data_len) return 0;               /* :82 */
-  *k = v->data + o + 2;
-  *kl = klen;
-  *val = v->data + o + 4 + klen;
-  *vl = vlen;
-  return 1;
+  return entry_class(v, i, k, kl, val, vl) == TPZO_ENTRY_OK;
 }
 
-/* Decode a block and validate every entry the way an iteration over all indices would
+/* Decode a block and classify every entry the way an iteration over all indices would read it
  * (iterator.rs:63-83 reads entry i at offsets[i] with no ordering or disjointness check: entries
- * may overlap or repeat). Sets TPZO_MALFORMED on any panicking entry. */
+ * may overlap or repeat). Block::decode itself checks no entry (block.rs:46-65): a block with an
+ * out-of-range entry is still Ok, reported TPZO_BAD_ENTRY here. kt / vt = the readable bytes. */
 static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt, uint64_t* vt) {
   block_decode(b, len, v);
   *kt = *vt = 0;
@@ -208,11 +222,12 @@ static void block_full(const uint8_t* b, size_t len, blockview* v, uint64_t* kt,
   for (uint32_t i = 0; i < v->n; i++) {
     const uint8_t *k, *val;
     uint32_t kl, vl;
-    if (!entry_at(v, i, &k, &kl, &val, &vl)) { v->status = TPZO_MALFORMED; *kt = *vt = 0; return; }
+    if (entry_class(v, i, &k, &kl, &val, &vl) != TPZO_ENTRY_OK) v->status = TPZO_BAD_ENTRY;
     *kt += kl;
     *vt += vl;
   }
 }
+static int block_ok(int st) { return st == TPZO_OK || st == TPZO_BAD_ENTRY; }
 
 void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint64_t* n_entries, uint64_t* key_bytes, uint64_t* val_bytes) {
@@ -225,7 +240,7 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
     size_t blen;
     if (codec_step(src + ext[i], ext[i + 1] - ext[i], &buf, &blk, &blen) == 0) {
       block_full(blk, blen, &v, &kt, &vt);
-      if (v.status == TPZO_OK) { ne += v.n; kb += kt; vb += vt; }
+      if (block_ok(v.status)) { ne += v.n; kb += kt; vb += vt; }
     }
     free(buf);
   }
@@ -237,7 +252,7 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
 int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint8_t* status, uint32_t* crc_actual, uint32_t* crc_expected,
                       uint32_t* count, uint32_t* klen, uint32_t* vlen,
-                      uint8_t* keys, uint8_t* vals) {
+                      uint8_t* keys, uint8_t* vals, uint8_t* cls) {
   uint64_t e = 0, kp = 0, vp = 0;
   for (uint32_t i = 0; i < n_blocks; i++) {
     blockview v;
@@ -256,12 +271,13 @@ int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
     crc_actual[i] = v.crc_actual;
     crc_expected[i] = v.crc_expected;
     count[i] = 0;
-    if (v.status != TPZO_OK) { free(buf); continue; }
+    if (!block_ok(v.status)) { free(buf); continue; }
     count[i] = v.n;
     for (uint32_t j = 0; j < v.n; j++, e++) {
       const uint8_t *k, *val;
       uint32_t kl, vl;
-      entry_at(&v, j, &k, &kl, &val, &vl);
+      const int c = entry_class(&v, j, &k, &kl, &val, &vl);
+      if (cls) cls[e] = (uint8_t)c;
       klen[e] = kl;
       vlen[e] = vl;
       memcpy(keys + kp, k, kl);
@@ -332,34 +348,41 @@ static void set_bytes(uint8_t** dst, size_t* cap, size_t* len, const uint8_t* s,
   *len = n;
 }
 
-/* BlockIterator::seek_to (iterator.rs:63-83). A panicking entry leaves the iterator invalid. */
-static void biter_seek_to(tpzo_sst_iter* it, uint32_t i) {
+/* BlockIterator::seek_to (iterator.rs:63-83). Returns TPZO_PANIC where the reference panics
+ * (an entry out of range: :74-82), else 0. */
+static int biter_seek_to(tpzo_sst_iter* it, uint32_t i) {
   it->kl = it->vl = 0;
-  if (i >= it->blk.n) { it->bidx = it->blk.n; return; }
+  if (i >= it->blk.n) { it->bidx = it->blk.n; return 0; }
   it->bidx = i;
   const uint8_t *k, *v;
   uint32_t kl, vl;
-  if (!entry_at(&it->blk, i, &k, &kl, &v, &vl)) return;
+  if (!entry_at(&it->blk, i, &k, &kl, &v, &vl)) return TPZO_PANIC;
   set_bytes(&it->key, &it->kcap, &it->kl, k, kl);
   set_bytes(&it->val, &it->vcap, &it->vl, v, vl);
+  return 0;
 }
 
-/* BlockIterator::seek_to_key (iterator.rs:91-109): lower-bound binary search. */
-static void biter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
+/* BlockIterator::seek_to_key (iterator.rs:91-109): lower-bound binary search; its key read
+ * (:95-98) panics on a BAD_KEY entry, and the final seek_to on any bad entry. */
+static int biter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
   uint32_t left = 0, right = it->blk.n;
   while (left < right) {
     uint32_t mid = (right - left) / 2 + left;
     const uint8_t *k, *v;
     uint32_t kl, vl;
-    if (!entry_at(&it->blk, mid, &k, &kl, &v, &vl)) { it->kl = it->vl = 0; return; }
+    if (entry_class(&it->blk, mid, &k, &kl, &v, &vl) == TPZO_ENTRY_BAD_KEY) {
+      it->bidx = mid;
+      it->kl = it->vl = 0;
+      return TPZO_PANIC;
+    }
     size_t m = kl < klen ? kl : klen;
     int c = memcmp(k, key, m);
     if (c == 0) c = (kl > klen) - (kl < klen);
     if (c > 0) right = mid;
     else if (c < 0) left = mid + 1;
-    else { biter_seek_to(it, mid); return; }
+    else return biter_seek_to(it, mid);
   }
-  biter_seek_to(it, left);
+  return biter_seek_to(it, left);
 }
 
 /* SsTable::read_block (table.rs:154-164) into the iterator's current block. */
@@ -373,7 +396,8 @@ static int read_block(tpzo_sst_iter* it, uint32_t i) {
     return -1;
   }
   block_decode(b, len, &it->blk);
-  return it->blk.status == TPZO_OK ? 0 : -1;
+  if (it->blk.status == TPZO_MALFORMED) return TPZO_PANIC;       /* block.rs:49-59 panics */
+  return it->blk.status == TPZO_OK ? 0 : TPZO_ERR;
 }
 
 tpzo_sst_iter* tpzo_sst_iter_create(const uint8_t* file, size_t len) {
@@ -409,9 +433,9 @@ void tpzo_sst_iter_destroy(tpzo_sst_iter* it) {
 
 /* seek_to_first_inner (table/iterator.rs:39-42) */
 static int seek_first_inner(tpzo_sst_iter* it, uint32_t idx) {
-  if (read_block(it, idx) != 0) return -1;
-  biter_seek_to(it, 0);
-  return 0;
+  const int r = read_block(it, idx);
+  if (r != 0) return r;
+  return biter_seek_to(it, 0);
 }
 
 int tpzo_sst_iter_seek_to_first(tpzo_sst_iter* it) { /* table/iterator.rs:28-37 */
@@ -435,22 +459,44 @@ static uint32_t find_block_idx(const tpzo_sst_iter* it, const uint8_t* key, size
 
 int tpzo_sst_iter_seek_to_key(tpzo_sst_iter* it, const uint8_t* key, size_t klen) {
   uint32_t idx = find_block_idx(it, key, klen);                   /* :55 */
-  if (read_block(it, idx) != 0) return -1;                        /* :56 */
-  biter_seek_to_key(it, key, klen);                               /* :57 */
+  it->idx = idx;
+  int r = read_block(it, idx);                                    /* :56 */
+  if (r != 0) return r;
+  r = biter_seek_to_key(it, key, klen);                           /* :57 */
+  if (r != 0) return r;
   if (it->kl == 0 && idx + 1 < it->nb) {                          /* :58-61 */
     idx += 1;
-    if (seek_first_inner(it, idx) != 0) return -1;
+    it->idx = idx;
+    r = seek_first_inner(it, idx);
+    if (r != 0) return r;
   }
-  it->idx = idx;
   return 0;
 }
 
 int tpzo_sst_iter_next(tpzo_sst_iter* it) { /* table/iterator.rs:88-95 */
-  biter_seek_to(it, it->bidx + 1);
+  const int r = biter_seek_to(it, it->bidx + 1);
+  if (r != 0) return r;
   if (it->kl == 0 && it->idx < it->nb - 1) {
     it->idx += 1;
     return seek_first_inner(it, it->idx);
   }
+  return 0;
+}
+
+/* SsTable::init_samllest_biggest_key (src/table.rs:143-151). */
+int tpzo_sst_biggest_key(tpzo_sst_iter* it, const uint8_t** key, size_t* len) {
+  *key = NULL;
+  *len = 0;
+  int r = read_block(it, it->nb - 1);                             /* :145 */
+  if (r != 0) return r;
+  r = biter_seek_to(it, 0);                                       /* :146 */
+  if (r != 0) return r;
+  if (it->blk.n == 0) return TPZO_PANIC;                          /* :147, iterator.rs:60 */
+  r = biter_seek_to(it, it->blk.n - 1);
+  if (r != 0) return r;
+  if (it->kl == 0) return TPZO_PANIC;                             /* :148 assert!(is_valid) */
+  *key = it->key;
+  *len = it->kl;
   return 0;
 }
 

@@ -29,12 +29,25 @@ enum {
   TPZO_BAD_TAG = 2,     /* Err("invaild data")       src/block/compress.rs:102   */
   TPZO_UNSUPPORTED = 3, /* no longer produced: lz4 (tag 3) is decoded (tpz_lz4.c) */
   TPZO_CHECKSUM = 4,    /* Err("checksum: ...")      src/checksum.rs:12-21       */
-  TPZO_MALFORMED = 5,   /* the reference panics      src/block.rs:49-59, iterator.rs:74-82 */
+  TPZO_MALFORMED = 5,   /* Block::decode itself panics   src/block.rs:49-59             */
   /* 6 (OK_SPILLED) and 7 (SPILL_FULL) are device-side placements of an Ok block (the spill
    * arena of include/tpz_gpu.h); the reference, and so this oracle, reports them TPZO_OK. */
-  TPZO_CODEC = 8        /* the codec returns Err: snap's decompress_vec (compress.rs:104-107),
+  TPZO_CODEC = 8,       /* the codec returns Err: snap's decompress_vec (compress.rs:104-107),
                            lz4::block::decompress (compress.rs:108-111)                     */
+  TPZO_BAD_ENTRY = 9    /* Block::decode is Ok (block.rs:46-65 checks no entry), but some entry
+                           is out of range: BlockIterator panics when it reaches it
+                           (iterator.rs:74-82); per-entry classes below                     */
 };
+
+/* Entry classes (tpz_entry_class of include/tpz_gpu.h): entry i at o = offsets[i], L = data.len():
+ *   0 OK         reads whole                                     iterator.rs:74-82
+ *   1 BAD_VALUE  o + 2 + klen <= L, but the value part panics    :80-82
+ *   2 BAD_KEY    o + 2 > L or o + 2 + klen > L                    :74-78 (and :95-98) */
+enum { TPZO_ENTRY_OK = 0, TPZO_ENTRY_BAD_VALUE = 1, TPZO_ENTRY_BAD_KEY = 2 };
+
+/* Iterator return codes: 0, TPZO_ERR (read_block_cached returned Err), TPZO_PANIC (the
+ * reference panics: an out-of-range entry read, or an assert). */
+enum { TPZO_ERR = -1, TPZO_PANIC = -2 };
 
 /* CRC-32/ISO-HDLC bit by bit (crc32fast's function): src/checksum.rs:6-10. */
 uint32_t tpzo_crc32(const uint8_t* p, size_t n);
@@ -49,12 +62,13 @@ void tpzo_batch_sizes(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks
 /* Block::decode (src/block.rs:46-65, snappy blocks decompressed first as compress.rs:104-107)
  * + BlockIterator::seek_to for every index (src/block/iterator.rs:63-83) over blocks
  * [ext[i], ext[i+1]). Dense outputs in block order:
- * entries are emitted for TPZO_OK blocks. crc_actual is the CRC the reference
- * computes over the payload (0 when it never gets that far). Returns 0. */
+ * entries are emitted for TPZO_OK and TPZO_BAD_ENTRY blocks (count = n); an entry's unreadable
+ * key or value is empty and cls[e] (may be NULL) holds its class. crc_actual is the CRC the
+ * reference computes over the payload (0 when it never gets that far). Returns 0. */
 int tpzo_decode_batch(const uint8_t* src, const uint64_t* ext, uint32_t n_blocks,
                       uint8_t* status, uint32_t* crc_actual, uint32_t* crc_expected,
                       uint32_t* count, uint32_t* klen, uint32_t* vlen,
-                      uint8_t* keys, uint8_t* vals);
+                      uint8_t* keys, uint8_t* vals, uint8_t* cls);
 
 /* FileObject::open (src/table/file_object.rs:57-78) + SsTable::open (src/table.rs:75-112).
  * Verifies the whole-file CRC, walks the trailer chain and returns the data-block extents
@@ -69,6 +83,7 @@ typedef struct tpzo_sst_iter tpzo_sst_iter;
 /* SsTableIterator over an in-memory SST file image (the caller keeps `file` alive). */
 tpzo_sst_iter* tpzo_sst_iter_create(const uint8_t* file, size_t len);
 void tpzo_sst_iter_destroy(tpzo_sst_iter* it);
+/* These return 0, TPZO_ERR or TPZO_PANIC. */
 int tpzo_sst_iter_seek_to_first(tpzo_sst_iter* it);                      /* :18-42 */
 int tpzo_sst_iter_seek_to_key(tpzo_sst_iter* it, const uint8_t* k, size_t kl); /* :44-72 */
 int tpzo_sst_iter_next(tpzo_sst_iter* it);                               /* :88-95 */
@@ -76,6 +91,10 @@ int tpzo_sst_iter_is_valid(const tpzo_sst_iter* it);                     /* :84-
 const uint8_t* tpzo_sst_iter_key(const tpzo_sst_iter* it, size_t* len);
 const uint8_t* tpzo_sst_iter_value(const tpzo_sst_iter* it, size_t* len);
 uint32_t tpzo_sst_iter_block_idx(const tpzo_sst_iter* it);
+/* SsTable::init_samllest_biggest_key (src/table.rs:143-151) over the iterator's table: read the
+ * last block, seek_to_first, seek_to_last, assert is_valid. 0 (key and len = biggest_key),
+ * TPZO_ERR or TPZO_PANIC. */
+int tpzo_sst_biggest_key(tpzo_sst_iter* it, const uint8_t** key, size_t* len);
 
 /* ---- snappy raw format (tpz_snappy.c; codec 2, src/block/compress.rs:66-71, 104-107) ------
  * decompress: 0 and *out_len on success, -1 where snap's decoder returns Err.

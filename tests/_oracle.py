@@ -16,6 +16,24 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 
 OK, EMPTY, BAD_TAG, UNSUPPORTED, CHECKSUM, MALFORMED = range(6)
 CODEC = 8   # 6 and 7 are device-side placements of Ok blocks (tpz_gpu.h); the oracle says OK
+BAD_ENTRY = 9   # Ok(Block) whose out-of-range entries panic when an iterator reaches them
+ENTRY_OK, ENTRY_BAD_VALUE, ENTRY_BAD_KEY = 0, 1, 2
+ERR, PANIC = -1, -2   # iterator return codes (oracle/tpz_oracle.h)
+
+
+class OracleErr(RuntimeError):
+    """read_block_cached returned Err in the reference."""
+
+
+class OraclePanic(RuntimeError):
+    """The reference panics here."""
+
+
+def _iter_rc(rc: int) -> None:
+    if rc == PANIC:
+        raise OraclePanic("the reference panics")
+    if rc != 0:
+        raise OracleErr("read_block returned Err")
 
 _lib = None
 
@@ -34,7 +52,8 @@ def lib() -> C.CDLL:
         L.tpzo_crc32.argtypes = [C.c_void_p, C.c_size_t]
         L.tpzo_crc32.restype = C.c_uint32
         L.tpzo_batch_sizes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, u64p, u64p, u64p]
-        L.tpzo_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 8
+        L.tpzo_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 9
+        L.tpzo_sst_biggest_key.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
         L.tpzo_sst_parse.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32,
                                      u32p, u64p, u64p]
         L.tpzo_sst_iter_create.argtypes = [C.c_void_p, C.c_size_t]
@@ -100,9 +119,10 @@ def crc32(b: bytes) -> int:
 class Decoded:
     """Dense decode of a batch: per-block status/crc/count, per-entry lengths and bytes."""
 
-    def __init__(self, status, crc_actual, crc_expected, count, klen, vlen, keys, vals):
+    def __init__(self, status, crc_actual, crc_expected, count, klen, vlen, keys, vals, cls=None):
         self.status, self.crc_actual, self.crc_expected = status, crc_actual, crc_expected
         self.count, self.klen, self.vlen, self.keys, self.vals = count, klen, vlen, keys, vals
+        self.cls = cls if cls is not None else np.zeros(len(klen), np.uint8)
         self.entry_base = np.zeros(len(count) + 1, np.int64)
         np.cumsum(count, out=self.entry_base[1:])
         self.kpos = np.zeros(len(klen) + 1, np.int64)
@@ -135,10 +155,11 @@ def decode_batch(src: np.ndarray, ext: np.ndarray) -> Decoded:
     vl = np.zeros(max(ne.value, 1), np.uint32)
     keys = np.zeros(max(kb.value, 1), np.uint8)
     vals = np.zeros(max(vb.value, 1), np.uint8)
+    cls = np.zeros(max(ne.value, 1), np.uint8)
     L.tpzo_decode_batch(_ptr(src), _ptr(ext), nb, _ptr(st), _ptr(ca), _ptr(ce), _ptr(cnt),
-                        _ptr(kl), _ptr(vl), _ptr(keys), _ptr(vals))
+                        _ptr(kl), _ptr(vl), _ptr(keys), _ptr(vals), _ptr(cls))
     return Decoded(st[:nb], ca[:nb], ce[:nb], cnt[:nb], kl[:ne.value], vl[:ne.value],
-                   keys[:kb.value], vals[:vb.value])
+                   keys[:kb.value], vals[:vb.value], cls[:ne.value])
 
 
 def sst_parse(f: bytes):
@@ -167,14 +188,20 @@ class SstIter:
             self._it = None
 
     def seek_to_first(self):
-        assert lib().tpzo_sst_iter_seek_to_first(self._it) == 0
+        _iter_rc(lib().tpzo_sst_iter_seek_to_first(self._it))
 
     def seek_to_key(self, k: bytes):
         kb = np.frombuffer(k, np.uint8) if k else np.zeros(1, np.uint8)
-        assert lib().tpzo_sst_iter_seek_to_key(self._it, _ptr(kb), len(k)) == 0
+        _iter_rc(lib().tpzo_sst_iter_seek_to_key(self._it, _ptr(kb), len(k)))
 
     def next(self):
-        assert lib().tpzo_sst_iter_next(self._it) == 0
+        _iter_rc(lib().tpzo_sst_iter_next(self._it))
+
+    def biggest_key(self) -> bytes:
+        """SsTable::init_samllest_biggest_key (src/table.rs:143-151); raises where it fails."""
+        p, n = C.c_void_p(), C.c_size_t()
+        _iter_rc(lib().tpzo_sst_biggest_key(self._it, C.byref(p), C.byref(n)))
+        return C.string_at(p.value, n.value)
 
     def is_valid(self) -> bool:
         return bool(lib().tpzo_sst_iter_is_valid(self._it))

@@ -459,13 +459,18 @@ class SsTableBuilder:
 # --------------------------------------------------------------------------- read side
 ST_OK, ST_EMPTY, ST_BAD_TAG, ST_UNSUPPORTED, ST_CHECKSUM, ST_MALFORMED = range(6)
 ST_CODEC = 8
+ST_BAD_ENTRY = 9     # Ok(Block) whose out-of-range entries panic when an iterator reaches them
+E_OK, E_BAD_VALUE, E_BAD_KEY = 0, 1, 2
 
 
 def decode_block(blk: bytes) -> dict:
     """Block::decode (src/block.rs:46-65) + BlockIterator::seek_to for every idx
     (src/block/iterator.rs:63-83). `status` names the reference's outcome:
-    Err("data is empty") / Err("invaild data") / snappy-lz4 / Err(checksum) / panic."""
-    r = {"status": ST_OK, "crc_expected": 0, "crc_actual": 0, "entries": []}
+    Err("data is empty") / Err("invaild data") / snappy-lz4 / Err(checksum) / a panic inside
+    Block::decode (ST_MALFORMED) / Ok with out-of-range entries (ST_BAD_ENTRY: Block::decode
+    checks no entry; `classes` says how reading each entry fails, its readable key or value is
+    in `entries`, the rest empty)."""
+    r = {"status": ST_OK, "crc_expected": 0, "crc_actual": 0, "entries": [], "classes": []}
     if len(blk) == 0:
         r["status"] = ST_EMPTY                             # compress.rs:96-98
         return r
@@ -502,25 +507,35 @@ def decode_block(blk: bytes) -> dict:
         return r
     offs = [struct.unpack(">H", payload[2 + 2 * i:4 + 2 * i])[0] for i in range(n)]
     body = payload[2 + 2 * n:]
-    ents = []
+    ents, classes = [], []
     for o in offs:                                         # iterator.rs:74-82
-        if o + 2 > len(body):
-            r["status"] = ST_MALFORMED
-            break
+        if o + 2 > len(body):                              # data[offset..], get_u16
+            ents.append((b"", b""))
+            classes.append(E_BAD_KEY)
+            continue
         kl = struct.unpack(">H", body[o:o + 2])[0]
-        if o + 2 + kl + 2 > len(body):
-            r["status"] = ST_MALFORMED
-            break
+        if o + 2 + kl > len(body):                         # buf[..klen]
+            ents.append((b"", b""))
+            classes.append(E_BAD_KEY)
+            continue
         key = body[o + 2:o + 2 + kl]
+        if o + 2 + kl + 2 > len(body):                     # get_u16 (vlen)
+            ents.append((key, b""))
+            classes.append(E_BAD_VALUE)
+            continue
         vl = struct.unpack(">H", body[o + 2 + kl:o + 4 + kl])[0]
-        if o + 4 + kl + vl > len(body):
-            r["status"] = ST_MALFORMED
-            break
+        if o + 4 + kl + vl > len(body):                    # buf[..vlen]
+            ents.append((key, b""))
+            classes.append(E_BAD_VALUE)
+            continue
         ents.append((key, body[o + 4 + kl:o + 4 + kl + vl]))
-    if r["status"] == ST_OK:
-        # entries may overlap or repeat (the iterator has no ordering or disjointness check);
-        # the device decodes such blocks through its spill path, with the same answer
-        r["entries"] = ents
+        classes.append(E_OK)
+    # entries may overlap or repeat (the iterator has no ordering or disjointness check); the
+    # device decodes such blocks through its spill path, with the same answer
+    r["entries"] = ents
+    if any(classes):
+        r["status"] = ST_BAD_ENTRY
+        r["classes"] = classes
     return r
 
 
@@ -728,6 +743,23 @@ def main() -> None:
     cases.append(("dup_offsets", raw(struct.pack(">H", 6) + struct.pack(">H", 0) * 6
                                      + struct.pack(">H", 20) + b"K" * 20 + struct.pack(">H", 0))))
     cases.append(("unsorted_offsets", raw(struct.pack(">HHH", 2, 9, 0) + e + e)))
+    # CRC-valid blocks with one out-of-range entry among good ones (Ok(Block) in the reference;
+    # the iterator panics only on reaching it): a bad key in the middle, a bad value at the end,
+    # an empty key before a bad entry (a scan stops there first)
+    ents3 = [(b"a1", b"x"), (b"a2", b"yy"), (b"a3", b"zzz"), (b"a4", b"w")]
+    d3, o3 = bytearray(), []
+    for k, v in ents3:
+        o3.append(len(d3))
+        d3 += struct.pack(">H", len(k)) + k + struct.pack(">H", len(v)) + v
+    mid = list(o3)
+    mid[1] = len(d3) - 1                                   # key length read past the data
+    cases.append(("bad_key_middle", raw(struct.pack(">H", 4) + b"".join(struct.pack(">H", x) for x in mid) + bytes(d3))))
+    tail = bytes(d3) + struct.pack(">H", 2) + b"a5" + struct.pack(">H", 40) + b"short"
+    cases.append(("bad_value_last", raw(struct.pack(">H", 5) + b"".join(struct.pack(">H", x) for x in o3 + [len(d3)]) + tail)))
+    ek = bytearray(d3)
+    o4 = o3 + [len(ek)]
+    ek += struct.pack(">H", 0) + struct.pack(">H", 1) + b"e"
+    cases.append(("empty_key_then_bad", raw(struct.pack(">H", 6) + b"".join(struct.pack(">H", x) for x in o4 + [60000]) + bytes(ek))))
     # tiny segments (1-byte keys, empty values) stress segment crossing in 16 B output chunks
     bb3 = BlockBuilder(4096)
     for i in range(300):
@@ -745,7 +777,8 @@ def main() -> None:
         d = decode_block(b)
         out.append({"name": name, "status": d["status"], "crc_expected": d["crc_expected"],
                     "crc_actual": d["crc_actual"],
-                    "entries": hexents(d["entries"]) if d["status"] == ST_OK else []})
+                    "entries": hexents(d["entries"]) if d["status"] in (ST_OK, ST_BAD_ENTRY) else [],
+                    "classes": d["classes"]})
     write("blocks_edge.bin", bytes(src))
     with open(os.path.join(HERE, "blocks_edge.json"), "w") as fj:
         json.dump({"ext": ext, "blocks": out}, fj, indent=0)

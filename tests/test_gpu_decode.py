@@ -63,7 +63,7 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
     np.testing.assert_array_equal(g.status, o.status)
     if expect_all_ok:
         assert (o.status == O.OK).all()
-    has_crc = np.isin(o.status, [O.OK, O.CHECKSUM, O.MALFORMED])
+    has_crc = np.isin(o.status, [O.OK, O.CHECKSUM, O.MALFORMED, O.BAD_ENTRY])
     # MALFORMED before the CRC stage (tiny blocks) carries no CRC in either
     has_crc &= ~((o.status == O.MALFORMED) & (o.crc_actual == 0) & (o.crc_expected == 0))
     np.testing.assert_array_equal(g.crc_actual[has_crc], o.crc_actual[has_crc])
@@ -73,6 +73,7 @@ def assert_parity(ctx, src, ext, expect_all_ok=False):
     np.testing.assert_array_equal(g.vlen, o.vlen)
     assert g.keys.tobytes() == o.keys.tobytes()
     assert g.vals.tobytes() == o.vals.tobytes()
+    np.testing.assert_array_equal(g.cls, o.cls)      # entry classes of BAD_ENTRY blocks
     return g, o
 
 
@@ -180,7 +181,8 @@ def test_blocks_past_the_lds_window(ctx):
     through the bigwave kernel (n < 64) or the spill path, straight from HBM, with the
     reference's answer: well-formed long
     blocks, corrupted ones (CHECKSUM_MISMATCH) and random block_size <= 200000 builder output
-    (mostly MALFORMED: the builder's u16 offsets wrap past 64 KiB)."""
+    (mostly BAD_ENTRY: the builder's u16 offsets wrap past 64 KiB, so entries fall out of range
+    while the block itself decodes)."""
     rng = np.random.default_rng(12)
     src, ext = _random_blocks(rng, 40, max_target=200000, corrupt_every=7)
     blocks = [src[int(ext[i]):int(ext[i + 1])].tobytes() for i in range(len(ext) - 1)]
@@ -204,7 +206,7 @@ def test_blocks_past_the_lds_window(ctx):
     assert (g.raw_status[ok_big & (n_ent >= 64)] == _lib.BLOCK_OK_SPILLED).all()
     assert (g.raw_status[ok_big & (n_ent < 64)] == _lib.BLOCK_OK).all()
     assert (big & (o.status == O.OK)).sum() >= 8 and (big & (o.status == O.CHECKSUM)).any()
-    assert (big & (o.status == O.MALFORMED)).any()
+    assert (big & (o.status == O.BAD_ENTRY)).any()
 
 
 def test_tiny_entries_many_per_block(ctx):
@@ -224,7 +226,8 @@ def test_big_path_entry_groups(ctx):
     """Big-path blocks (one 16-wave workgroup each) with 300..11000 entries: the entry table in
     LDS (2n + 1 <= 1152) and in global scratch, 1..170 64-entry groups spread over the waves
     (the cross-wave prefix of the group sums), and malformed offsets in early and late groups
-    of otherwise valid blocks (valid CRC: the status must be MALFORMED)."""
+    of otherwise valid blocks (valid CRC: Ok(Block) whose bad entries panic on access, status
+    BAD_ENTRY, every readable entry decoded)."""
     src = bytearray()
     ext = [0]
     ns = []
@@ -248,7 +251,7 @@ def test_big_path_entry_groups(ctx):
     assert max(ns) > 64 * 16 and min(ns) > 256 and any(2 * n + 1 <= 1152 for n in ns)
     g, o = assert_parity(ctx, np.frombuffer(bytes(src), np.uint8), ext)
     assert (o.status[0::3] == O.OK).all()
-    assert (o.status[1::3] == O.MALFORMED).all() and (o.status[2::3] == O.MALFORMED).all()
+    assert (o.status[1::3] == O.BAD_ENTRY).all() and (o.status[2::3] == O.BAD_ENTRY).all()
 
 
 def test_batch_not_starting_at_zero(ctx):

@@ -91,7 +91,7 @@ def test_repeated_and_overlapping_offsets(ctx):
 
 def fuzz_blocks(rng, n_blocks):
     """BlockBuilder blocks whose offsets are redrawn: random picks (with repeats) of the valid
-    entry offsets, random lengths, sometimes an arbitrary offset (usually MALFORMED), sometimes a
+    entry offsets, random lengths, sometimes an arbitrary offset (usually BAD_ENTRY), sometimes a
     corrupted byte (CHECKSUM_MISMATCH)."""
     out = []
     for t in range(n_blocks):
@@ -125,7 +125,7 @@ def test_fuzzed_offsets(ctx, seed):
     ok = o.status == O.OK
     assert (ok & (g.raw_status == _lib.BLOCK_OK_SPILLED)).sum() >= 10
     assert (ok & (g.raw_status == _lib.BLOCK_OK)).sum() >= 10
-    assert (o.status == O.MALFORMED).any() and (o.status == O.CHECKSUM).any()
+    assert (o.status == O.BAD_ENTRY).any() and (o.status == O.CHECKSUM).any()
 
 
 def test_spill_full_then_retry(ctx):

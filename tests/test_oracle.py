@@ -183,11 +183,16 @@ def test_edge_blocks():
     d = O.decode_batch(src, np.array(exp["ext"], np.uint64))
     for b, eb in enumerate(exp["blocks"]):
         assert d.status[b] == eb["status"], eb["name"]
-        if eb["status"] in (O.CHECKSUM, O.OK):
+        if eb["status"] in (O.CHECKSUM, O.OK, O.BAD_ENTRY):
             assert d.crc_actual[b] == eb["crc_actual"], eb["name"]
             assert d.crc_expected[b] == eb["crc_expected"], eb["name"]
-        if eb["status"] == O.OK:
+        if eb["status"] in (O.OK, O.BAD_ENTRY):
             check_ents(eb["entries"], d.entries(b))
+            cls = list(d.cls[d.entry_base[b]:d.entry_base[b + 1]])
+            assert cls == (eb["classes"] or [0] * len(eb["entries"])), eb["name"]
+    names = {eb["name"]: eb["status"] for eb in exp["blocks"]}
+    assert names["bad_key_middle"] == names["bad_value_last"] == O.BAD_ENTRY
+    assert names["n_too_big"] == names["payload1"] == O.MALFORMED
 
 
 def test_python_and_c_restatements_agree_on_random_blocks():

@@ -19,8 +19,12 @@ HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
- BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR) = range(9)
-LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks take the spill path
+ BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR, BLOCK_BAD_ENTRY) = range(10)
+# tpz_entry_class (BAD_ENTRY blocks)
+ENTRY_OK, ENTRY_BAD_VALUE, ENTRY_BAD_KEY = 0, 1, 2
+ABI_VERSION = 3           # TPZ_ABI_VERSION this binding was written against
+LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks with 64+ entries take the spill path
+BIGWAVE_BLOCK_BYTES = 0x40000000   # TPZ_BIGWAVE_BLOCK_BYTES
 
 
 class TpzError(RuntimeError):
@@ -136,6 +140,12 @@ def lib() -> C.CDLL:
         L.tpz_host_xxh3_64.restype = C.c_uint64
         L.tpz_layout_spill_stream.argtypes = [C.c_uint64]
         L.tpz_layout_spill_stream.restype = C.c_uint64
+        L.tpz_layout_spill_classes.argtypes = [C.c_uint64] * 3
+        L.tpz_layout_spill_classes.restype = C.c_uint64
+        L.tpz_abi_version.restype = C.c_int
+        if L.tpz_abi_version() != ABI_VERSION:
+            raise TpzError(f"{LIB_PATH}: ABI version {L.tpz_abi_version()}, this binding "
+                           f"needs {ABI_VERSION}: rebuild (make -C topazdb_amd/csrc)")
         for f in ("slot_base", "entry_base", "data_capacity", "entry_capacity"):
             fn = getattr(L, "tpz_layout_" + f)
             fn.argtypes = [C.c_uint64, C.c_uint64]
@@ -175,9 +185,15 @@ def spill_stream(n):
     return (8 * n + 127) & ~127
 
 
+def spill_classes(n, k, v):
+    """tpz_spill_classes: a BAD_ENTRY record's class bytes follow its ends and stream."""
+    return spill_stream(n) + ((value_start(k) + v + 127) & ~127)
+
+
 def block_decoded(status) -> bool:
-    """Ok(Block) in the reference: TPZ_BLOCK_OK, or OK_SPILLED (decoded into the spill arena)."""
-    return status == BLOCK_OK or status == BLOCK_OK_SPILLED
+    """Ok(Block) in the reference: TPZ_BLOCK_OK, OK_SPILLED (decoded into the spill arena) or
+    BAD_ENTRY (Ok, with entries that panic when an iterator reaches them)."""
+    return status in (BLOCK_OK, BLOCK_OK_SPILLED, BLOCK_BAD_ENTRY)
 
 
 def data_capacity(src_bytes: int, n_blocks: int) -> int:

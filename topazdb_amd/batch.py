@@ -100,13 +100,15 @@ class SlottedColumns:
 
     def dense(self, ext_host: np.ndarray) -> "DenseDecode":
         """Gather every decoded block's entries into dense arrays (block order); statuses are
-        the reference's (OK_SPILLED reads as OK; raw_status keeps the device's)."""
+        the reference's (OK_SPILLED reads as OK; raw_status keeps the device's). BAD_ENTRY
+        blocks (Ok(Block) with out-of-range entries) keep their status and contribute all n
+        entries, their unreadable keys / values empty, with the entry classes in `cls`."""
         self.complete()
         status, crc, count = self.meta_host()
         nb = self.n_blocks
         ext = np.asarray(ext_host[:nb], np.int64)
         bid = np.arange(nb, dtype=np.int64)
-        spilled = status == _lib.BLOCK_OK_SPILLED
+        spilled = (status == _lib.BLOCK_OK_SPILLED) | (status == _lib.BLOCK_BAD_ENTRY)
         okm = (status == BLOCK_OK) | spilled
         n_ok = np.where(okm, count, 0).astype(np.int64)
         ebase = np.zeros(nb + 1, np.int64)
@@ -121,7 +123,7 @@ class SlottedColumns:
         # [slotted data | spill arena]
         sb = _lib.entry_base(ext, bid)
         slot = sb[eblk] + j
-        nbad = np.zeros(total, bool)
+        cls = np.zeros(total, np.uint8)
         ke = np.zeros(total, np.int64)
         ve = np.zeros(total, np.int64)
         ks = np.zeros(total, np.int64)
@@ -137,8 +139,10 @@ class SlottedColumns:
             ks[slotm] = np.where(first, 0, kend_d[np.maximum(s_slot - 1, 0)])
             vs[slotm] = np.where(first, 0, vend_d[np.maximum(s_slot - 1, 0)])
             # the block's key bytes = kend of its last entry; its values start 16-aligned after
-            b_ok = okm & ~spilled
-            ktot = np.where(b_ok & (n_ok > 0), kend_d[sb + np.maximum(n_ok - 1, 0)].astype(np.int64), 0)
+            # (indexed for slot blocks only: a spilled block's n can point past the ends array)
+            b_ok = okm & ~spilled & (n_ok > 0)
+            ktot = np.zeros(nb, np.int64)
+            ktot[b_ok] = kend_d[(sb + n_ok - 1)[b_ok]]
             sbase = _lib.slot_base(ext, bid)
             base[slotm] = sbase[eblk[slotm]]
             vbase[slotm] = (sbase + _lib.value_start(ktot))[eblk[slotm]]
@@ -161,13 +165,17 @@ class SlottedColumns:
                 st0 = len(data) + r + _lib.spill_stream(n)
                 base[sl] = st0
                 vbase[sl] = st0 + _lib.value_start(int(kk[-1]))
+                if status[b] == _lib.BLOCK_BAD_ENTRY:
+                    c0 = r + _lib.spill_classes(n, int(kk[-1]), int(vv[-1]))
+                    cls[sl] = sp[c0:c0 + n]
         klen, vlen = ke - ks, ve - vs
         keys = _gather(buf, base + ks, klen)
         vals = _gather(buf, vbase + vs, vlen)
-        ref_status = np.where(spilled, BLOCK_OK, status).astype(np.uint8)
+        ref_status = np.where(status == _lib.BLOCK_OK_SPILLED, BLOCK_OK, status).astype(np.uint8)
         d = DenseDecode(ref_status, crc, np.where(okm, count, 0).astype(np.uint32),
                         count, klen.astype(np.uint32), vlen.astype(np.uint32), keys, vals)
         d.raw_status = status
+        d.cls = cls
         return d
 
 
@@ -187,6 +195,7 @@ class DenseDecode:
     def __init__(self, status, crc, count, raw_count, klen, vlen, keys, vals):
         self.status, self.crc_actual, self.count, self.raw_count = status, crc, count, raw_count
         self.klen, self.vlen, self.keys, self.vals = klen, vlen, keys, vals
+        self.cls = np.zeros(len(klen), np.uint8)     # tpz_entry_class per entry (BAD_ENTRY)
         self.entry_base = np.zeros(len(count) + 1, np.int64)
         np.cumsum(count, out=self.entry_base[1:])
         self.kpos = np.zeros(len(klen) + 1, np.int64)

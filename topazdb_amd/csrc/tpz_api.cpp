@@ -221,6 +221,10 @@ uint64_t tpz_layout_entry_base(uint64_t ext_i, uint64_t i) { return tpz_entry_ba
 uint64_t tpz_layout_data_capacity(uint64_t s, uint64_t n) { return tpz_data_capacity(s, n); }
 uint64_t tpz_layout_entry_capacity(uint64_t s, uint64_t n) { return tpz_entry_capacity(s, n); }
 uint64_t tpz_layout_spill_stream(uint64_t n) { return tpz_spill_stream(n); }
+uint64_t tpz_layout_spill_classes(uint64_t n, uint64_t k, uint64_t v) {
+  return tpz_spill_classes(n, k, v);
+}
+int tpz_abi_version(void) { return TPZ_ABI_VERSION; }
 
 const char* tpz_last_error(void) { return g_last_error.c_str(); }
 
@@ -634,6 +638,7 @@ int tpz_format_block_error(int status, uint32_t crc_expected, uint32_t crc_actua
     case TPZ_BLOCK_OK_SPILLED: tmp[0] = 0; break;   // Ok(Block), decoded into the spill arena
     case TPZ_BLOCK_SPILL_FULL: std::snprintf(tmp, sizeof tmp, "spill arena too small"); break;
     case TPZ_BLOCK_CODEC_ERROR: std::snprintf(tmp, sizeof tmp, "decompression failed"); break;
+    case TPZ_BLOCK_BAD_ENTRY: tmp[0] = 0; break;    // Ok(Block); its bad entries panic on access
     default: std::snprintf(tmp, sizeof tmp, "unknown status %d", status); break;
   }
   int n = (int)std::strlen(tmp);

@@ -555,11 +555,9 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
         // the {kend, vend} pairs, whole 128-byte lines (pairs past n are zero)
         uint2* ends_g = reinterpret_cast<uint2*>(p.ends) + entry_base(s, b);
         if (slots_fit && lane < ((n + 15) & ~15u)) ends_g[lane] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
-        if (bad) {
-          st = TPZ_BLOCK_MALFORMED;
-          bcnt = 0;
-        } else if (!slots_fit || (u64)vs + vtot > (u64)len + 2) {
-          // entries overlap or repeat: the spill path decodes the block (CRC included)
+        if (bad || !slots_fit || (u64)vs + vtot > (u64)len + 2) {
+          // entries out of range (TPZ_BLOCK_BAD_ENTRY), or entries that overlap or repeat: the
+          // spill path decodes the block (CRC included)
           if (lane == 0) p.spill_list[atomicAdd(p.spill_count, 1u)] = b;
           return;
         } else {

@@ -907,11 +907,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 
     const u32 vs = (kc + 15) & ~15u;
     TPZ_STAMP(S, 2);
-    if (bad) {
-      st = TPZ_BLOCK_MALFORMED;
-      cnt = 0;
-    } else if (!slots_fit || vs + vc > len + 2) {   // the slot holds len + 129 bytes
-      // entries overlap or repeat: the spill path decodes the block (CRC included)
+    if (bad || !slots_fit || vs + vc > len + 2) {   // the slot holds len + 129 bytes
+      // entries out of range (Ok(Block) with per-entry classes: TPZ_BLOCK_BAD_ENTRY), or
+      // entries that overlap or repeat: the spill path decodes the block (CRC included)
       defer_to(o.spill_list, o.spill_count, b);
       return;
     } else {
@@ -1076,7 +1074,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (!__ballot(lng)) return;
     u32 nent = 0xFFFFu;
     if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
-    const bool to_bw = lng && nent < 64 && p.out.bw_list;
+    const bool to_bw = lng && nent < 64 && p.out.bw_list && ge - gs <= TPZ_BIGWAVE_BLOCK_BYTES;
     const bool to_spill = lng && !to_bw && ge - gs > kBigMaxLen;
     if (p.out.bw_list) defer_lanes(p.out.bw_list, p.out.bw_count, to_bw, (u32)bb);
     defer_lanes(p.out.spill_list, p.out.spill_count, to_spill, (u32)bb);
@@ -1346,11 +1344,8 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     BigSums T;
     T.add(gsum, 0, G);
     const u32 vs = (T.kb + 15) & ~15u;
-    if (T.bad) {
-      st = TPZ_BLOCK_MALFORMED;
-      bcnt = 0;
-    } else if (!slots_fit || (u64)vs + T.vb > (u64)len + 2) {  // the slot holds len + 129 B
-      spill = true;   // entries overlap or repeat: the spill path decodes the block
+    if (T.bad || !slots_fit || (u64)vs + T.vb > (u64)len + 2) {  // the slot holds len + 129 B
+      spill = true;   // entries out of range, or overlapping / repeated: the spill path
     } else {
       copy = true;
       nk = T.kn + T.vn;

@@ -281,7 +281,7 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     std::memcpy(o->h_crc + S.lo, S.h_crc.p, m * 4);
     for (uint32_t j = 0; j < m; j++) {
       o->h_first[S.lo + j] = g_first + first[j];
-      if (bst[j] == TPZ_BLOCK_OK_SPILLED) o->h_spill_off[S.lo + j] = g_spill + soff[j];
+      if (tpz::block_in_spill(bst[j])) o->h_spill_off[S.lo + j] = g_spill + soff[j];
     }
     g_first += total;
     g_spill += used;

@@ -49,6 +49,17 @@ __host__ __device__ inline uint64_t spill_stream(uint64_t n) {
 __host__ __device__ inline uint64_t spill_record_bytes(uint64_t n, uint64_t k, uint64_t v) {
   return spill_stream(n) + ((value_start(k) + v + 127u) & ~(uint64_t)127u);
 }
+// A TPZ_BLOCK_BAD_ENTRY record's class bytes follow its ends and stream.
+__host__ __device__ inline uint64_t spill_classes(uint64_t n, uint64_t k, uint64_t v) {
+  return spill_record_bytes(n, k, v);
+}
+// Readers of decoded blocks: a block whose entries are in its slot or in a spill record.
+__host__ __device__ inline bool block_decoded(uint32_t st) {
+  return st == TPZ_BLOCK_OK || st == TPZ_BLOCK_OK_SPILLED || st == TPZ_BLOCK_BAD_ENTRY;
+}
+__host__ __device__ inline bool block_in_spill(uint32_t st) {
+  return st == TPZ_BLOCK_OK_SPILLED || st == TPZ_BLOCK_BAD_ENTRY;
+}
 
 struct LaunchArgs {
   const uint8_t* src;

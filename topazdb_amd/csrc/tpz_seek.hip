@@ -13,7 +13,9 @@
 // One thread per query: both are a few binary-search steps of dependent global loads (keys of a
 // few tens of bytes), latency-bound, so the launch simply puts many queries in flight. A query
 // whose block did not decode gets that block's status (the reference's read_block_cached Err, or
-// its panic for MALFORMED); OK_SPILLED blocks are read from their spill records and report OK.
+// its panic for MALFORMED); OK_SPILLED and BAD_ENTRY blocks are read from their spill records and
+// report OK, unless the seek reads an entry of a BAD_ENTRY block the reference panics on (the
+// key of a BAD_KEY entry in the bisection, or any bad entry it lands on): MALFORMED.
 
 #if defined(TPZ_BLOOM_ABL_BLOOMBYTES)   // diagnostic: the byte-load xxh3 reads
 #define TPZ_XXH3_BYTEREADS
@@ -62,18 +64,27 @@ struct SeekParams {
   uint8_t* out_valid;
 };
 
-// A decoded block's ends and stream: its slot, or its spill record (include/tpz_gpu.h).
+// A decoded block's ends and stream: its slot, or its spill record (include/tpz_gpu.h); the
+// entry classes of a BAD_ENTRY block (null otherwise: every entry reads whole).
 struct BlockView {
   const u32* ends;
   const uint8_t* stream;
+  const uint8_t* cls;
+  // seek_to(j) / the bisection's key read panic on entry j (iterator.rs:74-82, :95-98)
+  __device__ __forceinline__ bool seek_panics(u32 j) const { return cls && cls[j] != TPZ_ENTRY_OK; }
+  __device__ __forceinline__ bool key_panics(u32 j) const { return cls && cls[j] == TPZ_ENTRY_BAD_KEY; }
 };
 __device__ __forceinline__ BlockView block_view(const SeekParams& p, u32 b, u32 st) {
-  if (st == TPZ_BLOCK_OK_SPILLED) {
+  if (block_in_spill(st)) {
+    const u32 n = p.count[b];
     const uint8_t* r = p.spill + p.spill_off[b];
-    return BlockView{reinterpret_cast<const u32*>(r), r + spill_stream(p.count[b])};
+    const u32* e = reinterpret_cast<const u32*>(r);
+    const uint8_t* cls = (st == TPZ_BLOCK_BAD_ENTRY && n)
+                             ? r + spill_classes(n, e[2 * (n - 1)], e[2 * (n - 1) + 1]) : nullptr;
+    return BlockView{e, r + spill_stream(n), cls};
   }
   const u64 e0 = p.ext[b];
-  return BlockView{p.ends + 2 * entry_base(e0, b), p.data + slot_base(e0, b)};
+  return BlockView{p.ends + 2 * entry_base(e0, b), p.data + slot_base(e0, b), nullptr};
 }
 // Entry j's key: its bytes and length.
 __device__ __forceinline__ const uint8_t* entry_key(const BlockView& v, u32 j, u64& len) {
@@ -81,9 +92,7 @@ __device__ __forceinline__ const uint8_t* entry_key(const BlockView& v, u32 j, u
   len = hi - lo;
   return v.stream + lo;
 }
-__device__ __forceinline__ bool decoded(u32 st) {
-  return st == TPZ_BLOCK_OK || st == TPZ_BLOCK_OK_SPILLED;
-}
+__device__ __forceinline__ bool decoded(u32 st) { return block_decoded(st); }
 
 __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -106,7 +115,7 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
   }
   u32 b = lo ? lo - 1 : 0;
   u32 st = p.bstatus[b], pos = 0;
-  bool valid = false;
+  bool valid = false, panic = false;
   if (decoded(st)) {
     // BlockIterator::seek_to_key
     const BlockView v = block_view(p, b, st);
@@ -116,6 +125,7 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
     bool found = false;
     while (l < r) {
       const u32 mid = (r - l) / 2 + l;
+      if (v.key_panics(mid)) { pos = mid; panic = true; break; }   // iterator.rs:95-98
       u64 kl;
       const uint8_t* k = entry_key(v, mid, kl);
       const int c = key_cmp(k, kl, qk, ql);
@@ -123,24 +133,28 @@ __global__ __launch_bounds__(256) void seek_kernel(SeekParams p) {
       else if (c < 0) l = mid + 1;
       else { pos = mid; found = true; break; }
     }
-    if (!found) pos = l;
+    if (!found && !panic) pos = l;
+    if (!panic && pos < n && v.seek_panics(pos)) panic = true;      // seek_to, :74-82
     u64 kl = 0;
     if (pos < n) entry_key(v, pos, kl);
-    valid = pos < n && kl > 0;                // is_valid: the current key is non-empty
-    if (!valid && b + 1 < p.n_blocks) {       // the next block, from its first entry
+    valid = !panic && pos < n && kl > 0;      // is_valid: the current key is non-empty
+    if (!panic && !valid && b + 1 < p.n_blocks) {   // the next block, from its first entry
       b++;
       st = p.bstatus[b];
       pos = 0;
       valid = false;
       if (decoded(st) && p.count[b] > 0) {
-        entry_key(block_view(p, b, st), 0, kl);
-        valid = kl > 0;
+        const BlockView w = block_view(p, b, st);
+        panic = w.seek_panics(0);
+        entry_key(w, 0, kl);
+        valid = !panic && kl > 0;
       }
     }
   }
   p.out_block[i] = b;
   p.out_entry[i] = pos;
-  p.out_status[i] = decoded(st) ? (uint8_t)TPZ_BLOCK_OK : (uint8_t)st;
+  p.out_status[i] = panic ? (uint8_t)TPZ_BLOCK_MALFORMED
+                          : decoded(st) ? (uint8_t)TPZ_BLOCK_OK : (uint8_t)st;
   p.out_valid[i] = decoded(st) && valid;
 }
 
@@ -483,8 +497,8 @@ __global__ __launch_bounds__(256) void pack_ends_kernel(PackLaunch a, uint2* den
   for (u32 b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < a.n_blocks; b += nw) {
     const u64 f = a.first[b], c = a.first[b + 1] - f;
     const u32 st = a.status[b];
-    const bool ok = st == TPZ_BLOCK_OK || st == TPZ_BLOCK_OK_SPILLED;
-    const uint2* src = st == TPZ_BLOCK_OK_SPILLED
+    const bool ok = block_decoded(st);
+    const uint2* src = block_in_spill(st)
                            ? reinterpret_cast<const uint2*>(a.spill + a.spill_off[b])
                            : reinterpret_cast<const uint2*>(a.ends) + entry_base(a.ext[b], b);
     for (u64 j = lane; j < c; j += 64) dense[f + j] = ok ? src[j] : make_uint2(0, 0);
@@ -500,7 +514,7 @@ __global__ __launch_bounds__(1024) void count_prefix_kernel(const u32* count, co
   const u32 lo = min(n, t * per), hi = min(n, lo + per);
   u64 s = 0;
   for (u32 i = lo; i < hi; i++)
-    s += (status[i] == TPZ_BLOCK_OK || status[i] == TPZ_BLOCK_OK_SPILLED) ? count[i] : 0u;
+    s += block_decoded(status[i]) ? count[i] : 0u;
   part[t] = s;
   __syncthreads();
   for (u32 o = 1; o < 1024; o <<= 1) {          // Hillis-Steele inclusive scan of the parts
@@ -512,7 +526,7 @@ __global__ __launch_bounds__(1024) void count_prefix_kernel(const u32* count, co
   u64 run = t ? part[t - 1] : 0;
   for (u32 i = lo; i < hi; i++) {
     first[i] = run;
-    run += (status[i] == TPZ_BLOCK_OK || status[i] == TPZ_BLOCK_OK_SPILLED) ? count[i] : 0u;
+    run += block_decoded(status[i]) ? count[i] : 0u;
   }
   if (t == 1023) first[n] = part[1023];
 }

@@ -6,8 +6,13 @@
 //   * blocks whose entries overlap or repeat: BlockIterator::seek_to (src/block/iterator.rs:
 //     63-83) reads entry i at offsets[i] with no ordering or disjointness check, so n entries may
 //     materialise far more bytes than the block holds;
-//   * blocks longer than TPZ_LDS_BLOCK_BYTES (Block::decode, src/block.rs:46-65, has no length
-//     limit; a block_size > 64 KiB builder, or a hand-made block, produces them).
+//   * blocks longer than the LDS paths take (Block::decode, src/block.rs:46-65, has no length
+//     limit; a block_size > 64 KiB builder, or a hand-made block, produces them);
+//   * blocks with entries out of range: Block::decode checks no entry, so the reference returns
+//     Ok(Block) and panics only when an iterator reaches such an entry (iterator.rs:74-82). These
+//     are decoded with a class byte per entry (TPZ_BLOCK_BAD_ENTRY, include/tpz_gpu.h): every
+//     readable key and value is materialised, and a reader fails exactly where the reference
+//     does.
 // Those paths append such blocks to the stream's spill worklist; this kernel decodes them into
 // the caller's spill arena (include/tpz_gpu.h: TPZ_BLOCK_OK_SPILLED), straight from HBM:
 //   1. compress::decode tag dispatch (src/block/compress.rs:95-113) and the CRC split
@@ -17,7 +22,7 @@
 //      (GF(2) multiplies, square-and-multiply over x^(8*2^j)), and the workgroup XORs them;
 //      the init value enters as shift_P(0xFFFFFFFF);
 //   3. n and the offsets (src/block.rs:54-59), every entry's bounds checks
-//      (src/block/iterator.rs:74-82) and the key/value totals;
+//      (src/block/iterator.rs:74-82) and class, and the key/value totals;
 //   4. the record is reserved in the arena with one 64-bit atomic add; the entry ends are
 //      written by a workgroup scan and each entry's key and value bytes are copied by one wave.
 // One 1024-thread workgroup per block, persistent over the worklist. Spills are rare (no block a
@@ -140,26 +145,30 @@ __device__ __forceinline__ u32 wg_scan(u32 x, u64* red, u32& total) {
   return x + before;
 }
 
-// Entry i's key and value (iterator.rs:74-82): lengths, offset; ok = false where it panics.
+// Entry i's key and value (iterator.rs:74-82): offset, the readable lengths (an unreadable key
+// or value counts 0 bytes) and the entry's class (tpz_entry_class): BAD_KEY where reading the
+// key panics (`data[offset..]`, get_u16, `buf[..klen]`, :74-78; seek_to_key reads no more,
+// :95-98), BAD_VALUE where only the value part panics (get_u16, `buf[..vlen]`, :80-82).
 struct Entry {
   u64 off;
   u32 kl, vl;
-  bool ok;
+  u32 cls;
 };
 __device__ __forceinline__ Entry parse(const uint8_t* blk, u64 db, u64 dl, u32 i) {
   Entry e;
   e.off = be16(blk + 2 + 2 * (u64)i);                                            // :74
   e.kl = e.vl = 0;
-  e.ok = e.off + 2 <= dl;                                                        // :75-77
-  if (e.ok) {
-    e.kl = be16(blk + db + e.off);
-    e.ok = e.off + 4 + e.kl <= dl;                                               // :78-81
-  }
-  if (e.ok) {
-    e.vl = be16(blk + db + e.off + 2 + e.kl);
-    e.ok = e.off + 4 + e.kl + e.vl <= dl;                                        // :82
-  }
-  if (!e.ok) e.kl = e.vl = 0;
+  e.cls = TPZ_ENTRY_BAD_KEY;
+  if (e.off + 2 > dl) return e;                                                  // :75-77
+  const u32 kl = be16(blk + db + e.off);
+  if (e.off + 2 + kl > dl) return e;                                             // :78
+  e.kl = kl;
+  e.cls = TPZ_ENTRY_BAD_VALUE;
+  if (e.off + 4 + kl > dl) return e;                                             // :80
+  const u32 vl = be16(blk + db + e.off + 2 + kl);
+  if (e.off + 4 + kl + vl > dl) return e;                                        // :81-82
+  e.vl = vl;
+  e.cls = TPZ_ENTRY_OK;
   return e;
 }
 
@@ -215,14 +224,17 @@ __global__ __launch_bounds__(kThreads, 1) void decode_spill_kernel(SpillParams p
     const u64 npc = (Aend - A0 + 15) >> 4;             // 16-byte pieces from A0
     const u64 pp = (npc + kThreads - 1) / kThreads;
     const u64 k0 = (u64)tid * pp, k1 = k0 + pp < npc ? k0 + pp : npc;
-    u64 rem = p.src_bytes - A0;
+    // the thread's own descriptor starts at its first piece, so a block of any length is read
+    // whole (a thread's run is npc / 1024 pieces: under 2 GiB for blocks under 2 TiB)
+    const u64 T0 = A0 + 16 * k0;
+    u64 rem = p.src_bytes > T0 ? p.src_bytes - T0 : 0;
     rem = rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(p.src + A0), (short)0, (int)rem, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.src + T0), (short)0, (int)rem, 0x00020000);
     u32 c = 0;
     for (u64 k = k0; k < k1; k++) {
       const u64 a = A0 + 16 * k;
-      uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(16 * k), 0, 0));
+      uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(16 * (k - k0)), 0, 0));
       if (a < s) {                                     // bytes before the payload: zero (a raw
         const u32 z = (u32)(s - a);                    // CRC ignores leading zeros)
         u32 w[4] = {v.x, v.y, v.z, v.w};
@@ -272,15 +284,12 @@ __global__ __launch_bounds__(kThreads, 1) void decode_spill_kernel(SpillParams p
       const Entry en = parse(blk, db, dl, i);
       kt += en.kl;
       vt += en.vl;
-      bad |= en.ok ? 0u : 1u;
+      bad |= en.cls != TPZ_ENTRY_OK ? 1u : 0u;
     }
     const u64 K = wg_sum64(kt, red), V = wg_sum64(vt, red), B = wg_sum64(bad, red);
-    if (B) {
-      put_meta(p, b, TPZ_BLOCK_MALFORMED, 0, crc);
-      continue;
-    }
-    // ---- the record: ends, then the stream (keys | values from value_start(K))
-    const u64 need = spill_record_bytes(n, K, V);
+    // ---- the record: ends, then the stream (keys | values from value_start(K)), then for a
+    // block with bad entries their classes (Ok(Block) either way: block.rs:46-65)
+    const u64 need = spill_record_bytes(n, K, V) + (B ? (((u64)n + 127u) & ~127ull) : 0u);
     if (tid == 0) {
       const u64 off = atomicAdd(reinterpret_cast<unsigned long long*>(p.spill_used),
                                 (unsigned long long)need);
@@ -296,16 +305,18 @@ __global__ __launch_bounds__(kThreads, 1) void decode_spill_kernel(SpillParams p
     }
     u32* ends = reinterpret_cast<u32*>(p.spill + roff);
     uint8_t* stream = p.spill + roff + spill_stream(n);
+    uint8_t* classes = p.spill + roff + spill_record_bytes(n, K, V);
     const u64 vs = value_start(K);
     u32 kc = 0, vc = 0;
     for (u32 r0 = 0; r0 < n; r0 += kThreads) {
       const u32 i = r0 + tid;
-      const Entry en = i < n ? parse(blk, db, dl, i) : Entry{0, 0, 0, true};
+      const Entry en = i < n ? parse(blk, db, dl, i) : Entry{0, 0, 0, TPZ_ENTRY_OK};
       u32 ktot, vtot;
       const u32 ki = wg_scan(en.kl, red, ktot) + kc;
       const u32 vi = wg_scan(en.vl, red, vtot) + vc;
       if (i < n) {
         *reinterpret_cast<uint2*>(ends + 2 * (u64)i) = make_uint2(ki, vi);
+        if (B) classes[i] = (uint8_t)en.cls;
         e_kst[tid] = ki - en.kl;
         e_vst[tid] = vi - en.vl;
       }
@@ -321,7 +332,7 @@ __global__ __launch_bounds__(kThreads, 1) void decode_spill_kernel(SpillParams p
       vc += vtot;
       __syncthreads();
     }
-    put_meta(p, b, TPZ_BLOCK_OK_SPILLED, n, crc);
+    put_meta(p, b, B ? TPZ_BLOCK_BAD_ENTRY : TPZ_BLOCK_OK_SPILLED, n, crc);
     (void)lane;
   }
 }

@@ -29,8 +29,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY, BLOCK_MALFORMED,
-                   BLOCK_OK, Context)
+from ._lib import (BLOCK_BAD_ENTRY, BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY,
+                   BLOCK_MALFORMED, BLOCK_OK, ENTRY_BAD_KEY, ENTRY_OK, Context)
 from .batch import DeviceBatch, decode_batch, decompress_batch, verify_files
 
 CHECKSUM_SIZE = 4  # src/checksum.rs:4
@@ -63,15 +63,20 @@ class Block:
 
     Built from the device's decoded columns; `offsets()`/`data()` rebuild the reference's private
     fields for a block written by BlockBuilder (entries back to back, src/block/builder.rs:26-57).
+    `cls` holds the entry classes of a block with out-of-range entries (TPZ_BLOCK_BAD_ENTRY:
+    Block::decode is Ok, the iterator panics when it reaches such an entry); None when every
+    entry reads whole.
     """
 
-    __slots__ = ("keys", "kpos", "vals", "vpos", "payload_len")
+    __slots__ = ("keys", "kpos", "vals", "vpos", "payload_len", "cls")
 
-    def __init__(self, keys: bytes, kpos, vals: bytes, vpos, payload_len: int | None = None):
+    def __init__(self, keys: bytes, kpos, vals: bytes, vpos, payload_len: int | None = None,
+                 cls=None):
         self.keys, self.vals = keys, vals
         self.kpos = [int(x) for x in kpos]
         self.vpos = [int(x) for x in vpos]
         n = len(self.kpos) - 1
+        self.cls = None if cls is None or not any(cls) else [int(c) for c in cls]
         self.payload_len = payload_len if payload_len is not None else (
             SIZEOF_U16 + n * (SIZEOF_U16 * 3) + len(keys) + len(vals))
 
@@ -84,6 +89,10 @@ class Block:
 
     def value_at(self, i: int) -> bytes:
         return self.vals[self.vpos[i]:self.vpos[i + 1]]
+
+    def entry_class(self, i: int) -> int:
+        """tpz_entry_class of entry i (ENTRY_OK unless the block has out-of-range entries)."""
+        return ENTRY_OK if self.cls is None else self.cls[i]
 
     def uncompress_size(self) -> int:
         """src/block.rs:27-29: 2 + 2 * n + data.len() = the decoded payload length."""
@@ -107,7 +116,8 @@ class Block:
         k0, k1 = int(d.kpos[e0]), int(d.kpos[e1])
         v0, v1 = int(d.vpos[e0]), int(d.vpos[e1])
         return Block(d.keys[k0:k1].tobytes(), d.kpos[e0:e1 + 1] - k0,
-                     d.vals[v0:v1].tobytes(), d.vpos[e0:e1 + 1] - v0, payload_len)
+                     d.vals[v0:v1].tobytes(), d.vpos[e0:e1 + 1] - v0, payload_len,
+                     d.cls[e0:e1] if d.status[b] == BLOCK_BAD_ENTRY else None)
 
     @staticmethod
     def decode(data: bytes, ctx: Context) -> "Block":
@@ -215,7 +225,7 @@ class DeviceTable:
                 continue
             st = int(d.status[b])
             lo, hi = int(dext[b]), int(dext[b + 1])
-            if st == BLOCK_OK:
+            if st == BLOCK_OK or st == BLOCK_BAD_ENTRY:
                 out.append(Block.from_dense(d, b, hi - lo - 5))
             else:
                 expected = 0
@@ -282,6 +292,8 @@ class BlockIterator:
             self.idx = n
             return
         self.idx = idx
+        if self.block.entry_class(idx) != ENTRY_OK:   # iterator.rs:74-82: get_u16 / slice panic
+            raise ReferencePanic(f"entry {idx} of the block is out of range")
         self._key = self.block.key_at(idx)
         self._value = self.block.value_at(idx)
 
@@ -293,6 +305,8 @@ class BlockIterator:
         left, right = 0, self.block.num_entries
         while left < right:
             mid = (right - left) // 2 + left
+            if self.block.entry_class(mid) == ENTRY_BAD_KEY:   # :95-98 reads the key: panics
+                raise ReferencePanic(f"entry {mid} of the block is out of range")
             mk = self.block.key_at(mid)
             if mk > key:
                 right = mid
