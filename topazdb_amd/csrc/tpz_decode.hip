@@ -687,7 +687,6 @@ __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, cons
   const bool rw = __ballot(act && (e0 <= x0 || (cross && e1 < x0 + 16 && j + 2 < F.nk))) != 0;
   if (rw) rare |= 1u << w;
   if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
-  if (act && x0 + 16 > F.tot) acc = keep_head(acc, F.tot - x0);   // the stream's last chunk
   // an idle lane read the zeroed guard: its pad chunk stores zeros without a select
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
                                          F.out, rw ? kOob : x0, 0, 0);
@@ -726,19 +725,24 @@ __device__ __forceinline__ u32 copy_fast3(const S& src, const ColSmall& col, con
   if (rw) rare |= 1u << w;
   if (b1) acc = merge_at(acc, n1, (int)(e0 - x0));
   if (b2) acc = merge_at(acc, n2, (int)(e1 - x0));
-  if (act && x0 + 16 > F.tot) acc = keep_head(acc, F.tot - x0);   // the stream's last chunk
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
                                          F.out, rw ? kOob : x0, 0, 0);
   return carry_out;
 }
 
 // Copy of a wave-path block's stream fused with its CRC: returns R0(payload' || 0^k) as
-// wave_crc does (the caller prepared the window the same way).
-template <class S>
+// wave_crc does (the caller prepared the window the same way). SHORT (segments under 16 bytes:
+// copy_fast3) is a template argument so that each instantiation is one straight-line region:
+// a per-window branch between the two copies kept the scheduler from interleaving the copy
+// windows with the CRC steps (3 % slower on the 4k config, profiles/r3/bisect_4k.jsonl).
+// The stream's last chunk carries no bytes of other blocks or of earlier ones: every byte a
+// chunk reads past its last segment lies in the block or in the 16 zeroed bytes after the payload.
+template <bool SHORT, class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const uint8_t* win, int pb, u32 Pa, u32 kshift,
-                                              bool short_segs, Stamps& St) {
+                                              Stamps& St) {
+  constexpr bool short_segs = SHORT;
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
@@ -944,16 +948,22 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     // matches. (The window is not used after this, so nothing is restored.)
     const u32 k = ((a0 + P + 15) & ~15u) - (a0 + P);
     if (lane < 4) win[a0 + lane] ^= 0xFFu;
-    if (lane < k) win[a0 + P + lane] = 0;
+    // the k bytes to the 16-byte boundary for the CRC; 16 in all, so that the copy's last chunk,
+    // which may read up to 15 bytes past the payload, reads zeros there (deterministic output)
+    if (lane < 16) win[a0 + P + lane] = 0;
     __builtin_amdgcn_wave_barrier();
 #if defined(TPZ_ABL_NOCRC) || defined(TPZ_ABL_MEMONLY)
     crc = stored;
 #else
     u32 R;
-    if (!BIG && fuse)
-      R = copy_crc_fused(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb, P + k,
-                         kshift, f_short, S);
+    if (!BIG && fuse && f_short)
+      R = copy_crc_fused<true>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                               reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
+                               P + k, kshift, S);
+    else if (!BIG && fuse)
+      R = copy_crc_fused<false>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                                reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
+                                P + k, kshift, S);
     else
       R = wave_crc(tab, win, pb, P + k);
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
