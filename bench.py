@@ -7,7 +7,8 @@ Metric (BASELINE.json): "GiB/s device-resident SSTable block decode+checksum, 4K
 A step = one tpz_decode_blocks call over this rank's whole batch (default 2^20 blocks of the
 "4k" config: block_size 4096, 16 B keys, 100 B values, 4155 B per block; BASELINE.json
 configs[1]). With N GPUs every rank decodes its own 2^20-block shard (round-robin shards of
-one N x 2^20-block data set, no collective on the data path): weak scaling.
+one N x 2^20-block data set, no collective on the data path): weak scaling, the same bytes per
+GPU at every N.
 
 Also reported:
   roofline     algorithmic bytes per step (reads + writes) / kernel time,
@@ -17,6 +18,10 @@ Also reported:
                (oracle/liboracle.so, kind "port") over a bounded sample of 64 MiB SST files of
                the same config, on this host's cores (rank 0, N = 1 only).
   e2e          H2D + decode + D2H rate from pinned host memory (not the metric).
+  config5      BASELINE.json configs[4]: 12.5 GiB of 4 KiB blocks per GPU (100 GiB over 8), the
+               generated shard replicated on the device, timed at every N like the metric.
+  zipf, 64k    BASELINE.json configs[3] and configs[2] at their full sizes (rank 0, N = 1): the
+               same decode timing and roofline as the metric, checked against the generator.
 """
 from __future__ import annotations
 
@@ -678,6 +683,94 @@ def validate_replicas(cols: SlottedColumns, ext: np.ndarray, nb: int, full: int,
                                 cols.data[sb0 + ln - int(ends0[-1]):sb0 + ln]), f"replica {c} data"
 
 
+def time_decode(ctx, batch: DeviceBatch, cols: SlottedColumns, stream, steps: int, warmup: int,
+                dist, dev) -> tuple[float, float]:
+    """W untimed + K timed decode steps bracketed by a barrier and a device sync on both sides;
+    returns (wall seconds, HIP-event ms per step on the decode stream), max over ranks."""
+    for _ in range(warmup):
+        decode_batch(ctx, batch, cols, stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        decode_batch(ctx, batch, cols, stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t_start
+    ev_ms = ev0.elapsed_time(ev1) / steps
+    wall_max, ev_ms_max = max_over_ranks(dist, [wall, ev_ms], dev)
+    return wall_max, ev_ms_max
+
+
+def config5_rate(ctx, src, ext, n_ent, kbytes, vbytes, gen, dev, dist, world: int,
+                 gib: float, steps: int, warmup: int) -> dict:
+    """BASELINE.json configs[4] at this rank: `gib` GiB of the 4k shard per GPU (the generated
+    shard replicated on the device, byte offsets past 2^32), K timed decode steps, max over
+    ranks; metadata of every block and a 1 % sample of slots checked against copy 0, and copy 0
+    against the generator. Every rank joins (its collectives), whatever N."""
+    nb = len(ext) - 1
+    full, part = replicate_plan(int(ext[-1]), nb, int(gib * GIB))
+    batch, ext_run = replicate_on_device(src, ext, full, part, dev)
+    cols = SlottedColumns(batch.n_blocks, batch.src_bytes, dev.index)
+    stream = torch.cuda.current_stream(dev)
+    ctx.reserve(batch.n_blocks, stream.cuda_stream)
+    wall_max, ev_ms_max = time_decode(ctx, batch, cols, stream, steps, warmup, dist, dev)
+    validate(cols, ext, n_ent, gen, dev)
+    validate_replicas(cols, ext, nb, full, part, dev)
+    alg = algorithmic_bytes(ext, n_ent, kbytes, vbytes) * full
+    if part:
+        e_p = int(n_ent[:part].sum())
+        alg += algorithmic_bytes(ext[:part + 1], n_ent[:part], int(gen[1][e_p]), int(gen[3][e_p]))
+    in_bytes = float(batch.src_bytes)
+    out = {"gib_per_gpu": round(in_bytes / GIB, 3), "blocks_per_gpu": batch.n_blocks,
+           "copies": full, "partial_blocks": part, "last_extent": int(ext_run[-1]),
+           "steps": steps, "ms_per_step": round(wall_max * 1e3 / steps, 4),
+           "kernel_ms": round(ev_ms_max, 4), "n_gpus": world,
+           "value_gib_s": round(job_rate(in_bytes, world, steps, wall_max), 2),
+           "roofline_frac": round(alg / (ev_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "device_bytes_per_gpu": int(batch.src.numel() + cols.data.numel() + 4 * cols.ends.numel()),
+           "validated": "copy 0 vs the generator (every block); copies 1..: every block's "
+                        "status/count/crc, 1 % of slots"}
+    del batch, cols
+    torch.cuda.empty_cache()
+    return out
+
+
+def side_config_rate(ctx, config: str, dev, steps: int, warmup: int) -> dict:
+    """BASELINE.json configs[2] (64k) / configs[3] (zipf) at full size on one GPU: the metric's
+    decode timing and roofline over that config's generated blocks, every block checked against
+    the generator afterwards."""
+    nb = DEFAULT_BLOCKS[config]
+    t0 = time.time()
+    src, ext, gen, n_ent, kbytes, vbytes = make_shard(config, nb, 0)
+    gen_s = time.time() - t0
+    batch = DeviceBatch(src, ext, dev.index)
+    cols = SlottedColumns(batch.n_blocks, batch.src_bytes, dev.index)
+    stream = torch.cuda.current_stream(dev)
+    ctx.reserve(batch.n_blocks, stream.cuda_stream)
+    wall, ev_ms = time_decode(ctx, batch, cols, stream, steps, warmup, None, dev)
+    validate(cols, ext, n_ent, gen, dev)
+    alg = algorithmic_bytes(ext, n_ent, kbytes, vbytes)
+    out = {"blocks": nb, "input_bytes": int(batch.src_bytes),
+           "median_block_bytes": int(np.median(np.diff(ext.astype(np.int64)))),
+           "entries_per_block": round(float(n_ent.mean()), 2), "steps": steps,
+           "ms_per_step": round(wall * 1e3 / steps, 4), "kernel_ms": round(ev_ms, 4),
+           "gib_s": round(batch.src_bytes / (ev_ms * 1e-3) / GIB, 1),
+           "algorithmic_bytes": alg,
+           "roofline_frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "validated": "every block against the generator", "generate_s": round(gen_s, 1)}
+    del batch, cols, src, gen
+    torch.cuda.empty_cache()
+    return out
+
+
 def max_over_ranks(dist, vals, device) -> list[float]:
     """MAX over ranks of the per-rank timings (the only collective; not on the data path)."""
     t = torch.tensor(vals, dtype=torch.float64, device=device)
@@ -699,8 +792,13 @@ def main():
     ap.add_argument("--config", default="4k", choices=sorted(synth.CONFIGS))
     ap.add_argument("--blocks", type=int, default=None, help="blocks generated per GPU")
     ap.add_argument("--gib-per-gpu", type=float, default=None,
-                    help="decode this many GiB per GPU by replicating the generated shard on the "
-                         "device (default: 12.5 with --gpus > 1, BASELINE.json configs[4])")
+                    help="make the metric's batch this many GiB per GPU by replicating the "
+                         "generated shard on the device (default: the 2^20-block shard at every N)")
+    ap.add_argument("--config5-gib", type=float, default=12.5,
+                    help="the config5 field: GiB per GPU (BASELINE.json configs[4]: 100 GiB over "
+                         "8 GPUs); 0 skips it")
+    ap.add_argument("--no-side-configs", action="store_true",
+                    help="skip the zipf and 64k fields (BASELINE.json configs[3], configs[2])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -729,8 +827,6 @@ def main():
 
     ctx = _lib.Context(local)
     gib = args.gib_per_gpu
-    if gib is None and world > 1 and args.config == "4k":
-        gib = 12.5                          # BASELINE.json configs[4]: 100 GiB over 8 GPUs
     full, part = (1, 0) if not gib else replicate_plan(int(ext[-1]), nb, int(gib * GIB))
     if full == 1 and part == 0:
         batch = DeviceBatch(src, ext, local)
@@ -744,25 +840,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx.reserve(nb_run, stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        decode_batch(ctx, batch, cols, stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t_start = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        decode_batch(ctx, batch, cols, stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t_start
-    ev_ms = ev0.elapsed_time(ev1) / args.steps
-    wall_max, ev_ms_max = max_over_ranks(dist, [wall, ev_ms], dev)
+    wall_max, ev_ms_max = time_decode(ctx, batch, cols, stream, args.steps, args.warmup, dist, dev)
     in_bytes = float(batch.src_bytes)
     value = job_rate(in_bytes, world, args.steps, wall_max)
     copies = full + (part / nb if part else 0.0)
@@ -779,6 +857,26 @@ def main():
         log(rank, "validation: all blocks OK, every key/value byte and end offset matches"
             + (" (replicas: metadata of every block, 1 % sample of slots)" if full > 1 or part else ""))
 
+
+    ceiling = None
+    try:   # the copy overwrites the decoded columns (validated above)
+        ceiling = copy_ceiling(batch, cols, alg, dev)   # rank 0's box is reported
+    except Exception as ex:  # reported, never the metric
+        log(rank, f"copy ceiling measurement failed: {ex}")
+
+    config5 = None
+    if args.config5_gib > 0 and args.config == "4k" and full == 1 and part == 0:
+        # BASELINE.json configs[4] on every rank, whatever N (all ranks join its collectives)
+        del cols
+        torch.cuda.empty_cache()
+        try:
+            config5 = config5_rate(ctx, src, ext, n_ent, kbytes, vbytes, gen, dev, dist, world,
+                                   args.config5_gib, args.steps, args.warmup)
+            log(rank, f"config5: {config5['gib_per_gpu']} GiB/GPU, {config5['value_gib_s']} GiB/s")
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"config5 measurement failed: {ex}")
+        cols = SlottedColumns(nb_run, batch.src_bytes, local)
+    decode_batch(ctx, batch, cols, stream)   # the decoded columns again (the seek field reads them)
 
     e2e = None
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
@@ -833,11 +931,16 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"reference-dataset baseline failed: {ex}")
 
-    ceiling = None
-    try:   # last: the copy overwrites the decoded columns
-        ceiling = copy_ceiling(batch, cols, alg, dev)   # rank 0's box is reported
-    except Exception as ex:  # reported, never the metric
-        log(rank, f"copy ceiling measurement failed: {ex}")
+    sides = {}
+    if side and not args.no_side_configs and args.config == "4k":
+        del batch, cols
+        torch.cuda.empty_cache()
+        for c in ("zipf", "64k"):
+            try:
+                sides[c] = side_config_rate(ctx, c, dev, args.steps, args.warmup)
+                log(rank, f"{c}: {sides[c]['gib_s']} GiB/s, frac {sides[c]['roofline_frac']}")
+            except Exception as ex:  # reported, never the metric
+                log(rank, f"{c} measurement failed: {ex}")
 
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -883,6 +986,9 @@ def main():
             "snappy": snappy,
             "lz4": lz4,
             "encode": encode,
+            "config5": config5,
+            "zipf": sides.get("zipf"),
+            "64k": sides.get("64k"),
         }
         print(json.dumps(out), flush=True)
     if dist:
