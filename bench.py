@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from topazdb_amd import _lib, synth  # noqa: E402
-from topazdb_amd.batch import DeviceBatch, SlottedColumns, decode_batch  # noqa: E402
+from topazdb_amd.batch import DeviceBatch, SlottedColumns, decode_batch, entry_first  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
 GIB = float(1 << 30)
@@ -79,7 +79,7 @@ def validate(cols: SlottedColumns, ext: np.ndarray, n_ent: np.ndarray, gen, dev)
     bid = np.arange(nb, dtype=np.int64)
     ext64 = ext[:-1].astype(np.int64)
     kb = _lib.slot_base(ext64, bid)
-    sb = _lib.entry_base(ext64, bid)
+    sb = cols.pair_base(ext64, bid)     # either ends layout
     ends = cols.ends.view(-1, 2)
     kpos = kpos.astype(np.int64)
     vpos = vpos.astype(np.int64)
@@ -295,7 +295,7 @@ def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps
     spill_used = np.zeros(1, np.uint64)
     cols = _lib.HostColumns(h_data.data_ptr(), h_ends.data_ptr(), ends_cap, first.ctypes.data,
                             count.ctypes.data, status.ctypes.data, crc.ctypes.data, None, 0,
-                            spill_off.ctypes.data, spill_used.ctypes.data)
+                            spill_off.ctypes.data, spill_used.ctypes.data, None, 0)
 
     def run():
         rc = ctx.decode_host_ptrs(h_src.data_ptr(), h_ext.ctypes.data, nb, cols, chunk_blocks)
@@ -330,6 +330,81 @@ def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps
             "copy_only_gib_s": round(in_bytes / ct / GIB, 2), "copy_only_s": round(ct, 4),
             "frac_of_copy_only": round(ct / dt, 3), "h2d_bytes": int(in_bytes), "d2h_bytes": down,
             "numa_cpus": len(cpus), "path": "tpz_decode_blocks_host (C ABI)"}
+
+
+def e2e_codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, reps: int = 2) -> dict:
+    """The host-to-host path for compressed blocks (tpz_decode_blocks_host with the codec step on
+    the device, compress.rs:104-111; snappy is topazdb's default, src/opt.rs:48): 2^18 "4kc"
+    blocks encoded with `codec`, pinned buffers on the GPU's NUMA node, h_data sized from
+    tpz_host_decoded_bound. Every status must be OK and every block's decoded length equal its
+    Uncompress form's. GiB/s of compressed input and of decoded (Uncompress) bytes; beside it
+    the copy-only ceiling of the same H2D and D2H volumes issued together."""
+    if nb not in _CODEC_REGION:
+        _CODEC_REGION[nb] = synth.make_region("4kc", nb)
+    src0, ext0 = _CODEC_REGION[nb]
+    raw = src0[:int(ext0[nb])]
+    enc = synth.snappy_blocks if codec == "snappy" else synth.lz4_blocks
+    s2, e2 = enc(raw, ext0[:nb + 1])
+    n_ent = block_counts(raw, ext0[:nb + 1])
+    cpus = gpu_local_cpus(dev.index)
+    old = os.sched_getaffinity(0)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    try:
+        h_src = torch.from_numpy(np.ascontiguousarray(s2)).pin_memory()
+        h_ext = np.ascontiguousarray(e2, np.uint64)
+        bound = _lib.host_decoded_bound(h_src.data_ptr(), h_ext.ctypes.data, nb)
+        dcap = _lib.data_capacity(bound, nb)
+        h_data = torch.empty(dcap, dtype=torch.uint8).pin_memory()
+        ends_cap = 2 * int(n_ent.sum()) + 64
+        h_ends = torch.empty(ends_cap, dtype=torch.int32).pin_memory()
+    finally:
+        os.sched_setaffinity(0, old)
+    first = np.zeros(nb + 1, np.uint64)
+    count = np.zeros(nb, np.uint32)
+    status = np.zeros(nb, np.uint8)
+    crc = np.zeros(nb, np.uint32)
+    spill_off = np.zeros(nb, np.uint64)
+    spill_used = np.zeros(1, np.uint64)
+    dext = np.zeros(nb + 1, np.uint64)
+    cols = _lib.HostColumns(h_data.data_ptr(), h_ends.data_ptr(), ends_cap, first.ctypes.data,
+                            count.ctypes.data, status.ctypes.data, crc.ctypes.data, None, 0,
+                            spill_off.ctypes.data, spill_used.ctypes.data, dext.ctypes.data, dcap)
+
+    def run():
+        rc = ctx.decode_host_ptrs(h_src.data_ptr(), h_ext.ctypes.data, nb, cols, 0)
+        assert rc == _lib.SUCCESS, "tpz_decode_blocks_host"
+    run()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t0)
+    assert (status == 0).all() and int(first[-1]) == int(n_ent.sum()), "e2e codec outputs"
+    assert np.array_equal(np.diff(dext.astype(np.int64)), np.diff(ext0[:nb + 1].astype(np.int64)))
+    dt = min(ts)
+    down = int(_lib.slot_base(int(dext[-1]), nb)) + 8 * int(first[-1])
+    d_src = torch.empty(int(h_ext[-1]), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(down, dtype=torch.uint8, device=dev)
+    h_out = h_data if down <= dcap else torch.empty(down, dtype=torch.uint8).pin_memory()
+    s_up, s_dn = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    cts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_up):
+            d_src.copy_(h_src[:int(h_ext[-1])], non_blocking=True)
+        with torch.cuda.stream(s_dn):
+            h_out[:down].copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        cts.append(time.perf_counter() - t0)
+    ct = min(cts[1:])
+    return {"codec": codec, "blocks": nb, "compressed_bytes": int(h_ext[-1]),
+            "decoded_bytes": int(dext[-1]), "s": round(dt, 4),
+            "gib_s_compressed_input": round(int(h_ext[-1]) / dt / GIB, 2),
+            "gib_s_decoded": round(int(dext[-1]) / dt / GIB, 2),
+            "copy_only_s": round(ct, 4), "frac_of_copy_only": round(ct / dt, 3),
+            "path": "tpz_decode_blocks_host (C ABI), codec step on the device"}
 
 
 def copy_ceiling(batch: DeviceBatch, cols: SlottedColumns, alg_bytes: int, dev,
@@ -743,6 +818,45 @@ def config5_rate(ctx, src, ext, n_ent, kbytes, vbytes, gen, dev, dist, world: in
     return out
 
 
+def exact_ends_rate(ctx, batch: DeviceBatch, ext, n_ent, gen, alg: int, dev, steps: int,
+                    warmup: int) -> dict:
+    """The metric's batch decoded into the exact ends layout (tpz_entry_first): the header pass
+    + scan and the decode timed with HIP events on the decode stream, every block validated, and
+    the device bytes each layout reserves per input byte."""
+    stream = torch.cuda.current_stream(dev)
+    first = entry_first(ctx, batch, stream)
+    for _ in range(warmup):
+        entry_first(ctx, batch, stream)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(steps):
+        ctx.entry_first_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
+                             batch.src_bytes, first.data_ptr(), stream.cuda_stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    first_ms = ev0.elapsed_time(ev1) / steps
+    n_pairs = int(first[batch.n_blocks].cpu())
+    cols = SlottedColumns(batch.n_blocks, batch.src_bytes, dev.index, 0, first, n_pairs)
+    wall, ev_ms = time_decode(ctx, batch, cols, stream, steps, warmup, None, dev)
+    validate(cols, ext, n_ent, gen, dev)
+    src_b = float(batch.src_bytes)
+    ends_exact = 8 * n_pairs
+    ends_slot = 8 * _lib.entry_capacity(batch.src_bytes, batch.n_blocks)
+    out = {"n_pairs": n_pairs, "entry_first_ms": round(first_ms, 4),
+           "kernel_ms": round(ev_ms, 4), "ms_per_step": round(wall * 1e3 / steps, 4),
+           "gib_s": round(src_b / (ev_ms * 1e-3) / GIB, 1),
+           "roofline_frac": round(alg / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "ends_bytes_per_input_byte": round(ends_exact / src_b, 4),
+           "slotted_ends_bytes_per_input_byte": round(ends_slot / src_b, 4),
+           "device_bytes_per_input_byte": round((cols.data.numel() + ends_exact + 8 * len(first))
+                                                / src_b, 4),
+           "slotted_device_bytes_per_input_byte": round((cols.data.numel() + ends_slot) / src_b, 4),
+           "validated": "every block against the generator"}
+    del cols, first
+    torch.cuda.empty_cache()
+    return out
+
+
 def side_config_rate(ctx, config: str, dev, steps: int, warmup: int) -> dict:
     """BASELINE.json configs[2] (64k) / configs[3] (zipf) at full size on one GPU: the metric's
     decode timing and roofline over that config's generated blocks, every block checked against
@@ -807,6 +921,7 @@ def main():
     ap.add_argument("--no-lz4", action="store_true")
     ap.add_argument("--no-seek", action="store_true")
     ap.add_argument("--no-encode", action="store_true")
+    ap.add_argument("--no-exact", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -880,6 +995,15 @@ def main():
 
     e2e = None
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
+    exact = None
+    if side and not args.no_exact and full == 1 and part == 0:
+        try:
+            exact = exact_ends_rate(ctx, batch, ext, n_ent, gen, alg, dev, args.steps, args.warmup)
+            log(rank, f"exact ends: {exact['gib_s']} GiB/s, {exact['ends_bytes_per_input_byte']} "
+                      "B of ends per input byte")
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"exact-ends measurement failed: {ex}")
+
     if not args.no_e2e:
         # every rank (BASELINE.json configs[4]: the H2D/D2H-inclusive rate at N GPUs, all ranks
         # sharing the host's links and memory): per-rank times, max over ranks, all bytes
@@ -917,6 +1041,10 @@ def main():
             snappy = codec_rate(ctx, dev, "snappy")
         except Exception as ex:  # reported, never the metric
             log(rank, f"snappy measurement failed: {ex}")
+        try:
+            snappy["e2e_h2d_d2h"] = e2e_codec_rate(ctx, dev, "snappy")
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"snappy e2e measurement failed: {ex}")
     if side and not args.no_lz4:
         try:
             lz4 = codec_rate(ctx, dev, "lz4")
@@ -987,6 +1115,7 @@ def main():
             "lz4": lz4,
             "encode": encode,
             "config5": config5,
+            "exact_ends": exact,
             "zipf": sides.get("zipf"),
             "64k": sides.get("64k"),
         }

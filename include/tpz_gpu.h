@@ -45,9 +45,11 @@ extern "C" {
  *   2  6 = OK_SPILLED, 7 = SPILL_FULL, 8 = CODEC_ERROR; spill arena fields in tpz_columns
  *   3  9 = BAD_ENTRY (a CRC-valid block with out-of-range entries decodes, with per-entry
  *      classes in its spill record, instead of MALFORMED); MALFORMED is now only the block-level
- *      panic of Block::decode; tpz_decode_blocks_host also takes snappy / lz4 blocks
+ *      panic of Block::decode
+ *   4  tpz_decode_blocks_host takes snappy / lz4 blocks (tpz_host_columns.h_dext, data_cap);
+ *      the exact ends layout (tpz_columns.d_entry_first, tpz_table.d_entry_first)
  * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
-#define TPZ_ABI_VERSION 3
+#define TPZ_ABI_VERSION 4
 int tpz_abi_version(void);
 
 /* ---- API return codes ------------------------------------------------------------------- */
@@ -184,6 +186,11 @@ typedef struct {
   uint64_t spill_cap;
   uint64_t* d_spill_off;    /* n_blocks: written for OK_SPILLED, BAD_ENTRY, SPILL_FULL only   */
   uint64_t* d_spill_used;   /* one u64                                                      */
+  const uint64_t* d_entry_first; /* NULL: the slotted ends (tpz_entry_base). Else the exact
+                                    ends layout: block i's {kend, vend} pairs at
+                                    d_ends[2*d_entry_first[i] ..], d_ends holding
+                                    2*d_entry_first[n_blocks] u32, d_entry_first from
+                                    tpz_entry_first (see below)                             */
 } tpz_columns;
 
 /* Offset of a spilled record's stream from the record start: its 2*n u32 ends, 128-aligned. */
@@ -245,6 +252,19 @@ tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
 tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* out,
                           void* stream);
 
+/* The exact ends layout. The slotted ends reserve the worst case (a pair per 6 input bytes,
+ * ~1.36x the input in ends alone for 4 KiB blocks) so that blocks need no prefix pass; a caller
+ * that keeps the decoded columns resident (a block cache in HBM) can instead reserve exactly n
+ * pairs per block, 8 bytes per entry: d_first[i] = the sum over blocks 0..i-1 of the header n
+ * (u16 at the block's first two bytes) of each block the decode parses in place (last byte 1,
+ * len >= 7 + 2n, 6n <= len; 0 for any other block, whose pairs, if any, live in its spill
+ * record), d_first[n_blocks] = the total, computed on the device (a header pass and a scan, no
+ * host sync). A block that decodes in place has count == its header n, so its pairs fit. Pass
+ * d_first as tpz_columns.d_entry_first / tpz_table.d_entry_first. The batch must be the one
+ * the decode runs over (after the codec step). Asynchronous on `stream`; uses the stream's
+ * workspace. */
+tpz_err tpz_entry_first(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_first, void* stream);
+
 /* Dense entry ends for consumers that copy a batch out (e.g. back to the host): the slotted
  * ends reserve the worst case (a pair per 6 input bytes, ~1.33x the input) so that blocks need no
  * prefix pass; this packs the used pairs. d_first = exclusive prefix sums of out->d_count
@@ -257,26 +277,39 @@ tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* c
 /* ---- the host pipeline -------------------------------------------------------------------
  * SsTable::read_block for a whole run of blocks that sit in HOST memory (src/table.rs:154-164;
  * the bytes FileObject::read's pread returns, src/table/file_object.rs:23-27): the library
- * copies the blocks to the device in chunks, decodes them (tpz_decode_blocks), packs the used
- * entry ends (tpz_pack_ends) and copies every output back, on three streams (upload, decode,
- * download) so that both PCIe directions stay busy. Synchronous: returns when every output is in
- * host memory. The caller's buffers are page-locked for the duration of the call when they are
- * not already (hipHostRegister); pinned buffers (hipHostMalloc) avoid that cost.
+ * copies the blocks to the device in chunks, runs compress::decode's codec step on them where a
+ * block is snappy or lz4 (src/block/compress.rs:104-111; topazdb's default codec is snappy,
+ * src/opt.rs:48), decodes them (tpz_decode_blocks), packs the used entry ends (tpz_pack_ends)
+ * and copies every output back, on three streams (upload, decode, download) so that both PCIe
+ * directions stay busy. Synchronous: returns when every output is in host memory. The caller's
+ * buffers are page-locked for the duration of the call when they are not already
+ * (hipHostRegister); pinned buffers (hipHostMalloc) avoid that cost.
  *
- * Block i = h_src[h_ext[i] .. h_ext[i+1]) (h_ext non-decreasing, any alignment). Outputs:
- *   h_data    tpz_data_capacity(h_ext[n], n) bytes: the slotted stream layout of tpz_columns,
- *             exactly as tpz_decode_blocks writes it for this batch (slot bases from h_ext)
+ * Block i = h_src[h_ext[i] .. h_ext[i+1]) (h_ext non-decreasing, any alignment, any mix of
+ * codec tags). The decoded layout is that of tpz_columns over the DECODED extents h_dext: for
+ * a batch of Uncompress blocks h_dext = h_ext; when any block is snappy or lz4, h_dext[i+1] -
+ * h_dext[i] = the block's length after the codec step (its Uncompress form; the codec's Err
+ * leaves a 1-byte stub, tpz_decompressed_sizes), computed on the device chunk by chunk with no
+ * whole-batch host sync. Outputs:
+ *   h_data    data_cap bytes (0 = tpz_data_capacity(h_ext[n], n), enough for Uncompress
+ *             batches; for snappy / lz4 blocks use tpz_data_capacity(bound, n) with bound from
+ *             tpz_host_decoded_bound): the slotted stream layout, block i's slot at
+ *             tpz_slot_base(h_dext[i], i)
+ *   h_dext    n + 1 decoded extents (may be NULL for a batch without snappy / lz4 blocks)
  *   h_ends    every decoded block's {kend, vend} pairs, dense in block order: block i's at
  *             h_ends[2*h_first[i] ..]; ends_cap = its capacity in u32
  *   h_first   n + 1 entries: h_first[i] = pairs before block i (OK, OK_SPILLED and BAD_ENTRY
  *             blocks only)
- *   h_count, h_status, h_crc    n each, as tpz_columns
+ *   h_count, h_status, h_crc    n each, as tpz_columns; a block whose codec step failed has
+ *             status TPZ_BLOCK_CODEC_ERROR (the reference's Err of the codec), count 0
  *   h_spill, spill_cap, h_spill_off, h_spill_used   as tpz_columns, in host memory: spilled
  *             blocks' records (the library's device arenas grow as needed)
- * Returns TPZ_ERR_NOMEM when ends_cap or spill_cap is too small: h_first[n] and *h_spill_used
- * then hold the sizes needed (the call can be repeated with larger buffers). chunk_blocks = 0
- * picks the default (8,192 blocks per chunk: 34 MB of 4 KiB blocks, the fastest of 4K..64K on
- * MI355X, profiles/r2/e2e_sweep.jsonl). */
+ * Returns TPZ_ERR_NOMEM when ends_cap, spill_cap or data_cap is too small: h_first[n],
+ * *h_spill_used and h_dext[n] then hold the sizes needed (the call can be repeated with larger
+ * buffers). chunk_blocks = 0 picks the default (8,192 blocks per chunk: 34 MB of 4 KiB blocks,
+ * the fastest of 4K..64K on MI355X, profiles/r2/e2e_sweep.jsonl). The streams and device buffers
+ * of a call are kept by the context and reused by its next calls (one set per concurrent
+ * caller). */
 typedef struct {
   uint8_t* h_data;
   uint32_t* h_ends;
@@ -289,7 +322,15 @@ typedef struct {
   uint64_t spill_cap;
   uint64_t* h_spill_off;
   uint64_t* h_spill_used;
+  uint64_t* h_dext;         /* n + 1 decoded extents, or NULL (see above)                   */
+  uint64_t data_cap;        /* bytes at h_data; 0 = tpz_data_capacity(h_ext[n], n)          */
 } tpz_host_columns;
+
+/* An upper bound of h_dext[n] for blocks in host memory, from their headers alone: a snappy
+ * block's preamble length + 1, an lz4 block's size prefix + 1 (lz4::block::decompress may keep
+ * fewer bytes), any other block's own length. Size h_data with tpz_data_capacity(bound, n). */
+tpz_err tpz_host_decoded_bound(const uint8_t* h_src, const uint64_t* h_ext, uint32_t n_blocks,
+                               uint64_t* bound);
 
 tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext,
                                uint32_t n_blocks, const tpz_host_columns* out,
@@ -368,6 +409,7 @@ typedef struct {
   const uint8_t* d_spill;      /* the decode's spill arena and record offsets (OK_SPILLED,
                                   BAD_ENTRY)                                               */
   const uint64_t* d_spill_off;
+  const uint64_t* d_entry_first; /* the decode's tpz_columns.d_entry_first (NULL: slotted)   */
 } tpz_table;
 
 tpz_err tpz_seek_keys(tpz_ctx* ctx, const tpz_table* table, const uint8_t* d_keys,

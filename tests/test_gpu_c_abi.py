@@ -1,9 +1,13 @@
 """The C ABI used from a plain C program on the GPU (examples/c_abi_decode.c): build blocks,
 decode + verify them, check every key/value, status and CRC against the host side, and the
 per-payload range CRCs. No Python on the data path."""
+import os
 import subprocess
 
 import pytest
+
+import _oracle as O
+from conftest import GOLDEN, read_golden
 
 from test_abi import _build_c_example
 
@@ -17,17 +21,44 @@ def test_c_program_decodes_and_verifies(tmp_path):
     assert r.stdout.startswith("ok ") and r.stdout.split()[2] == "30000"
 
 
+@pytest.mark.parametrize("codec", [0, 2, 3])
 @pytest.mark.parametrize("chunk,pinned", [(37, 0), (1000, 1), (65536, 0)])
-def test_c_host_pipeline(tmp_path, chunk, pinned):
+def test_c_host_pipeline(tmp_path, chunk, pinned, codec):
     """tpz_decode_blocks_host from plain C (examples/c_host_decode.c): blocks in host memory
-    through the library's H2D -> decode -> D2H pipeline, several chunks per call, pageable or
-    pinned buffers; every status/CRC/key/value checked, including a corrupted block and a
-    spilled block's record."""
+    through the library's H2D -> codec step -> decode -> D2H pipeline, several chunks per call,
+    pageable or pinned buffers, Uncompress / snappy / lz4 blocks (compress.rs:104-111, the
+    reference's default codec is snappy); every status/CRC/key/value checked at the decoded
+    extents, including a corrupted block, a stream the codec rejects and a spilled block's
+    record."""
     exe = _build_c_example(tmp_path, "c_host_decode")
-    r = subprocess.run([exe, "30000", str(chunk), str(pinned)], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([exe, "30000", str(chunk), str(pinned), str(codec)], capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("ok ") and r.stdout.split()[2] == "30000"
+
+
+@pytest.mark.parametrize("name", ["sst_snappy_bench", "sst_snappy_4k", "sst_lz4_bench",
+                                  "sst_lz4_4k", "sst_4k_k16_v100", "sst_100_b128"])
+@pytest.mark.parametrize("chunk", [0, 3])
+def test_c_host_pipeline_golden_sst(tmp_path, name, chunk):
+    """Golden SST files (snappy, lz4, Uncompress) read from disk by plain C and decoded through
+    tpz_decode_blocks_host: every entry byte-equal to the oracle's SsTableIterator over the same
+    file."""
+    exe = _build_c_example(tmp_path, "c_host_decode")
+    path = os.path.join(GOLDEN, name + ".sst")
+    r = subprocess.run([exe, "--sst", path, str(chunk)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().split("\n")
+    assert lines[-1].startswith("ok sst ")
+    got = [tuple(bytes.fromhex(x) for x in ln.split(" ")) for ln in lines[:-1]]
+    it = O.SstIter(read_golden(name + ".sst"))
+    it.seek_to_first()
+    want = []
+    while it.is_valid():
+        want.append((it.key(), it.value()))
+        it.next()
+    assert got == want and len(want) > 0
 
 
 @pytest.mark.parametrize("n,block_size", [(50000, 4096), (3000, 65536), (20000, 128)])

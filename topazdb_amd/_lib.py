@@ -22,7 +22,7 @@ SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
  BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR, BLOCK_BAD_ENTRY) = range(10)
 # tpz_entry_class (BAD_ENTRY blocks)
 ENTRY_OK, ENTRY_BAD_VALUE, ENTRY_BAD_KEY = 0, 1, 2
-ABI_VERSION = 3           # TPZ_ABI_VERSION this binding was written against
+ABI_VERSION = 4           # TPZ_ABI_VERSION this binding was written against
 LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks with 64+ entries take the spill path
 BIGWAVE_BLOCK_BYTES = 0x40000000   # TPZ_BIGWAVE_BLOCK_BYTES
 
@@ -40,10 +40,10 @@ class Columns(C.Structure):
     _fields_ = [("d_data", C.c_void_p), ("d_ends", C.c_void_p), ("d_count", C.c_void_p),
                 ("d_status", C.c_void_p), ("d_crc", C.c_void_p), ("d_spill", C.c_void_p),
                 ("spill_cap", C.c_uint64), ("d_spill_off", C.c_void_p),
-                ("d_spill_used", C.c_void_p)]
+                ("d_spill_used", C.c_void_p), ("d_entry_first", C.c_void_p)]
 
 COLUMN_FIELDS = ("data", "ends", "count", "status", "crc", "spill", "spill_cap", "spill_off",
-                 "spill_used")
+                 "spill_used", "entry_first")
 
 
 class Table(C.Structure):
@@ -51,7 +51,7 @@ class Table(C.Structure):
     _fields_ = [("d_first_keys", C.c_void_p), ("d_first_pos", C.c_void_p), ("d_ext", C.c_void_p),
                 ("n_blocks", C.c_uint32), ("d_data", C.c_void_p), ("d_ends", C.c_void_p),
                 ("d_count", C.c_void_p), ("d_status", C.c_void_p), ("d_spill", C.c_void_p),
-                ("d_spill_off", C.c_void_p)]
+                ("d_spill_off", C.c_void_p), ("d_entry_first", C.c_void_p)]
 
 
 class Entries(C.Structure):
@@ -66,7 +66,8 @@ class HostColumns(C.Structure):
     _fields_ = [("h_data", C.c_void_p), ("h_ends", C.c_void_p), ("ends_cap", C.c_uint64),
                 ("h_first", C.c_void_p), ("h_count", C.c_void_p), ("h_status", C.c_void_p),
                 ("h_crc", C.c_void_p), ("h_spill", C.c_void_p), ("spill_cap", C.c_uint64),
-                ("h_spill_off", C.c_void_p), ("h_spill_used", C.c_void_p)]
+                ("h_spill_off", C.c_void_p), ("h_spill_used", C.c_void_p),
+                ("h_dext", C.c_void_p), ("data_cap", C.c_uint64)]
 
 
 _lib = None
@@ -120,9 +121,14 @@ def lib() -> C.CDLL:
         L.tpz_pack_ends.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
                                     C.c_void_p, C.c_void_p, C.c_void_p]
         L.tpz_pack_ends.restype = C.c_int
+        L.tpz_entry_first.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
+        L.tpz_entry_first.restype = C.c_int
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
+        L.tpz_host_decoded_bound.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.POINTER(C.c_uint64)]
+        L.tpz_host_decoded_bound.restype = C.c_int
         L.tpz_plan_blocks.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_uint32, C.c_void_p,
                                       C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
                                       C.c_void_p]
@@ -236,6 +242,13 @@ class Context:
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")
 
+    def entry_first_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
+                         d_first: int, stream: int = 0) -> None:
+        """tpz_entry_first: the exact ends layout's per-block pair offsets (n_blocks + 1 u64)."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        check(lib().tpz_entry_first(self.handle, C.byref(b), C.c_void_p(d_first),
+                                    C.c_void_p(stream)), "tpz_entry_first")
+
     def decode_host_ptrs(self, h_src: int, h_ext: int, n_blocks: int, cols: HostColumns,
                          chunk_blocks: int = 0) -> int:
         """tpz_decode_blocks_host (blocks in host memory; H2D, decode, D2H inside the library).
@@ -321,6 +334,14 @@ def _pack_ends(ctx, d_ext: int, n_blocks: int, src_bytes: int, cols: dict, d_fir
     c = Columns(*[cols[f] for f in COLUMN_FIELDS])
     check(lib().tpz_pack_ends(ctx.handle, C.byref(b), C.byref(c), C.c_void_p(d_first),
                               C.c_void_p(d_dense), C.c_void_p(stream)), "tpz_pack_ends")
+
+
+def host_decoded_bound(h_src: int, h_ext: int, n_blocks: int) -> int:
+    """tpz_host_decoded_bound: an upper bound of the decoded bytes of blocks in host memory."""
+    b = C.c_uint64()
+    check(lib().tpz_host_decoded_bound(C.c_void_p(h_src), C.c_void_p(h_ext), n_blocks,
+                                       C.byref(b)), "tpz_host_decoded_bound")
+    return int(b.value)
 
 
 def bloom_geometry(n_keys: int, fpp: float):

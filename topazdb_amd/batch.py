@@ -51,12 +51,16 @@ class SlottedColumns:
     """Device output buffers in the slotted layout of include/tpz_gpu.h (tpz_columns), plus the
     spill arena for blocks whose decoded entries do not fit their slot (TPZ_BLOCK_OK_SPILLED)."""
 
-    def __init__(self, n_blocks: int, src_bytes: int, device: int = 0, spill_cap: int = 0):
+    def __init__(self, n_blocks: int, src_bytes: int, device: int = 0, spill_cap: int = 0,
+                 entry_first: torch.Tensor | None = None, n_pairs: int | None = None):
+        """entry_first / n_pairs: the exact ends layout (tpz_entry_first's offsets and their
+        total, see exact_columns); None: the slotted ends (tpz_entry_base)."""
         dev = _dev(device)
         cap = _lib.data_capacity(src_bytes, n_blocks)
-        ecap = _lib.entry_capacity(src_bytes, n_blocks)
+        ecap = _lib.entry_capacity(src_bytes, n_blocks) if entry_first is None else max(n_pairs, 1)
         nb = max(n_blocks, 1)
         self.device = device
+        self.entry_first = entry_first
         self.data = torch.empty(cap, dtype=torch.uint8, device=dev)   # keys | gap | values
         self.ends = torch.empty(2 * ecap, dtype=torch.int32, device=dev)  # {kend, vend} pairs
         self.count = torch.empty(nb, dtype=torch.int32, device=dev)
@@ -78,7 +82,14 @@ class SlottedColumns:
                                                      "spill_off", "spill_used")}
         p["spill"] = self.spill.data_ptr() if self.spill is not None else None
         p["spill_cap"] = self.spill_cap
+        p["entry_first"] = self.entry_first.data_ptr() if self.entry_first is not None else None
         return p
+
+    def pair_base(self, ext: np.ndarray, bid: np.ndarray) -> np.ndarray:
+        """Index of each block's first {kend, vend} pair in `ends` (either layout)."""
+        if self.entry_first is None:
+            return _lib.entry_base(ext, bid)
+        return self.entry_first.cpu().numpy()[bid]
 
     def complete(self) -> "SlottedColumns":
         """Waits for the decode; if its spill arena was too small (TPZ_BLOCK_SPILL_FULL blocks),
@@ -121,7 +132,7 @@ class SlottedColumns:
         kend_d, vend_d = ends[0::2], ends[1::2]
         # every entry's key/value end, previous end and stream base in one virtual buffer:
         # [slotted data | spill arena]
-        sb = _lib.entry_base(ext, bid)
+        sb = self.pair_base(ext, bid)
         slot = sb[eblk] + j
         cls = np.zeros(total, np.uint8)
         ke = np.zeros(total, np.int64)
@@ -224,6 +235,27 @@ def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None =
     return cols
 
 
+def entry_first(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None
+                ) -> torch.Tensor:
+    """tpz_entry_first (asynchronous): int64 pair offsets of the exact ends layout, n_blocks + 1."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(s):
+        first = torch.empty(batch.n_blocks + 1, dtype=torch.int64, device=dev)
+    ctx.entry_first_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
+                         batch.src_bytes, first.data_ptr(), s.cuda_stream)
+    return first
+
+
+def exact_columns(ctx: Context, batch: DeviceBatch, spill_cap: int = 0,
+                  stream: torch.cuda.Stream | None = None) -> SlottedColumns:
+    """Columns with the exact ends layout: 8 bytes of ends per entry instead of the slotted
+    worst case. Reads the total back (one sync) to size the ends."""
+    first = entry_first(ctx, batch, stream)
+    n_pairs = int(first[batch.n_blocks].cpu())
+    return SlottedColumns(batch.n_blocks, batch.src_bytes, ctx.device, spill_cap, first, n_pairs)
+
+
 def pack_ends(ctx: Context, batch: DeviceBatch, cols: SlottedColumns,
               stream: torch.cuda.Stream | None = None):
     """tpz_pack_ends: the used {kend, vend} pairs of every block, dense in block order (for a
@@ -236,7 +268,8 @@ def pack_ends(ctx: Context, batch: DeviceBatch, cols: SlottedColumns,
     with torch.cuda.stream(s):
         first = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
         torch.cumsum(cols.count[:nb].to(torch.int64), 0, out=first[1:])
-        dense = torch.empty(cols.ends.numel(), dtype=torch.int32, device=dev)
+        dense = torch.empty(max(cols.ends.numel(), 2 * _lib.entry_capacity(batch.src_bytes, nb)),
+                            dtype=torch.int32, device=dev)
     _lib._pack_ends(ctx, batch.ext.data_ptr(), nb, batch.src_bytes, cols.ptrs(), first.data_ptr(),
                     dense.data_ptr(), s.cuda_stream)
     return first, dense

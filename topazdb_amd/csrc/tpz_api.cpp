@@ -140,8 +140,10 @@ struct tpz_ctx {
   uint32_t* d_tables = nullptr;        // block-decode CRC tables
   uint32_t* d_range_tables = nullptr;  // range-CRC tables
   uint32_t* d_rep_tables = nullptr;    // replicated slice-by-4 tables
-  std::mutex mu;  // guards the workspace map
+  std::mutex mu;  // guards the workspace map and the host pipelines
   std::unordered_map<void*, tpz_workspace> ws;
+  std::vector<void*> pipes;        // every host pipeline of the context (owned)
+  std::vector<void*> pipes_free;   // those not in use by a tpz_decode_blocks_host call
 };
 
 namespace {
@@ -211,6 +213,18 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
 }  // namespace
 
 int tpz_internal_device(tpz_ctx* c) { return c->device; }
+void* tpz_internal_pipe_acquire(tpz_ctx* c) {
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->pipes_free.empty()) return nullptr;
+  void* p = c->pipes_free.back();
+  c->pipes_free.pop_back();
+  return p;
+}
+void tpz_internal_pipe_release(tpz_ctx* c, void* pipe, bool fresh) {
+  std::lock_guard<std::mutex> g(c->mu);
+  if (fresh) c->pipes.push_back(pipe);
+  c->pipes_free.push_back(pipe);
+}
 tpz_err tpz_internal_hip_fail(hipError_t e, const char* what) { return hip_fail(e, what); }
 
 extern "C" {
@@ -271,6 +285,7 @@ void tpz_ctx_destroy(tpz_ctx* c) {
   if (c->d_range_tables) (void)hipFree(c->d_range_tables);
   if (c->d_rep_tables) (void)hipFree(c->d_rep_tables);
   for (auto& kv : c->ws) free_workspace(kv.second);
+  for (void* p : c->pipes) tpz_internal_pipe_destroy(p);
   delete c;
 }
 
@@ -329,6 +344,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.num_cus = c->num_cus;
   a.big_scratch = w->d_big_scratch;
   a.big_grid = c->num_cus;
+  a.efirst = o->d_entry_first;
   tpz::launch_decode(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
@@ -413,6 +429,22 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
   return TPZ_SUCCESS;
 }
 
+tpz_err tpz_entry_first(tpz_ctx* c, const tpz_batch* b, uint64_t* d_first, void* stream) {
+  if (!c || !b || !d_first) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks && (!b->d_src || !b->d_ext)) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  uint32_t* part = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err e = get_acc(c, stream, 2 * (uint32_t)tpz::entry_first_parts(b->n_blocks), &part);
+    if (e != TPZ_SUCCESS) return e;
+  }
+  tpz::launch_entry_first(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, d_first,
+                          reinterpret_cast<uint64_t*>(part), (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
 tpz_err tpz_crc32_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t* d_crc, void* stream) {
   return crc_ranges(c, r, 0, d_crc, nullptr, stream);
 }
@@ -435,7 +467,8 @@ tpz_err tpz_seek_keys(tpz_ctx* c, const tpz_table* t, const uint8_t* d_keys,
   TPZ_HIP(hipSetDevice(c->device));
   tpz::SeekLaunch a{t->d_first_keys, t->d_first_pos, t->n_blocks, t->d_ext, t->d_data,
                     t->d_ends, t->d_count, t->d_status, t->d_spill, t->d_spill_off, d_keys,
-                    d_key_pos, n_keys, d_block, d_entry, d_status, d_valid};
+                    d_key_pos, n_keys, d_block, d_entry, d_status, d_valid,
+                    t->d_entry_first};
   tpz::launch_seek(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
@@ -613,7 +646,7 @@ tpz_err tpz_pack_ends(tpz_ctx* c, const tpz_batch* b, const tpz_columns* cols,
   if (!b->d_ext || !cols->d_ends || !cols->d_count || !cols->d_status) return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   tpz::PackLaunch a{b->d_ext, b->n_blocks, cols->d_ends, cols->d_count, cols->d_status,
-                    cols->d_spill, cols->d_spill_off, d_first, d_dense};
+                    cols->d_spill, cols->d_spill_off, d_first, d_dense, cols->d_entry_first};
   tpz::launch_pack_ends(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;

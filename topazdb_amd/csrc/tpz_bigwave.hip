@@ -177,6 +177,7 @@ struct BWParams {
   u32* spill_count;
   u32* big_list;
   u32* big_count;
+  const u64* efirst;        // exact ends layout, or null: slotted
   u32 lane_shift[64];       // x^(8 * 128 l) mod P
   u32 win_shift;            // x^(8 * 8192) mod P
   u32 half_shift;           // x^(8 * 64) mod P
@@ -553,8 +554,9 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
         const u32 vs = (ktot + 15) & ~15u;                                     // tpz_value_start
         const bool slots_fit = 6u * n <= len;
         // the {kend, vend} pairs, whole 128-byte lines (pairs past n are zero)
-        uint2* ends_g = reinterpret_cast<uint2*>(p.ends) + entry_base(s, b);
-        if (slots_fit && lane < ((n + 15) & ~15u)) ends_g[lane] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
+        uint2* ends_g = reinterpret_cast<uint2*>(p.ends) + ends_base(p.efirst, s, b);
+        if (slots_fit && lane < (p.efirst ? n : (n + 15) & ~15u))
+          ends_g[lane] = act ? make_uint2(ki, vi) : make_uint2(0, 0);
         if (bad || !slots_fit || (u64)vs + vtot > (u64)len + 2) {
           // entries out of range (TPZ_BLOCK_BAD_ENTRY), or entries that overlap or repeat: the
           // spill path decodes the block (CRC included)
@@ -721,6 +723,7 @@ void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream) {
   p.spill_count = a.spill_count;
   p.big_list = a.big_list;
   p.big_count = a.big_count;
+  p.efirst = a.efirst;
   for (int l = 0; l < 64; l++) p.lane_shift[l] = x8n_host((u64)kRun * l);
   for (int l = 0; l < 64; l++) p.step_lane_shift[l] = x8n_host((u64)kStepRun * l);
   p.step_shift = x8n_host(kStep);

@@ -464,6 +464,7 @@ struct Out {
   u32* spill_count;
   u32* bw_list;        // long blocks with n < 64: decode_bigwave_kernel (tpz_bigwave.hip)
   u32* bw_count;
+  const u64* efirst;   // exact ends layout (tpz_columns.d_entry_first), or null: slotted
 };
 
 // Lane 0 appends block b to a worklist (the big path's or the spill path's).
@@ -829,8 +830,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
     const u32 dl = P - 2 - 2 * n;
     const bool slots_fit = 6u * n <= len;
-    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
-    const u32 n_pad = (n + 15) & ~15u;  // whole 128-byte lines of {kend, vend}
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
+    // whole 128-byte lines of {kend, vend} in the slotted layout; exactly n in the exact one
+    const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
     {
       // clear the chunk map up to the largest chunk index a block that fits its slot can
       // produce (stream <= len + 2 bytes; the others go to the spill path)
@@ -1290,8 +1292,8 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
 #ifndef TPZ_ABL_NOPARSE
     const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
     const bool slots_fit = 6u * n <= len;
-    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + entry_base(ext_b, b);
-    const u32 n_pad = (n + 15) & ~15u;
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
+    const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
     const u32 G = (n + 63) >> 6;
     // pass 1: group sums (read back by the same wave when there is one group)
     for (u32 g = wid; g < G; g += kBigWaves) {
@@ -1571,7 +1573,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.big_scratch = a.big_scratch;
   p.spill_used = a.spill_used;
   p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count,
-              a.spill_list, a.spill_count, a.bw_list, a.bw_count};
+              a.spill_list, a.spill_count, a.bw_list, a.bw_count, a.efirst};
   const u32* xp = big_super_shifts();
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   const u32* ls = lane_run_shifts();
@@ -1584,7 +1586,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
     // before the big kernel: it may hand a block with 64+ entries to the big list
     BigWaveLaunch bw{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.bw_count,
                      a.data, a.ends, a.count, a.status, a.crc, a.spill_list, a.spill_count,
-                     a.defer_list, a.defer_count, a.num_cus};
+                     a.defer_list, a.defer_count, a.num_cus, a.efirst};
     launch_bigwave(bw, stream);
   }
   hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p);

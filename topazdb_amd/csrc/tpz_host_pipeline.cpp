@@ -2,10 +2,11 @@
 //
 // topazdb reads a block with one pread into a fresh Vec (FileObject::read,
 // src/table/file_object.rs:23-27) and decodes it on the CPU (SsTable::read_block,
-// src/table.rs:154-164). Here a whole run of blocks in host memory goes through the device:
-// chunks of blocks are uploaded, decoded (tpz_decode_blocks), their entry ends packed
-// (tpz_pack_ends) and every output copied back, on two streams so that chunk k+1's upload and
-// decode overlap chunk k's downloads.
+// src/table.rs:154-164), snappy and lz4 blocks through the codec first (compress::decode,
+// src/block/compress.rs:104-111). Here a whole run of blocks in host memory goes through the
+// device: chunks of blocks are uploaded, decompressed where they are snappy / lz4
+// (tpz_decompressed_sizes + tpz_decompress_blocks), decoded (tpz_decode_blocks), their entry
+// ends packed (tpz_pack_ends) and every output copied back.
 //
 // Chunk geometry. A chunk of blocks [lo, hi) is uploaded to a device buffer whose byte 0 stands
 // for host byte B = ext[lo] rounded down to a multiple of 384 (= lcm(128, 96)); its extents are
@@ -16,13 +17,26 @@
 // [ext[lo], ext[hi]) are uploaded; the decode never reads the bytes of the device buffer before
 // the chunk's first block (the first 16-byte piece is masked, tpz_decode.hip zero_head).
 //
+// Codec batches. When any block of the batch is snappy or lz4, the slotted layout follows the
+// DECODED extents (each block's length after the codec step), which only the device learns.
+// Every chunk then runs the codec step, and a one-workgroup kernel (chunk_extents_kernel) turns
+// the chunk's decoded sizes into its extents: global ones (the chunk's decoded base, kept in a
+// device array chunk_base[] that each chunk extends for the next one in stream order, plus the
+// prefix) for h_dext, and local ones relative to the decoded base rounded down to 384 for the
+// decode, exactly as above. It also checks the chunk's device buffers: a chunk whose decoded
+// bytes, slots or entry ends do not fit gets empty extents (nothing is decompressed or decoded
+// out of bounds) and an overflow flag; the host grows the buffers and runs the chunk again when
+// it reads the chunk's metadata. No whole-batch host sync.
+//
 // Three streams and three buffer slots, so that the two copy directions run at once:
 //   up:    H2D of chunk k's blocks and extents (after chunk k-3's downloads freed its slot)
-//   comp:  decode, the entry prefix (count_prefix_kernel), D2H of the per-block metadata;
-//          later, once the host has placed the chunk, tpz_pack_ends
+//   comp:  the codec step, decode, the entry prefix (count_prefix_kernel), D2H of the per-block
+//          metadata; later, once the host has placed the chunk, tpz_pack_ends
 //   down:  D2H of the slots, the packed ends and the spill records
-// The host waits only for chunk k's metadata (entry total, spill bytes), while chunk k+1 uploads
-// and chunk k-1 downloads; a spill arena that overflowed is grown and the chunk decoded again.
+// The host waits only for chunk k's metadata (entry total, spill bytes, decoded extents), while
+// chunk k+1 uploads and chunk k-1 downloads; a spill arena or codec buffer that overflowed is
+// grown and the chunk decoded again. The streams, events and buffers belong to a Pipe that the
+// context keeps and reuses across calls (one per concurrent caller).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -70,6 +84,18 @@ struct Pin {
   }
 };
 
+// Per-chunk metadata of a codec chunk, written by chunk_extents_kernel.
+struct ChunkMeta {
+  uint64_t dbase;      // the chunk's first decoded byte in the batch
+  uint64_t dbase384;   // dbase rounded down to 384: device byte 0 of the decoded chunk
+  uint64_t total;      // the chunk's decoded bytes
+  uint64_t need_dst;   // device bytes the decoded chunk needs (dbase - dbase384 + total)
+  uint64_t need_data;  // tpz_data_capacity of the local extents
+  uint64_t need_ends;  // u32 of the slotted ends
+  uint32_t overflow;   // a need exceeded the chunk's buffers: extents emptied, redo
+  uint32_t pad;
+};
+
 struct Slot {
   hipEvent_t ev = nullptr;        // metadata landed (comp)
   hipEvent_t ev_up = nullptr;     // blocks uploaded (up)
@@ -78,12 +104,13 @@ struct Slot {
   bool used = false;
   Buf d_src, d_ext, d_data, d_ends, d_count, d_status, d_crc, d_spill, d_spill_off, d_used,
       d_first, d_dense;
-  Buf h_ext, h_first, h_count, h_status, h_crc, h_spill_off, h_used;
-  uint32_t lo = 0, hi = 0;
+  Buf d_size, d_dext, d_gext, d_dst, d_cstat, d_meta;          // the codec step
+  Buf h_ext, h_first, h_count, h_status, h_crc, h_spill_off, h_used, h_gext, h_meta;
+  uint32_t lo = 0, hi = 0, k = 0;
   uint64_t base = 0;   // host byte of device byte 0 (a multiple of 384)
   Slot() {
     h_ext.host = h_first.host = h_count.host = h_status.host = h_crc.host = h_spill_off.host =
-        h_used.host = true;
+        h_used.host = h_gext.host = h_meta.host = true;
   }
   ~Slot() {
     for (hipEvent_t e : {ev, ev_up, ev_pack, ev_down})
@@ -91,13 +118,117 @@ struct Slot {
   }
 };
 
+constexpr int kSlots = 3;
+
 #define PIPE_HIP(call)                                                         \
   do {                                                                         \
     hipError_t e_ = (call);                                                    \
     if (e_ != hipSuccess) return tpz_internal_hip_fail(e_, #call);             \
   } while (0)
 
+// One workgroup: decoded sizes -> the chunk's global and local extents, the next chunk's base,
+// the buffer checks (see the file comment).
+__global__ __launch_bounds__(1024) void chunk_extents_kernel(const uint64_t* size, uint32_t m,
+                                                             uint64_t* chunk_base, uint32_t k,
+                                                             uint64_t cap_dst, uint64_t cap_data,
+                                                             uint64_t cap_ends, uint64_t* gext,
+                                                             uint64_t* lext, ChunkMeta* meta) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x, per = (m + 1023) / 1024;
+  const uint32_t i0 = t * per < m ? t * per : m, i1 = i0 + per < m ? i0 + per : m;
+  uint64_t s = 0;
+  for (uint32_t i = i0; i < i1; i++) s += size[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {        // inclusive scan of the thread sums
+    const uint64_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const uint64_t dbase = chunk_base[k], total = part[1023];
+  const uint64_t b384 = dbase - dbase % 384, off = dbase - b384;
+  const uint64_t need_dst = off + total + 16;
+  const uint64_t need_data = tpz::slot_base(off + total, m) + 128;
+  const uint64_t need_ends = 2 * (tpz::entry_base(off + total, m) + 16);
+  const bool over = need_dst > cap_dst || need_data > cap_data || need_ends > cap_ends;
+  uint64_t run = part[t] - s;
+  for (uint32_t i = i0; i < i1; i++) {
+    gext[i] = dbase + run;
+    lext[i] = over ? 0 : off + run;
+    run += size[i];
+  }
+  if (t == 0) {
+    gext[m] = dbase + total;
+    lext[m] = over ? 0 : off + total;
+    chunk_base[k + 1] = dbase + total;
+    meta->dbase = dbase;
+    meta->dbase384 = b384;
+    meta->total = total;
+    meta->need_dst = need_dst;
+    meta->need_data = need_data;
+    meta->need_ends = need_ends;
+    meta->overflow = over ? 1u : 0u;
+  }
+}
+
+// A block whose codec step failed reports the codec's status (its stub decodes as BAD_TAG).
+__global__ void codec_status_kernel(const uint8_t* cstat, uint8_t* status, uint32_t* count,
+                                    uint32_t m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m && cstat[i] != TPZ_BLOCK_OK) {
+    status[i] = cstat[i];
+    count[i] = 0;
+  }
+}
+
 }  // namespace
+
+// The streams and buffers of one caller, kept by the context between calls.
+struct TpzHostPipe {
+  hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+  Slot slot[kSlots];
+  Buf d_chunk_base;
+  ~TpzHostPipe() {
+    for (hipStream_t q : {up, comp, down})
+      if (q) (void)hipStreamDestroy(q);
+  }
+};
+
+void tpz_internal_pipe_destroy(void* p) { delete static_cast<TpzHostPipe*>(p); }
+
+// Block i's length after the codec step, bounded from its header (tpz_host_decoded_bound).
+static uint64_t decoded_bound(const uint8_t* b, uint64_t len) {
+  if (len == 0) return 0;
+  const uint8_t tag = b[len - 1];
+  if (tag == 2) {                                 // snappy: the varint preamble (+ tag byte)
+    uint64_t v = 0;
+    for (uint32_t i = 0, sh = 0; i < 5 && i + 1 < len; i++, sh += 7) {
+      v |= (uint64_t)(b[i] & 0x7F) << sh;
+      if (!(b[i] & 0x80)) return v + 1;
+    }
+    return 1;
+  }
+  if (tag == 3) {                                 // lz4: the LE size prefix (+ tag byte)
+    if (len < 5) return 1;
+    const int32_t sz = (int32_t)((uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 |
+                                 (uint32_t)b[3] << 24);
+    return sz > 0 ? (uint64_t)sz + 1 : 1;
+  }
+  return len;
+}
+
+extern "C" tpz_err tpz_host_decoded_bound(const uint8_t* h_src, const uint64_t* h_ext,
+                                          uint32_t n, uint64_t* bound) {
+  if (!h_ext || !bound || (n && !h_src)) return TPZ_ERR_INVALID_ARG;
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (h_ext[i + 1] < h_ext[i]) return TPZ_ERR_INVALID_ARG;
+    s += decoded_bound(h_src + h_ext[i], h_ext[i + 1] - h_ext[i]);
+  }
+  *bound = s;
+  return TPZ_SUCCESS;
+}
 
 extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
                                           const uint64_t* h_ext, uint32_t n,
@@ -110,10 +241,20 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     if (h_ext[i + 1] < h_ext[i]) return TPZ_ERR_INVALID_ARG;
   o->h_first[0] = 0;
   *o->h_spill_used = 0;
+  // a snappy / lz4 block anywhere: the decoded extents differ from h_ext for the whole batch
+  bool codec = false;
+  for (uint32_t i = 0; i < n && !codec; i++)
+    codec = h_ext[i + 1] > h_ext[i] && (h_src[h_ext[i + 1] - 1] == 2 || h_src[h_ext[i + 1] - 1] == 3);
+  if (codec && !o->h_dext) return TPZ_ERR_INVALID_ARG;
+  if (o->h_dext && !codec)
+    for (uint32_t i = 0; i <= n; i++) o->h_dext[i] = h_ext[i];
   if (n == 0) return TPZ_SUCCESS;
+  const uint64_t src_bytes = h_ext[n];
+  const uint64_t data_cap = o->data_cap ? o->data_cap : tpz_data_capacity(src_bytes, n);
+  if (!codec && data_cap < tpz_data_capacity(src_bytes, n)) return TPZ_ERR_INVALID_ARG;
   PIPE_HIP(hipSetDevice(tpz_internal_device(ctx)));
   const uint32_t cb = chunk_blocks ? chunk_blocks : 8192u;
-  const uint64_t src_bytes = h_ext[n];
+  const uint32_t n_chunks = (n + cb - 1) / cb;
 
   // the largest chunk's byte span (from its 384-aligned base)
   uint64_t max_span = 0;
@@ -123,37 +264,45 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   }
   Pin pin_src, pin_data, pin_ends, pin_spill;
   pin_src.pin(h_src + h_ext[0], h_ext[n] - h_ext[0]);
-  pin_data.pin(o->h_data, tpz_data_capacity(src_bytes, n));
+  pin_data.pin(o->h_data, data_cap);
   pin_ends.pin(o->h_ends, o->ends_cap * 4);
   pin_spill.pin(o->h_spill, o->spill_cap);
 
-  struct Streams {
-    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
-    ~Streams() {
-      for (hipStream_t q : {up, comp, down})
-        if (q) (void)hipStreamDestroy(q);
-    }
-  } st;
-  PIPE_HIP(hipStreamCreateWithFlags(&st.up, hipStreamNonBlocking));
-  PIPE_HIP(hipStreamCreateWithFlags(&st.comp, hipStreamNonBlocking));
-  PIPE_HIP(hipStreamCreateWithFlags(&st.down, hipStreamNonBlocking));
-  constexpr int kSlots = 3;
-  Slot slot[kSlots];
-  for (Slot& S : slot) {
-    for (hipEvent_t* e : {&S.ev, &S.ev_up, &S.ev_pack, &S.ev_down})
-      PIPE_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  // a pipeline of the context's pool (or a new one, returned to the pool at the end)
+  TpzHostPipe* P = static_cast<TpzHostPipe*>(tpz_internal_pipe_acquire(ctx));
+  const bool fresh = P == nullptr;
+  if (fresh) P = new TpzHostPipe();
+  struct Release {
+    tpz_ctx* c;
+    TpzHostPipe* p;
+    bool fresh;
+    ~Release() { tpz_internal_pipe_release(c, p, fresh); }
+  } release{ctx, P, fresh};
+  if (fresh) {
+    PIPE_HIP(hipStreamCreateWithFlags(&P->up, hipStreamNonBlocking));
+    PIPE_HIP(hipStreamCreateWithFlags(&P->comp, hipStreamNonBlocking));
+    PIPE_HIP(hipStreamCreateWithFlags(&P->down, hipStreamNonBlocking));
+    for (Slot& S : P->slot)
+      for (hipEvent_t* e : {&S.ev, &S.ev_up, &S.ev_pack, &S.ev_down})
+        PIPE_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  Slot* slot = P->slot;
+  for (Slot& S : P->slot) S.used = false;
+  // decoded bytes per chunk, first guess: compressed spans expand by up to ~2x in practice
+  const uint64_t dst_guess = codec ? 2 * max_span + (64u << 10) : max_span;
+  for (Slot& S : P->slot) {
     const uint64_t m = std::min<uint64_t>(cb, n);
     PIPE_HIP(S.d_src.ensure(max_span + 16));
     PIPE_HIP(S.d_ext.ensure((m + 1) * 8));
-    PIPE_HIP(S.d_data.ensure(tpz_data_capacity(max_span, m)));
-    PIPE_HIP(S.d_ends.ensure(2 * tpz_entry_capacity(max_span, m) * 4));
+    PIPE_HIP(S.d_data.ensure(tpz_data_capacity(dst_guess, m)));
+    PIPE_HIP(S.d_ends.ensure(2 * tpz_entry_capacity(dst_guess, m) * 4));
     PIPE_HIP(S.d_count.ensure(m * 4));
     PIPE_HIP(S.d_status.ensure(m));
     PIPE_HIP(S.d_crc.ensure(m * 4));
     PIPE_HIP(S.d_spill_off.ensure(m * 8));
     PIPE_HIP(S.d_used.ensure(8));
     PIPE_HIP(S.d_first.ensure((m + 1) * 8));
-    PIPE_HIP(S.d_dense.ensure(2 * tpz_entry_capacity(max_span, m) * 4));
+    PIPE_HIP(S.d_dense.ensure(2 * tpz_entry_capacity(dst_guess, m) * 4));
     PIPE_HIP(S.h_ext.ensure((m + 1) * 8));
     PIPE_HIP(S.h_first.ensure((m + 1) * 8));
     PIPE_HIP(S.h_count.ensure(m * 4));
@@ -161,9 +310,23 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     PIPE_HIP(S.h_crc.ensure(m * 4));
     PIPE_HIP(S.h_spill_off.ensure(m * 8));
     PIPE_HIP(S.h_used.ensure(8));
+    if (codec) {
+      PIPE_HIP(S.d_size.ensure(m * 8));
+      PIPE_HIP(S.d_dext.ensure((m + 1) * 8));
+      PIPE_HIP(S.d_gext.ensure((m + 1) * 8));
+      PIPE_HIP(S.d_dst.ensure(dst_guess + 16));
+      PIPE_HIP(S.d_cstat.ensure(m));
+      PIPE_HIP(S.d_meta.ensure(sizeof(ChunkMeta)));
+      PIPE_HIP(S.h_gext.ensure((m + 1) * 8));
+      PIPE_HIP(S.h_meta.ensure(sizeof(ChunkMeta)));
+    }
+  }
+  if (codec) {
+    PIPE_HIP(P->d_chunk_base.ensure((n_chunks + 1) * 8));
+    PIPE_HIP(hipMemsetAsync(P->d_chunk_base.p, 0, 8, P->comp));
   }
 
-  // upload + decode + entry prefix + metadata download of the chunk in S (lo/hi/base set)
+  // codec step + decode + entry prefix + metadata download of the chunk in S (lo/hi/base set)
   auto decode_chunk = [&](Slot& S) -> tpz_err {
     const uint32_t m = S.hi - S.lo;
     const uint64_t span = h_ext[S.hi] - S.base;
@@ -177,74 +340,126 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     cols.spill_cap = S.d_spill.n;
     cols.d_spill_off = S.d_spill_off.as<uint64_t>();
     cols.d_spill_used = S.d_used.as<uint64_t>();
-    const tpz_batch b{S.d_src.as<uint8_t>(), S.d_ext.as<uint64_t>(), m, span};
-    PIPE_HIP(hipStreamWaitEvent(st.comp, S.ev_up, 0));
-    tpz_err r = tpz_decode_blocks(ctx, &b, &cols, st.comp);
+    const tpz_batch bc{S.d_src.as<uint8_t>(), S.d_ext.as<uint64_t>(), m, span};
+    PIPE_HIP(hipStreamWaitEvent(P->comp, S.ev_up, 0));
+    tpz_batch bd = bc;
+    if (codec) {
+      tpz_err r = tpz_decompressed_sizes(ctx, &bc, S.d_size.as<uint64_t>(), P->comp);
+      if (r != TPZ_SUCCESS) return r;
+      hipLaunchKernelGGL(chunk_extents_kernel, dim3(1), dim3(1024), 0, P->comp,
+                         S.d_size.as<uint64_t>(), m, P->d_chunk_base.as<uint64_t>(), S.k,
+                         (uint64_t)S.d_dst.n, (uint64_t)S.d_data.n, (uint64_t)(S.d_ends.n / 4),
+                         S.d_gext.as<uint64_t>(), S.d_dext.as<uint64_t>(),
+                         S.d_meta.as<ChunkMeta>());
+      PIPE_HIP(hipGetLastError());
+      r = tpz_decompress_blocks(ctx, &bc, S.d_dst.as<uint8_t>(), S.d_dext.as<uint64_t>(),
+                                S.d_cstat.as<uint8_t>(), P->comp);
+      if (r != TPZ_SUCCESS) return r;
+      // the decode reads the decoded chunk; its descriptors end at the buffer's capacity
+      bd = tpz_batch{S.d_dst.as<uint8_t>(), S.d_dext.as<uint64_t>(), m, (uint64_t)S.d_dst.n - 16};
+    }
+    tpz_err r = tpz_decode_blocks(ctx, &bd, &cols, P->comp);
     if (r != TPZ_SUCCESS) return r;
-    tpz::launch_count_prefix(cols.d_count, cols.d_status, m, S.d_first.as<uint64_t>(), st.comp);
+    if (codec) {
+      hipLaunchKernelGGL(codec_status_kernel, dim3((m + 255) / 256), dim3(256), 0, P->comp,
+                         S.d_cstat.as<uint8_t>(), cols.d_status, cols.d_count, m);
+      PIPE_HIP(hipGetLastError());
+    }
+    tpz::launch_count_prefix(cols.d_count, cols.d_status, m, S.d_first.as<uint64_t>(), P->comp);
     PIPE_HIP(hipGetLastError());
-    PIPE_HIP(hipMemcpyAsync(S.h_first.p, S.d_first.p, (m + 1) * 8, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipMemcpyAsync(S.h_count.p, S.d_count.p, m * 4, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipMemcpyAsync(S.h_status.p, S.d_status.p, m, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipMemcpyAsync(S.h_crc.p, S.d_crc.p, m * 4, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipMemcpyAsync(S.h_spill_off.p, S.d_spill_off.p, m * 8, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipMemcpyAsync(S.h_used.p, S.d_used.p, 8, hipMemcpyDeviceToHost, st.comp));
-    PIPE_HIP(hipEventRecord(S.ev, st.comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_first.p, S.d_first.p, (m + 1) * 8, hipMemcpyDeviceToHost, P->comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_count.p, S.d_count.p, m * 4, hipMemcpyDeviceToHost, P->comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_status.p, S.d_status.p, m, hipMemcpyDeviceToHost, P->comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_crc.p, S.d_crc.p, m * 4, hipMemcpyDeviceToHost, P->comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_spill_off.p, S.d_spill_off.p, m * 8, hipMemcpyDeviceToHost, P->comp));
+    PIPE_HIP(hipMemcpyAsync(S.h_used.p, S.d_used.p, 8, hipMemcpyDeviceToHost, P->comp));
+    if (codec) {
+      PIPE_HIP(hipMemcpyAsync(S.h_gext.p, S.d_gext.p, (m + 1) * 8, hipMemcpyDeviceToHost, P->comp));
+      PIPE_HIP(hipMemcpyAsync(S.h_meta.p, S.d_meta.p, sizeof(ChunkMeta), hipMemcpyDeviceToHost, P->comp));
+    }
+    PIPE_HIP(hipEventRecord(S.ev, P->comp));
     return TPZ_SUCCESS;
   };
 
-  auto issue = [&](Slot& S, uint32_t lo) -> tpz_err {
+  auto issue = [&](Slot& S, uint32_t k) -> tpz_err {
     if (S.used) {
       // the slot's previous chunk: its downloads must be done before the upload overwrites the
       // device buffers (a stream wait), and its extents upload before h_ext is rewritten (long
       // done; its metadata was consumed by finish())
-      PIPE_HIP(hipStreamWaitEvent(st.up, S.ev_down, 0));
+      PIPE_HIP(hipStreamWaitEvent(P->up, S.ev_down, 0));
       PIPE_HIP(hipEventSynchronize(S.ev_up));
     }
     S.used = true;
-    S.lo = lo;
-    S.hi = std::min(n, lo + cb);
-    S.base = h_ext[lo] - h_ext[lo] % 384;
+    S.k = k;
+    S.lo = k * cb;
+    S.hi = std::min(n, S.lo + cb);
+    S.base = h_ext[S.lo] - h_ext[S.lo] % 384;
     uint64_t* e = S.h_ext.as<uint64_t>();
     for (uint32_t i = S.lo; i <= S.hi; i++) e[i - S.lo] = h_ext[i] - S.base;
-    const uint64_t off = h_ext[lo] - S.base;
-    PIPE_HIP(hipMemcpyAsync(S.d_src.as<uint8_t>() + off, h_src + h_ext[lo], h_ext[S.hi] - h_ext[lo],
-                            hipMemcpyHostToDevice, st.up));
+    const uint64_t off = h_ext[S.lo] - S.base;
+    PIPE_HIP(hipMemcpyAsync(S.d_src.as<uint8_t>() + off, h_src + h_ext[S.lo],
+                            h_ext[S.hi] - h_ext[S.lo], hipMemcpyHostToDevice, P->up));
     PIPE_HIP(hipMemcpyAsync(S.d_ext.p, S.h_ext.p, (S.hi - S.lo + 1) * 8, hipMemcpyHostToDevice,
-                            st.up));
-    PIPE_HIP(hipEventRecord(S.ev_up, st.up));
+                            P->up));
+    PIPE_HIP(hipEventRecord(S.ev_up, P->up));
     return decode_chunk(S);
   };
 
   uint64_t g_first = 0, g_spill = 0;
-  bool short_ends = false, short_spill = false;
+  bool short_ends = false, short_spill = false, short_data = false;
   auto finish = [&](Slot& S) -> tpz_err {
     PIPE_HIP(hipEventSynchronize(S.ev));
     const uint32_t m = S.hi - S.lo;
-    uint64_t used = *S.h_used.as<uint64_t>();
-    if (used > S.d_spill.n) {                 // the spill arena overflowed: grow, decode again
-      PIPE_HIP(hipStreamSynchronize(st.comp));
-      PIPE_HIP(S.d_spill.ensure(used + (used >> 2)));
+    for (int redo = 0; redo < 4; redo++) {
+      bool again = false;
+      if (codec) {
+        const ChunkMeta& cm = *S.h_meta.as<ChunkMeta>();
+        if (cm.overflow) {                      // the chunk's codec / decode buffers: grow, redo
+          PIPE_HIP(hipStreamSynchronize(P->comp));
+          PIPE_HIP(hipStreamSynchronize(P->down));
+          PIPE_HIP(S.d_dst.ensure(cm.need_dst + (cm.need_dst >> 2)));
+          PIPE_HIP(S.d_data.ensure(cm.need_data + (cm.need_data >> 2)));
+          PIPE_HIP(S.d_ends.ensure(4 * (cm.need_ends + (cm.need_ends >> 2))));
+          PIPE_HIP(S.d_dense.ensure(4 * (cm.need_ends + (cm.need_ends >> 2))));
+          again = true;
+        }
+      }
+      const uint64_t used = *S.h_used.as<uint64_t>();
+      if (!again && used > S.d_spill.n) {     // the spill arena overflowed: grow, decode again
+        PIPE_HIP(hipStreamSynchronize(P->comp));
+        PIPE_HIP(S.d_spill.ensure(used + (used >> 2)));
+        again = true;
+      }
+      if (!again) break;
       tpz_err r = decode_chunk(S);
       if (r != TPZ_SUCCESS) return r;
       PIPE_HIP(hipEventSynchronize(S.ev));
-      used = *S.h_used.as<uint64_t>();
     }
+    const uint64_t used = *S.h_used.as<uint64_t>();
     const uint64_t* first = S.h_first.as<uint64_t>();
     const uint64_t total = first[m];
-    const uint64_t span = h_ext[S.hi] - S.base;
+    // the chunk's extents as the decode saw them: host bytes, or decoded bytes
+    const uint64_t* gx = codec ? S.h_gext.as<uint64_t>() : nullptr;
+    const uint64_t e_lo = codec ? gx[0] : h_ext[S.lo], e_hi = codec ? gx[m] : h_ext[S.hi];
+    const uint64_t dbase = codec ? S.h_meta.as<ChunkMeta>()->dbase384 : S.base;
+    if (codec)
+      for (uint32_t i = 0; i <= m; i++) o->h_dext[S.lo + i] = gx[i];
     // the chunk's own slots, into the batch's slotted layout
-    const uint64_t d0 = tpz_slot_base(h_ext[S.lo] - S.base, 0);
-    const uint64_t d1 = tpz_slot_base(span, m);
-    const uint64_t h0 = tpz_slot_base(h_ext[S.lo], S.lo);
-    PIPE_HIP(hipStreamWaitEvent(st.down, S.ev, 0));
-    PIPE_HIP(hipMemcpyAsync(o->h_data + h0, S.d_data.as<uint8_t>() + d0, d1 - d0,
-                            hipMemcpyDeviceToHost, st.down));
+    const uint64_t d0 = tpz_slot_base(e_lo - dbase, 0);
+    const uint64_t d1 = tpz_slot_base(e_hi - dbase, m);
+    const uint64_t h0 = tpz_slot_base(e_lo, S.lo);
+    PIPE_HIP(hipStreamWaitEvent(P->down, S.ev, 0));
+    if (h0 + (d1 - d0) <= data_cap) {
+      PIPE_HIP(hipMemcpyAsync(o->h_data + h0, S.d_data.as<uint8_t>() + d0, d1 - d0,
+                              hipMemcpyDeviceToHost, P->down));
+    } else {
+      short_data = true;
+    }
     // the used entry ends, packed
     if (2 * (g_first + total) <= o->ends_cap) {
       if (2 * total * 4 > S.d_dense.n) {      // only spilled blocks can exceed the slot bound
-        PIPE_HIP(hipStreamSynchronize(st.comp));
-        PIPE_HIP(hipStreamSynchronize(st.down));
+        PIPE_HIP(hipStreamSynchronize(P->comp));
+        PIPE_HIP(hipStreamSynchronize(P->down));
         PIPE_HIP(S.d_dense.ensure(2 * total * 4));
       }
       tpz_columns cols{};
@@ -253,15 +468,17 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       cols.d_status = S.d_status.as<uint8_t>();
       cols.d_spill = S.d_spill.n ? S.d_spill.as<uint8_t>() : nullptr;
       cols.d_spill_off = S.d_spill_off.as<uint64_t>();
-      const tpz_batch b{S.d_src.as<uint8_t>(), S.d_ext.as<uint64_t>(), m, span};
+      const tpz_batch b{codec ? S.d_dst.as<uint8_t>() : S.d_src.as<uint8_t>(),
+                        codec ? S.d_dext.as<uint64_t>() : S.d_ext.as<uint64_t>(), m,
+                        codec ? (uint64_t)S.d_dst.n - 16 : h_ext[S.hi] - S.base};
       tpz_err r = tpz_pack_ends(ctx, &b, &cols, S.d_first.as<uint64_t>(), S.d_dense.as<uint32_t>(),
-                                st.comp);
+                                P->comp);
       if (r != TPZ_SUCCESS) return r;
-      PIPE_HIP(hipEventRecord(S.ev_pack, st.comp));
-      PIPE_HIP(hipStreamWaitEvent(st.down, S.ev_pack, 0));
+      PIPE_HIP(hipEventRecord(S.ev_pack, P->comp));
+      PIPE_HIP(hipStreamWaitEvent(P->down, S.ev_pack, 0));
       if (total)
         PIPE_HIP(hipMemcpyAsync(o->h_ends + 2 * g_first, S.d_dense.p, 2 * total * 4,
-                                hipMemcpyDeviceToHost, st.down));
+                                hipMemcpyDeviceToHost, P->down));
     } else {
       short_ends = true;
     }
@@ -269,7 +486,7 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     if (g_spill + used <= o->spill_cap) {
       if (used)
         PIPE_HIP(hipMemcpyAsync(o->h_spill + g_spill, S.d_spill.p, used, hipMemcpyDeviceToHost,
-                                st.down));
+                                P->down));
     } else {
       short_spill = true;
     }
@@ -287,16 +504,15 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     g_spill += used;
     o->h_first[S.hi] = g_first;
     *o->h_spill_used = g_spill;
-    PIPE_HIP(hipEventRecord(S.ev_down, st.down));
+    PIPE_HIP(hipEventRecord(S.ev_down, P->down));
     return TPZ_SUCCESS;
   };
 
   // chunk k is issued, then chunk k-1 finished: the host waits for k-1's metadata while k
   // uploads and k-2 downloads
-  const uint32_t n_chunks = (n + cb - 1) / cb;
   for (uint32_t k = 0; k <= n_chunks; k++) {
     if (k < n_chunks) {
-      tpz_err r = issue(slot[k % kSlots], k * cb);
+      tpz_err r = issue(slot[k % kSlots], k);
       if (r != TPZ_SUCCESS) return r;
     }
     if (k >= 1) {
@@ -304,8 +520,8 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       if (r != TPZ_SUCCESS) return r;
     }
   }
-  PIPE_HIP(hipStreamSynchronize(st.up));
-  PIPE_HIP(hipStreamSynchronize(st.comp));
-  PIPE_HIP(hipStreamSynchronize(st.down));
-  return (short_ends || short_spill) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
+  PIPE_HIP(hipStreamSynchronize(P->up));
+  PIPE_HIP(hipStreamSynchronize(P->comp));
+  PIPE_HIP(hipStreamSynchronize(P->down));
+  return (short_ends || short_spill || short_data) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
 }

@@ -9,6 +9,13 @@
 // Context accessors for the host pipeline (tpz_host_pipeline.cpp; defined in tpz_api.cpp).
 int tpz_internal_device(tpz_ctx* c);
 tpz_err tpz_internal_hip_fail(hipError_t e, const char* what);
+// The context's pool of host pipelines (streams + buffers of tpz_decode_blocks_host, reused
+// across calls; one per concurrent caller): acquire returns a free one or nullptr; release puts
+// one back (fresh = created by this call: the context takes ownership); the context destroys
+// them with tpz_internal_pipe_destroy (tpz_host_pipeline.cpp).
+void* tpz_internal_pipe_acquire(tpz_ctx* c);
+void tpz_internal_pipe_release(tpz_ctx* c, void* pipe, bool fresh);
+void tpz_internal_pipe_destroy(void* pipe);
 
 namespace tpz {
 
@@ -86,7 +93,13 @@ struct LaunchArgs {
   uint32_t* bw_list;      // workspace: n_blocks entries (blocks for the bigwave kernel)
   uint32_t* bw_count;     // workspace: one u32, zeroed before the launch
   const uint32_t* rep;    // replicated slice-by-4 tables (the bigwave kernel's CRC)
+  const uint64_t* efirst; // exact ends layout (tpz_columns.d_entry_first) or null
 };
+// Pair index of block b's first {kend, vend}: the exact layout's d_entry_first[b], or the
+// slotted tpz_entry_base.
+__host__ __device__ inline uint64_t ends_base(const uint64_t* efirst, uint64_t ext_b, uint64_t b) {
+  return efirst ? efirst[b] : entry_base(ext_b, b);
+}
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
 
@@ -109,6 +122,7 @@ struct BigWaveLaunch {
   uint32_t* big_list;
   uint32_t* big_count;
   uint32_t grid;
+  const uint64_t* efirst;
 };
 void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream);
 
@@ -165,6 +179,7 @@ struct SeekLaunch {
   uint32_t* out_entry;
   uint8_t* out_status;
   uint8_t* out_valid;
+  const uint64_t* efirst;
 };
 void launch_seek(const SeekLaunch& a, hipStream_t stream);
 
@@ -202,8 +217,14 @@ struct PackLaunch {
   const uint64_t* spill_off;
   const uint64_t* first;
   uint32_t* dense;
+  const uint64_t* efirst;
 };
 void launch_pack_ends(const PackLaunch& a, hipStream_t stream);
+// d_first[i] = sum of the header n of blocks < i (tpz_entry_first); `part` = workspace of
+// entry_first_parts(n_blocks) u64.
+uint64_t entry_first_parts(uint32_t n_blocks);
+void launch_entry_first(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
+                        uint32_t n_blocks, uint64_t* first, uint64_t* part, hipStream_t stream);
 // first[i] = exclusive prefix of count over decoded (OK / OK_SPILLED) blocks, first[n] = total.
 void launch_count_prefix(const uint32_t* count, const uint8_t* status, uint32_t n,
                          uint64_t* first, hipStream_t stream);

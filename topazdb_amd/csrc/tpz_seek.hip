@@ -62,6 +62,7 @@ struct SeekParams {
   u32* out_entry;
   uint8_t* out_status;
   uint8_t* out_valid;
+  const u64* efirst;        // exact ends layout, or null: slotted
 };
 
 // A decoded block's ends and stream: its slot, or its spill record (include/tpz_gpu.h); the
@@ -84,7 +85,7 @@ __device__ __forceinline__ BlockView block_view(const SeekParams& p, u32 b, u32 
     return BlockView{e, r + spill_stream(n), cls};
   }
   const u64 e0 = p.ext[b];
-  return BlockView{p.ends + 2 * entry_base(e0, b), p.data + slot_base(e0, b), nullptr};
+  return BlockView{p.ends + 2 * ends_base(p.efirst, e0, b), p.data + slot_base(e0, b), nullptr};
 }
 // Entry j's key: its bytes and length.
 __device__ __forceinline__ const uint8_t* entry_key(const BlockView& v, u32 j, u64& len) {
@@ -500,7 +501,7 @@ __global__ __launch_bounds__(256) void pack_ends_kernel(PackLaunch a, uint2* den
     const bool ok = block_decoded(st);
     const uint2* src = block_in_spill(st)
                            ? reinterpret_cast<const uint2*>(a.spill + a.spill_off[b])
-                           : reinterpret_cast<const uint2*>(a.ends) + entry_base(a.ext[b], b);
+                           : reinterpret_cast<const uint2*>(a.ends) + ends_base(a.efirst, a.ext[b], b);
     for (u64 j = lane; j < c; j += 64) dense[f + j] = ok ? src[j] : make_uint2(0, 0);
   }
 }
@@ -531,7 +532,107 @@ __global__ __launch_bounds__(1024) void count_prefix_kernel(const u32* count, co
   if (t == 1023) first[n] = part[1023];
 }
 
+// The exact ends layout's reservation for block b: its header n when the decode parses it in
+// place and writes its pairs to d_ends (uncompressed tag, len >= 7 + 2n: block.rs:49-59 pass;
+// 6n <= len: the slot holds it), else 0 (tpz_gpu.h, tpz_entry_first).
+__device__ __forceinline__ u32 exact_entries(const uint8_t* src, const u64* ext, u64 src_bytes,
+                                             u32 b) {
+  const u64 e0 = ext[b], e1 = ext[b + 1];
+  if (e1 < e0 || e1 > src_bytes || e1 - e0 < 7) return 0;
+  const u32 len = (u32)min(e1 - e0, (u64)0xffffffffu);
+  if (src[e1 - 1] != 1) return 0;
+  const u32 n = ((u32)src[e0] << 8) | src[e0 + 1];
+  return (len >= 7 + 2 * n && 6 * n <= len) ? n : 0;
+}
+
+constexpr u32 kEfPer = 4;                 // blocks per thread
+constexpr u32 kEfWg = 256 * kEfPer;       // blocks per workgroup
+
+// Inclusive scan over the 256 threads of a workgroup (a shuffle prefix per wave, then
+// the 4 wave totals).
+__device__ __forceinline__ u64 wg_inclusive(u64 v, u64* wsum) {
+  const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (u32 o = 1; o < 64; o <<= 1) {
+    const u64 t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  for (u32 i = 0; i < w; i++) v += wsum[i];
+  return v;
+}
+
+__global__ __launch_bounds__(256) void entry_first_count(const uint8_t* src, const u64* ext,
+                                                         u64 src_bytes, u32 n, u64* part) {
+  __shared__ u64 wsum[4];
+  const u64 b0 = (u64)blockIdx.x * kEfWg + threadIdx.x * kEfPer;
+  u64 s = 0;
+  for (u32 j = 0; j < kEfPer; j++)
+    if (b0 + j < n) s += exact_entries(src, ext, src_bytes, (u32)(b0 + j));
+  s = wg_inclusive(s, wsum);
+  if (threadIdx.x == 255) part[blockIdx.x] = s;
+}
+
+// Exclusive scan of the workgroup totals in place, total at part[n_parts] (one workgroup).
+__global__ __launch_bounds__(1024) void entry_first_parts_scan(u64* part, u32 n_parts) {
+  __shared__ u64 acc[1024];
+  const u32 t = threadIdx.x, per = (n_parts + 1023) / 1024;
+  const u32 lo = min(n_parts, t * per), hi = min(n_parts, lo + per);
+  u64 s = 0;
+  for (u32 i = lo; i < hi; i++) s += part[i];
+  acc[t] = s;
+  __syncthreads();
+  for (u32 o = 1; o < 1024; o <<= 1) {
+    const u64 v = t >= o ? acc[t - o] : 0;
+    __syncthreads();
+    acc[t] += v;
+    __syncthreads();
+  }
+  u64 run = t ? acc[t - 1] : 0;
+  for (u32 i = lo; i < hi; i++) {
+    const u64 x = part[i];
+    part[i] = run;
+    run += x;
+  }
+  if (t == 1023) part[n_parts] = acc[1023];
+}
+
+__global__ __launch_bounds__(256) void entry_first_write(const uint8_t* src, const u64* ext,
+                                                         u64 src_bytes, u32 n, const u64* part,
+                                                         u32 n_parts, u64* first) {
+  __shared__ u64 wsum[4];
+  const u64 b0 = (u64)blockIdx.x * kEfWg + threadIdx.x * kEfPer;
+  u32 c[kEfPer];
+  u64 s = 0;
+  for (u32 j = 0; j < kEfPer; j++) {
+    c[j] = b0 + j < n ? exact_entries(src, ext, src_bytes, (u32)(b0 + j)) : 0;
+    s += c[j];
+  }
+  u64 run = wg_inclusive(s, wsum) - s + part[blockIdx.x];
+  for (u32 j = 0; j < kEfPer; j++) {
+    if (b0 + j < n) first[b0 + j] = run;
+    run += c[j];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) first[n] = part[n_parts];
+}
+
 }  // namespace
+
+uint64_t entry_first_parts(uint32_t n_blocks) { return (n_blocks + kEfWg - 1) / kEfWg + 1; }
+
+void launch_entry_first(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n_blocks,
+                        u64* first, u64* part, hipStream_t stream) {
+  if (n_blocks == 0) {
+    (void)hipMemsetAsync(first, 0, 8, stream);
+    return;
+  }
+  const u32 parts = (u32)entry_first_parts(n_blocks) - 1;
+  hipLaunchKernelGGL(entry_first_count, dim3(parts), dim3(256), 0, stream, src, ext, src_bytes,
+                     n_blocks, part);
+  hipLaunchKernelGGL(entry_first_parts_scan, dim3(1), dim3(1024), 0, stream, part, parts);
+  hipLaunchKernelGGL(entry_first_write, dim3(parts), dim3(256), 0, stream, src, ext, src_bytes,
+                     n_blocks, part, parts, first);
+}
 
 void launch_count_prefix(const u32* count, const uint8_t* status, u32 n, u64* first,
                          hipStream_t stream) {
@@ -548,7 +649,7 @@ void launch_pack_ends(const PackLaunch& a, hipStream_t stream) {
 void launch_seek(const SeekLaunch& a, hipStream_t stream) {
   SeekParams p{a.fk, a.fk_pos, a.n_blocks, a.ext, a.data, a.ends, a.count, a.bstatus,
                a.spill, a.spill_off, a.q, a.q_pos, a.n_q, a.out_block, a.out_entry,
-               a.out_status, a.out_valid};
+               a.out_status, a.out_valid, a.efirst};
   hipLaunchKernelGGL(seek_kernel, dim3((a.n_q + 255) / 256), dim3(256), 0, stream, p);
 }
 

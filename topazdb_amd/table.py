@@ -31,7 +31,7 @@ import torch
 from . import _lib
 from ._lib import (BLOCK_BAD_ENTRY, BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY,
                    BLOCK_MALFORMED, BLOCK_OK, ENTRY_BAD_KEY, ENTRY_OK, Context)
-from .batch import DeviceBatch, decode_batch, decompress_batch, verify_files
+from .batch import DeviceBatch, decode_batch, decompress_batch, exact_columns, verify_files
 
 CHECKSUM_SIZE = 4  # src/checksum.rs:4
 SIZEOF_U16 = 2
@@ -144,7 +144,10 @@ class DeviceTable:
     (tpz_seek_keys) and `may_contain` SsTable::may_contain (tpz_bloom_may_contain)."""
 
     def __init__(self, ctx: Context, region: bytes, ext: np.ndarray,
-                 first_keys: list[bytes] | None = None, bloom: bytes | None = None):
+                 first_keys: list[bytes] | None = None, bloom: bytes | None = None,
+                 exact_ends: bool = True):
+        """exact_ends: the resident columns keep 8 bytes of ends per entry (tpz_entry_first)
+        instead of the slotted worst-case reservation."""
         self.ctx = ctx
         dev = torch.device("cuda", ctx.device)
         src = np.frombuffer(region, np.uint8) if region else np.zeros(0, np.uint8)
@@ -157,7 +160,8 @@ class DeviceTable:
             self.codec = st[:nb]
         self.batch = batch
         # complete(): blocks that spilled into a too-small arena are decoded again with room
-        self.cols = decode_batch(ctx, batch).complete()
+        cols = exact_columns(ctx, batch) if exact_ends else None
+        self.cols = decode_batch(ctx, batch, cols).complete()
         # the status a reader of block i sees: the codec's Err wins over the decode of its stub
         self.status = self.cols.status[:max(nb, 1)].clone()
         if self.codec is not None:
@@ -175,7 +179,8 @@ class DeviceTable:
                           self.batch.ext.data_ptr(), self.n_blocks, c.data.data_ptr(),
                           c.ends.data_ptr(), c.count.data_ptr(), self.status.data_ptr(),
                           c.spill.data_ptr() if c.spill is not None else None,
-                          c.spill_off.data_ptr())
+                          c.spill_off.data_ptr(),
+                          c.entry_first.data_ptr() if c.entry_first is not None else None)
 
     def seek_keys(self, keys: list[bytes]) -> dict:
         """SsTableIterator::seek_to_key (src/table/iterator.rs:44-72) for every key: the block
