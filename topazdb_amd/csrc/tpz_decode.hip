@@ -1038,6 +1038,11 @@ struct Params {
 };
 
 // ------------------------------------------------------------------ wave path kernel
+#ifdef TPZ_ABL_ONCHIP
+// diagnostic (timing only): every wave decodes blocks 0..4095 over and over, so loads and stores
+// stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
+constexpr u32 kOnchipMask = 4095;
+#endif
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
@@ -1072,6 +1077,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     // destination registers directly, nothing waits for it until the group is used)
     u64 bb = (u64)b0 + ((u64)g * 64 + lane) * nw;
     bb = bb < p.n_blocks ? bb : p.n_blocks - 1;
+#ifdef TPZ_ABL_ONCHIP
+    bb &= kOnchipMask;   // timing build: the same 4096 blocks over and over (L2/MALL-resident)
+#endif
     gs = p.ext[bb];
     ge = p.ext[bb + 1];
   };
@@ -1156,8 +1164,13 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
     if (fits) {
+#ifdef TPZ_ABL_ONCHIP
+      const u32 bdec = bcur & kOnchipMask;
+#else
+      const u32 bdec = bcur;
+#endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bcur, s, p.out, kshift, S);
+                                                           len64, bdec, s, p.out, kshift, S);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
