@@ -579,7 +579,8 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
     clock) and tpz_encode_blocks (Block::encode + CRC + tag, HIP events). The encoded region
     must equal the shard's blocks byte for byte. Algorithmic bytes: keys + values + kpos/vpos
     (16 B per entry) + first/ext (12 B per block) read, the region written. Not the metric."""
-    from topazdb_amd.encode import DeviceEntries, encode_blocks, plan_blocks
+    from topazdb_amd.encode import (DeviceEntries, encode_blocks, encode_blocks_async, plan_blocks,
+                                    plan_blocks_async)
     keys, kpos, vals, vpos = gen
     etot = int(n_ent.sum())
     nb = len(ext) - 1
@@ -602,13 +603,34 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
+    # the asynchronous plan (no host round trip) and plan + encode as one device-side step
+    afirst, aext, ainfo = plan_blocks_async(ctx, ent, block_size)
+    aout = torch.empty(int(ext[-1]) + 16, dtype=torch.uint8, device=dev)
+    encode_blocks_async(ctx, ent, afirst, aext, ainfo, out=aout)
+    torch.cuda.synchronize(dev)
+    assert int(ainfo[2]) == nb and torch.equal(aout[:int(ext[-1])], out[:int(ext[-1])]), "async encode"
+    e0.record(stream)
+    for _ in range(steps):
+        plan_blocks_async(ctx, ent, block_size)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms_plan_async = e0.elapsed_time(e1) / steps
+    e0.record(stream)
+    for _ in range(steps):
+        afirst, aext, ainfo = plan_blocks_async(ctx, ent, block_size)
+        encode_blocks_async(ctx, ent, afirst, aext, ainfo, out=aout)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms_both = e0.elapsed_time(e1) / steps
     alg = int(kpos[etot] - kpos[0]) + int(vpos[etot] - vpos[0]) + 16 * etot + 12 * nb + int(ext[-1])
     bloom = bloom_build_rate(ctx, ent, stream, dev)
     # the host builder beside it (tpz_build_blocks, one thread: SsTableBuilder's loop restated)
     t0 = time.perf_counter()
     synth.build_blocks(keys, kpos[:etot + 1], vals, vpos[:etot + 1], block_size)
     cpu_s = time.perf_counter() - t0
-    return {"entries": etot, "blocks": nb, "ms_plan": round(ms_plan, 3), "ms_encode": round(ms, 4),
+    return {"entries": etot, "blocks": nb, "ms_plan": round(ms_plan, 3),
+            "ms_plan_async": round(ms_plan_async, 4), "ms_plan_encode_async": round(ms_both, 4),
+            "ms_encode": round(ms, 4),
             "cpu_host_builder_ms_1_thread": round(cpu_s * 1e3, 1),
             "gib_s_encoded": round(int(ext[-1]) / (ms * 1e-3) / GIB, 1),
             "algorithmic_bytes": alg, "achieved_gb_s": round(alg / (ms * 1e-3) / 1e9, 1),

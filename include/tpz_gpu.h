@@ -455,7 +455,19 @@ tpz_err tpz_bloom_build(tpz_ctx* ctx, const uint8_t* d_keys, const uint64_t* d_k
  *     d_ext[n_blocks] bytes; no byte outside the blocks is written) for d_first / d_ext /
  *     n_blocks exactly as tpz_plan_blocks returned them for these entries and block_size.
  *     Asynchronous on `stream`; uses the stream's workspace (like tpz_decode_blocks).
+ *   tpz_plan_blocks_async: tpz_plan_blocks with its results left on the device:
+ *     d_info[0] = the most entries a block starting at any entry would take (>= the longest
+ *     block; the plan's chunk tables are that wide), d_info[1] = the first entry the reference rejects
+ *     (0xFFFFFFFF: none; d_first / d_ext are then meaningless), d_info[2] = n_blocks (4 u32 of
+ *     device memory). No host round trip for block_size <= TPZ_PLAN_ASYNC_MAX_BLOCK (every block
+ *     then holds at most 2048 entries, the transfer tables are sized from that bound); a larger
+ *     block size reads the longest block back once (its plan chunks follow it). tpz_plan_blocks
+ *     is this call plus one read of d_info.
+ *   tpz_encode_blocks_async: tpz_encode_blocks with the block count read on the device from
+ *     tpz_plan_blocks_async's d_info (a plan with a rejected entry encodes nothing). d_out needs
+ *     d_ext[n_blocks] bytes; key_bytes + val_bytes + 13 * n_entries bounds that without reading it.
  * BlockMeta::first_key of block b is entry d_first[b]'s key. */
+#define TPZ_PLAN_ASYNC_MAX_BLOCK 10242u
 typedef struct {
   const uint8_t* d_keys;
   const uint64_t* d_kpos;
@@ -471,6 +483,11 @@ tpz_err tpz_plan_blocks(tpz_ctx* ctx, const tpz_entries* entries, uint32_t block
                         uint64_t* h_bad_entry, void* stream);
 tpz_err tpz_encode_blocks(tpz_ctx* ctx, const tpz_entries* entries, const uint32_t* d_first,
                           const uint64_t* d_ext, uint32_t n_blocks, uint8_t* d_out, void* stream);
+tpz_err tpz_plan_blocks_async(tpz_ctx* ctx, const tpz_entries* entries, uint32_t block_size,
+                              uint32_t* d_first, uint64_t* d_ext, uint32_t* d_info, void* stream);
+tpz_err tpz_encode_blocks_async(tpz_ctx* ctx, const tpz_entries* entries, const uint32_t* d_first,
+                                const uint64_t* d_ext, const uint32_t* d_info, uint8_t* d_out,
+                                void* stream);
 
 /* ---- host write side (inputs for benches and the table facade) ---------------------------
  * SsTableBuilder::add + block_build (src/table/builder.rs:49-85) with BlockBuilder's fill rule

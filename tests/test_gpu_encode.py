@@ -18,7 +18,8 @@ from conftest import GOLDEN
 from test_encode_host import GOLDEN_SSTS, golden_entries, pack, random_kvs
 from topazdb_amd import _lib, synth
 from topazdb_amd.batch import DeviceBatch, decode_batch
-from topazdb_amd.encode import DeviceEntries, EntryError, build_region, encode_blocks, plan_blocks
+from topazdb_amd.encode import (DeviceEntries, EntryError, build_region, encode_blocks, encode_blocks_async,
+                                plan_blocks, plan_blocks_async)
 
 pytestmark = pytest.mark.gpu
 
@@ -121,6 +122,48 @@ def test_no_entries(ctx):
     out = encode_blocks(ctx, ent, first, ext, 0)
     torch.cuda.synchronize()
     assert out.numel() >= 0
+
+
+@pytest.mark.parametrize("block_size,kmax,vmax,n", [
+    (64, 8, 20, 3000), (4096, 40, 400, 5000), (4096, 4, 8, 20000), (10242, 60, 900, 4000),
+    (10243, 60, 900, 4000), (65536, 200, 3000, 3000)])
+def test_async_plan_and_encode(ctx, block_size, kmax, vmax, n):
+    """tpz_plan_blocks_async + tpz_encode_blocks_async (the block count stays on the device)
+    equal the oracle's builder; block sizes on both sides of TPZ_PLAN_ASYNC_MAX_BLOCK."""
+    rng = random.Random(block_size * 7 + n)
+    kvs = [(k, v) for k, v in random_kvs(rng, n, kmax, vmax) if 6 + len(k) + len(v) <= block_size]
+    keys, kpos, vals, vpos = pack(kvs)
+    ent = DeviceEntries(keys, kpos, vals, vpos)
+    first, ext, info = plan_blocks_async(ctx, ent, block_size)
+    out = encode_blocks_async(ctx, ent, first, ext, info)
+    torch.cuda.synchronize()
+    o_region, o_ext, o_first = O.build_blocks(keys, kpos, vals, vpos, block_size)
+    w, bad, nb = info[:3].cpu().numpy().view(np.uint32).tolist()
+    assert bad == 0xFFFFFFFF and nb == len(o_ext) - 1
+    # d_info[0]: the most entries a block starting at any entry takes (>= the longest block)
+    assert int(np.diff(o_first.astype(np.int64)).max()) <= w <= max(1, (block_size - 2) // 5)
+    assert ext[:nb + 1].cpu().numpy().view(np.uint64).tolist() == o_ext.tolist()
+    assert first[:nb + 1].cpu().numpy().tolist() == o_first.astype(np.int64).tolist()
+    assert out[:int(o_ext[-1])].cpu().numpy().tobytes() == o_region.tobytes()
+
+
+def test_async_plan_reports_rejected_entries(ctx):
+    for kvs, bs, bad in [([(b"a", b"1"), (b"", b"x"), (b"c", b"3")], 64, 1),
+                         ([(b"a", b"1")] * 3000 + [(b"b", b"x" * 60)], 64, 3000),
+                         ([(b"a", b"1")] * 9000 + [(b"", b"")] * 3 + [(b"ab", b"c" * 5000)], 4096, 9000),
+                         ([(b"ab", b"c" * 70000)], 65536, 0)]:
+        ent = DeviceEntries(*pack(kvs))
+        first, ext, info = plan_blocks_async(ctx, ent, bs)
+        out = torch.full((4096,), 0x5A, dtype=torch.uint8, device="cuda")
+        encode_blocks_async(ctx, ent, first, ext, info, out=out)     # encodes nothing
+        torch.cuda.synchronize()
+        assert int(info[1].cpu().numpy().view(np.uint32)) == bad
+        assert (out == 0x5A).all()
+    ent = DeviceEntries(*pack([]))
+    first, ext, info = plan_blocks_async(ctx, ent, 4096)
+    torch.cuda.synchronize()
+    assert info[:3].cpu().numpy().view(np.uint32).tolist() == [0, 0xFFFFFFFF, 0]
+    assert int(ext[0]) == 0 and int(first[0]) == 0
 
 
 def test_encode_leaves_bytes_outside_the_blocks_alone(ctx):

@@ -136,6 +136,12 @@ def lib() -> C.CDLL:
         L.tpz_encode_blocks.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_void_p, C.c_void_p,
                                         C.c_uint32, C.c_void_p, C.c_void_p]
         L.tpz_encode_blocks.restype = C.c_int
+        L.tpz_plan_blocks_async.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_uint32, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tpz_plan_blocks_async.restype = C.c_int
+        L.tpz_encode_blocks_async.argtypes = [C.c_void_p, C.POINTER(Entries), C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tpz_encode_blocks_async.restype = C.c_int
         L.tpz_bloom_geometry.argtypes = [C.c_uint64, C.c_double, C.POINTER(C.c_uint64),
                                          C.POINTER(C.c_uint32)]
         L.tpz_bloom_geometry.restype = C.c_int
@@ -319,6 +325,22 @@ class Context:
             return rc, int(bad.value)
         check(rc, "tpz_plan_blocks")
         return rc, int(nb.value)
+
+    def plan_blocks_async_ptrs(self, ent: Entries, block_size: int, d_first: int, d_ext: int,
+                               d_info: int, stream: int = 0) -> None:
+        """tpz_plan_blocks_async: the plan on `stream`, its {widest block start, first bad entry,
+        n_blocks} left in d_info (4 u32 of device memory); no host round trip for block sizes up
+        to TPZ_PLAN_ASYNC_MAX_BLOCK."""
+        check(lib().tpz_plan_blocks_async(self.handle, C.byref(ent), block_size, C.c_void_p(d_first),
+                                          C.c_void_p(d_ext), C.c_void_p(d_info),
+                                          C.c_void_p(stream)), "tpz_plan_blocks_async")
+
+    def encode_blocks_async_ptrs(self, ent: Entries, d_first: int, d_ext: int, d_info: int,
+                                 d_out: int, stream: int = 0) -> None:
+        """tpz_encode_blocks_async: the encode with the block count read from d_info."""
+        check(lib().tpz_encode_blocks_async(self.handle, C.byref(ent), C.c_void_p(d_first),
+                                            C.c_void_p(d_ext), C.c_void_p(d_info), C.c_void_p(d_out),
+                                            C.c_void_p(stream)), "tpz_encode_blocks_async")
 
     def encode_blocks_ptrs(self, ent: Entries, d_first: int, d_ext: int, n_blocks: int,
                            d_out: int, stream: int = 0) -> None:

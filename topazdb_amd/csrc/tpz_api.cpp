@@ -132,6 +132,7 @@ struct tpz_workspace {
   size_t plan1_cap = 0;
   void* d_bloom = nullptr;      // tpz_bloom_build: probe buckets + slice histograms
   size_t bloom_cap = 0;
+  uint32_t* h_info = nullptr;   // pinned: tpz_plan_blocks' read-back of its 16-byte info
 };
 
 struct tpz_ctx {
@@ -155,6 +156,7 @@ void free_workspace(tpz_workspace& w) {
   if (w.d_plan0) (void)hipFree(w.d_plan0);
   if (w.d_plan1) (void)hipFree(w.d_plan1);
   if (w.d_bloom) (void)hipFree(w.d_bloom);
+  if (w.h_info) (void)hipHostFree(w.h_info);
   w = tpz_workspace{};
 }
 
@@ -535,38 +537,28 @@ tpz_err tpz_bloom_may_contain(tpz_ctx* c, const uint8_t* d_filter, uint64_t filt
 }
 
 
-tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, uint32_t* d_first,
-                        uint64_t* d_ext, uint32_t* h_n_blocks, uint64_t* h_bad_entry,
-                        void* stream) {
-  if (!c || !en || !d_first || !d_ext || !h_n_blocks || !h_bad_entry) return TPZ_ERR_INVALID_ARG;
-  *h_bad_entry = UINT64_MAX;
-  *h_n_blocks = 0;
-  if (block_size <= 2 || block_size > 65536 || en->n_entries == 0xFFFFFFFFu)
-    return TPZ_ERR_INVALID_ARG;
-  TPZ_HIP(hipSetDevice(c->device));
+// The block plan on the stream, into info[0..3) = {most entries a block starting at any entry
+// takes (>= the longest block), first entry the
+// reference rejects (~0u: none), block count} (device memory, written by the kernels). With
+// block_size <= kPlanBoundBlock no block holds more than kPlanChunk entries (each is >= 5 bytes), so
+// the transfer tables are sized from that bound and the launch needs no host round trip; larger block
+// sizes read the longest block back once (the chunk length follows it). *h_bad is set, and
+// TPZ_ERR_INVALID_ARG returned, when that round trip finds a rejected entry.
+static tpz_err plan_launch(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, uint32_t* d_first,
+                           uint64_t* d_ext, uint32_t* info, void* stream, uint64_t* h_bad) {
   hipStream_t s = (hipStream_t)stream;
   const uint32_t n = en->n_entries;
-  if (n == 0) {  // SsTableBuilder with no entries: no block, an empty data region
-    TPZ_HIP(hipMemsetAsync(d_first, 0, 4, s));
-    TPZ_HIP(hipMemsetAsync(d_ext, 0, 8, s));
-    TPZ_HIP(hipStreamSynchronize(s));
-    return TPZ_SUCCESS;
-  }
-  if (!en->d_kpos || !en->d_vpos) return TPZ_ERR_INVALID_ARG;
-  // the stream's grow-only plan buffers (one plan per stream at a time: the call is synchronous)
   std::unique_lock<std::mutex> lk(c->mu);
   tpz_workspace& w = c->ws[stream];
   lk.unlock();
-  const size_t nx_words = (size_t)n + n / 2048 + 2;        // nx, then per-workgroup maxima
+  const size_t nwg = ((size_t)n + tpz::kPlanNextPer - 1) / tpz::kPlanNextPer;              // plan_next_kernel workgroups
+  const size_t nx_words = (size_t)n + 2 * nwg + 2;           // nx, per-workgroup maxima and bad
   {
     std::lock_guard<std::mutex> g(c->mu);
     tpz_err r = grow(stream, &w.d_plan0, &w.plan0_cap, (nx_words + 4) * 4);
     if (r != TPZ_SUCCESS) return r;
   }
   uint32_t* nx = static_cast<uint32_t*>(w.d_plan0);
-  uint32_t* info = nx + nx_words;
-  uint32_t h_info[4] = {0u, 0xFFFFFFFFu, 0u, 0u};
-  TPZ_HIP(hipMemcpyAsync(info, h_info, 16, hipMemcpyHostToDevice, s));
   tpz::PlanLaunch a{};
   a.phase = 0;
   a.kpos = en->d_kpos;
@@ -578,16 +570,22 @@ tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, 
   a.first = d_first;
   a.ext = d_ext;
   TPZ_HIP(tpz::launch_plan(a, s));
-  TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
-  TPZ_HIP(hipStreamSynchronize(s));
-  if (h_info[1] != 0xFFFFFFFFu) {
-    *h_bad_entry = h_info[1];
-    return TPZ_ERR_INVALID_ARG;
-  }
-  // chunks of at least w entries keep the transfer tables (K x w) within n entries
   a.phase = 1;
-  a.w = h_info[0];
-  a.chunk = a.w > tpz::kPlanChunk ? a.w : tpz::kPlanChunk;
+  const uint32_t span = (block_size - 2) / 5 ? (block_size - 2) / 5 : 1u;   // entries per block <= span
+  if (span <= tpz::kPlanChunk) {
+    a.w = span;
+    a.chunk = tpz::kPlanChunk;
+  } else {
+    uint32_t h_info[4];
+    TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
+    TPZ_HIP(hipStreamSynchronize(s));
+    if (h_info[1] != 0xFFFFFFFFu) {
+      *h_bad = h_info[1];
+      return TPZ_ERR_INVALID_ARG;
+    }
+    a.w = h_info[0];
+    a.chunk = a.w > tpz::kPlanChunk ? a.w : tpz::kPlanChunk;
+  }
   const uint64_t K = (n + (uint64_t)a.chunk - 1) / a.chunk;
   {
     std::lock_guard<std::mutex> g(c->mu);
@@ -599,16 +597,87 @@ tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, 
   a.cnt = reinterpret_cast<uint32_t*>(a.tab_b + K * a.w);
   a.n_blocks = info + 2;
   TPZ_HIP(tpz::launch_plan(a, s));
-  TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));
+  return TPZ_SUCCESS;
+}
+
+static bool plan_args_ok(const tpz_entries* en, uint32_t block_size) {
+  return block_size > 2 && block_size <= 65536 && en->n_entries != 0xFFFFFFFFu &&
+         (en->n_entries == 0 || (en->d_kpos && en->d_vpos));
+}
+
+tpz_err tpz_plan_blocks(tpz_ctx* c, const tpz_entries* en, uint32_t block_size, uint32_t* d_first,
+                        uint64_t* d_ext, uint32_t* h_n_blocks, uint64_t* h_bad_entry,
+                        void* stream) {
+  if (!c || !en || !d_first || !d_ext || !h_n_blocks || !h_bad_entry) return TPZ_ERR_INVALID_ARG;
+  *h_bad_entry = UINT64_MAX;
+  *h_n_blocks = 0;
+  if (!plan_args_ok(en, block_size)) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (en->n_entries == 0) {  // SsTableBuilder with no entries: no block, an empty data region
+    TPZ_HIP(hipMemsetAsync(d_first, 0, 4, s));
+    TPZ_HIP(hipMemsetAsync(d_ext, 0, 8, s));
+    TPZ_HIP(hipStreamSynchronize(s));
+    return TPZ_SUCCESS;
+  }
+  // the stream's grow-only plan buffers; info sits after nx (one plan per stream at a time: the
+  // call returns once the plan is done)
+  tpz_err r = TPZ_SUCCESS;
+  uint32_t* info = nullptr;
+  uint32_t* h_info = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_workspace& w = c->ws[stream];
+    const size_t nwg = ((size_t)en->n_entries + tpz::kPlanNextPer - 1) / tpz::kPlanNextPer;
+    r = grow(stream, &w.d_plan0, &w.plan0_cap, ((size_t)en->n_entries + 2 * nwg + 2 + 4) * 4);
+    if (r == TPZ_SUCCESS)
+      info = static_cast<uint32_t*>(w.d_plan0) + (size_t)en->n_entries + 2 * nwg + 2;
+    if (r == TPZ_SUCCESS && !w.h_info && hipHostMalloc(&w.h_info, 16) != hipSuccess) {
+      w.h_info = nullptr;
+      r = TPZ_ERR_NOMEM;
+    }
+    h_info = w.h_info;
+  }
+  if (r != TPZ_SUCCESS) return r;
+  r = plan_launch(c, en, block_size, d_first, d_ext, info, stream, h_bad_entry);
+  if (r != TPZ_SUCCESS) return r;
+  TPZ_HIP(hipMemcpyAsync(h_info, info, 16, hipMemcpyDeviceToHost, s));   // one round trip
   TPZ_HIP(hipStreamSynchronize(s));
+  if (h_info[1] != 0xFFFFFFFFu) {
+    *h_bad_entry = h_info[1];
+    return TPZ_ERR_INVALID_ARG;
+  }
   *h_n_blocks = h_info[2];
   return TPZ_SUCCESS;
 }
 
-tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_first,
-                          const uint64_t* d_ext, uint32_t n_blocks, uint8_t* d_out, void* stream) {
-  if (!c || !en || !d_first || !d_ext || !d_out) return TPZ_ERR_INVALID_ARG;
-  if (n_blocks == 0) return TPZ_SUCCESS;
+tpz_err tpz_plan_blocks_async(tpz_ctx* c, const tpz_entries* en, uint32_t block_size,
+                              uint32_t* d_first, uint64_t* d_ext, uint32_t* d_info, void* stream) {
+  if (!c || !en || !d_first || !d_ext || !d_info) return TPZ_ERR_INVALID_ARG;
+  if (!plan_args_ok(en, block_size)) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (en->n_entries == 0) {
+    TPZ_HIP(hipMemsetAsync(d_first, 0, 4, s));
+    TPZ_HIP(hipMemsetAsync(d_ext, 0, 8, s));
+    TPZ_HIP(hipMemsetAsync(d_info, 0, 16, s));
+    TPZ_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_info + 1), 0xFFFFFFFFu, 1, s));
+    return TPZ_SUCCESS;
+  }
+  uint64_t h_bad = UINT64_MAX;
+  const tpz_err r = plan_launch(c, en, block_size, d_first, d_ext, d_info, stream, &h_bad);
+  // a rejected entry found by the round trip of a large block size: the kernels have written
+  // d_info[1] already, and the plan stops there (d_info[2] stays 0)
+  if (r == TPZ_ERR_INVALID_ARG && h_bad != UINT64_MAX) {
+    TPZ_HIP(hipMemsetAsync(d_info + 2, 0, 4, s));
+    return TPZ_SUCCESS;
+  }
+  return r;
+}
+
+static tpz_err encode_launch(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_first,
+                             const uint64_t* d_ext, uint32_t n_blocks, const uint32_t* d_info,
+                             uint8_t* d_out, void* stream) {
   if ((reinterpret_cast<uintptr_t>(d_out) & 15u) || !en->d_kpos || !en->d_vpos ||
       (!en->d_keys && en->key_bytes) || (!en->d_vals && en->val_bytes))
     return TPZ_ERR_INVALID_ARG;
@@ -630,6 +699,7 @@ tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_f
   a.first = d_first;
   a.ext = d_ext;
   a.n_blocks = n_blocks;
+  a.plan_info = d_info;
   a.crc_tables = c->d_tables;
   a.out = d_out;
   a.big_count = w->d_defer;
@@ -637,6 +707,22 @@ tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_f
   a.num_cus = c->num_cus;
   TPZ_HIP(tpz::launch_encode(a, s));
   return TPZ_SUCCESS;
+}
+
+tpz_err tpz_encode_blocks(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_first,
+                          const uint64_t* d_ext, uint32_t n_blocks, uint8_t* d_out, void* stream) {
+  if (!c || !en || !d_first || !d_ext || !d_out) return TPZ_ERR_INVALID_ARG;
+  if (n_blocks == 0) return TPZ_SUCCESS;
+  return encode_launch(c, en, d_first, d_ext, n_blocks, nullptr, d_out, stream);
+}
+
+tpz_err tpz_encode_blocks_async(tpz_ctx* c, const tpz_entries* en, const uint32_t* d_first,
+                                const uint64_t* d_ext, const uint32_t* d_info, uint8_t* d_out,
+                                void* stream) {
+  if (!c || !en || !d_first || !d_ext || !d_info || !d_out) return TPZ_ERR_INVALID_ARG;
+  if (en->n_entries == 0) return TPZ_SUCCESS;
+  // at most one block per entry: the worklist bound
+  return encode_launch(c, en, d_first, d_ext, en->n_entries, d_info, d_out, stream);
 }
 
 tpz_err tpz_pack_ends(tpz_ctx* c, const tpz_batch* b, const tpz_columns* cols,

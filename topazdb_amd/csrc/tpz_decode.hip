@@ -114,8 +114,12 @@ __device__ __forceinline__ u32 lds_u32(const uint8_t* base, u32 a) {
 }
 // Big-endian u16 at byte offset a (bytes::Buf::get_u16).
 __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
+#ifdef TPZ_ABL_BE16U8
+  return ((u32)base[a] << 8) | base[a + 1];   // two ds_read_u8 + v_lshl_or
+#else
   u32 w = lds_u32(base, a);
   return ((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu);
+#endif
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
@@ -281,6 +285,20 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
 // in lanes 0, 16, 32, 48; those are shifted by 1280 / 2560 B and read out.
 __device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
   const u32 lane = lane_id();
+#ifdef TPZ_ABL_FLATCOMB
+  // diagnostic: every lane looks up at every level (no exec branches, more LDS lookups)
+  { const u32 t = crc_shift<0>(tab, A); A = (lane & 1u) ? t : A; }
+  A ^= dpp<kRowShl + 1>(A);
+  { const u32 t = crc_shift<1>(tab, A); A = (lane & 3u) == 2u ? t : A; }
+  A ^= dpp<kRowShl + 2>(A);
+  { const u32 t = crc_shift<2>(tab, A); A = (lane & 7u) == 4u ? t : A; }
+  A ^= dpp<kRowShl + 4>(A);
+  { const u32 t = crc_shift<3>(tab, A); A = (lane & 15u) == 8u ? t : A; }
+  A ^= dpp<kRowShl + 8>(A);
+  { const u32 t = crc_shift<4>(tab, A); A = (lane & 31u) == 16u ? t : A; }
+  { const u32 t = crc_shift<5>(tab, A); A = (lane & 47u) == 32u ? t : A; }
+  return readlane(A, 0) ^ readlane(A, 16) ^ readlane(A, 32) ^ readlane(A, 48);
+#endif
   if ((lane & 1u) == 1u) A = crc_shift<0>(tab, A);
   A ^= dpp<kRowShl + 1>(A);
   if ((lane & 3u) == 2u) A = crc_shift<1>(tab, A);
@@ -771,13 +789,6 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
     carry = short_segs ? copy_fast3(src, col, map, F, 4u, carry, rare)
                        : copy_fast(src, col, map, F, 4u, carry, rare);
   TPZ_STAMP(St, 4);
-#ifdef TPZ_GF_COMBINE
-  // lane l's run ends 80 l bytes before the end: shift it there with one GF(2) multiply by
-  // x^(640 l) mod P (a per-lane constant), then XOR the lanes
-  const u32 R = wave_xor(gf_mul_lane(kshift, L.c));
-#else
-  const u32 R = crc_combine(tab, L.c);
-#endif
 #ifdef TPZ_ABL_STAMPS
   St.rare += __builtin_popcount(rare);
 #endif
@@ -785,7 +796,26 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
     for (u32 w = 0; w < nw; w++)
       if (rare & (1u << w)) copy_window(src, col, map, nk, F.tot, F.npad, dst, (u32)kWaveMapLen, w, cw[w]);
   }
-  return R;
+  return L.c;   // the lane's raw run CRC: crc_combine gives R0 of the whole range
+}
+
+// The wave path defers a block's CRC combine and status write into the next block's decode
+// (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
+// and parse round trips instead of ending the block's dependent chain.
+struct PendingCrc {
+  u32 live;            // (uniform) a block's combine is pending
+  u32 b, st, cnt, stored, k;
+  u32 lc;              // per lane: the raw CRC of the lane's 80-byte run
+};
+
+__device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
+  if (!pd.live) return;
+  const u32 R = crc_combine(tab, pd.lc);
+  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
+                                                                 : ~crc_unshift_small(tab, R, pd.k);
+  const bool ok = crc == pd.stored;                                            // checksum.rs:17
+  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
+  pd.live = 0;
 }
 
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. `map` is the
@@ -793,7 +823,7 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
 template <class Col, class MapT, int kMapLen, bool BIG>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
-                                             const Out& o, u32 kshift, Stamps& S) {
+                                             const Out& o, u32 kshift, Stamps& S, PendingCrc& pd) {
   const u32 lane = lane_id();
 #ifdef TPZ_ABL_LOADONLY
   put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
@@ -804,6 +834,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   const u32 tag = win[(int)(a0 + len) - 1];                                    // compress.rs:99
   const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));      // block.rs:51
   const u32 n = lds_be16(win, a0);                                             // block.rs:54
+#ifndef TPZ_ABL_NODEFER
+  finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
+#endif
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
   if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
@@ -867,6 +900,19 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       const bool act = i < n;
       u32 off = 0, kl = 0, vl = 0;
       bool ok = true;
+#ifdef TPZ_ABL_BFPARSE
+      // diagnostic: branch-free reads (an out-of-range read goes to the block start instead)
+      {
+        off = lds_be16(win, act ? a0 + 2 + 2 * i : a0);
+        const bool ok1 = act && off + 2 <= dl;
+        kl = lds_be16(win, ok1 ? db + off : a0);
+        const bool ok2 = ok1 && off + 4 + kl <= dl;
+        vl = lds_be16(win, ok2 ? db + off + 2 + kl : a0);
+        ok = !act || (ok2 && off + 4 + kl + vl <= dl);
+        if (!(act && ok)) kl = vl = 0;
+        if (!act) off = 0;
+      }
+#else
       if (act) {
         off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
         ok = off + 2 <= dl;
@@ -874,6 +920,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
         if (!ok) kl = vl = 0;
       }
+#endif
       bad |= __ballot(act && !ok) != 0;
       short_segs |= __ballot((kl != 0 && kl < 16) || (vl != 0 && vl < 16)) != 0;
       const u32 ki = wave_scan_incl(kl) + kc;
@@ -958,16 +1005,23 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     crc = stored;
 #else
     u32 R;
-    if (!BIG && fuse && f_short)
-      R = copy_crc_fused<true>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                               reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
-                               P + k, kshift, S);
-    else if (!BIG && fuse)
-      R = copy_crc_fused<false>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                                reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
-                                P + k, kshift, S);
-    else
+    if (!BIG && fuse) {
+      const u32 lc = f_short
+          ? copy_crc_fused<true>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                                 reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
+                                 P + k, kshift, S)
+          : copy_crc_fused<false>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                                  reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
+                                  P + k, kshift, S);
+#ifndef TPZ_ABL_NODEFER
+      pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
+      return;
+#else
+      R = crc_combine(tab, lc);
+#endif
+    } else {
       R = wave_crc(tab, win, pb, P + k);
+    }
     crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
 #if defined(TPZ_ABL_NOCF) || defined(TPZ_ABL_LUTVALU)
     asm volatile("" ::"v"(R));   // keep the CRC work, report a match (timing builds only)
@@ -1052,6 +1106,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
   const u32 kshift = p.lane_shift[lane];
+#ifdef TPZ_ABL_PRIO
+  if (wid & 1u) __builtin_amdgcn_s_setprio(1);   // diagnostic: static priority for half the waves
+#endif
   uint8_t* slot = lds + kTableBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
@@ -1134,6 +1191,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     }
   };
   u32 k = 0;  // this wave's block counter
+  PendingCrc pd{0u, 0u, 0u, 0u, 0u, 0u, 0u};
   issue(b, 0, s_cur, e_cur);
   vm_pad<kVmAfter>(p.out);
 
@@ -1170,11 +1228,12 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       const u32 bdec = bcur;
 #endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bdec, s, p.out, kshift, S);
+                                                           len64, bdec, s, p.out, kshift, S, pd);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
   }
+  finish_pending(tab, p.out, pd);    // the wave's last block
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kWavesPerWG + wid;
   if (lane == 0 && gw < (u32)kStampWaves)

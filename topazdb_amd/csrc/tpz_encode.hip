@@ -216,13 +216,14 @@ struct PlanParams {
   u32 T;             // block_size - 2: an entry fits while size + encode_len <= T
   u32 span;          // max(1, T / 5): a block holds at most this many entries (each >= 5 B)
   u32* nx;           // n
-  u32* info;         // [0] max nx (w), [1] first bad entry (~0u: none), zeroed/set by the host
+  u32* info;         // [0] max nx (w), [1] first bad entry (~0u: none): plan_reduce_kernel
   u32* wgmax;        // phase 0: per-workgroup max nx
-  int* tab_a;        // chunk transfer tables, K x w
+  u32* wgbad;        // phase 0: per-workgroup first bad entry (~0u: none)
+  int* tab_a;        // chunk transfer tables, K x w (w read on the device: info[0])
   int* tab_b;
   u32 C;             // entries per chunk (>= w)
   u32 K;             // chunks
-  u32 w;
+  u32 grid;          // phase 1: workgroups of the grid-stride table / round kernels
   u32* cnt;          // K: blocks per chunk, then their exclusive prefix
   u32* first;        // n + 1: block starts
   u64* ext;          // n + 1: encoded byte extents
@@ -239,7 +240,7 @@ __device__ __forceinline__ u64 S_at(const u64* kpos, const u64* vpos, u64 k0, u6
 // (its entries + span) are staged in LDS once. The longest block (w) is reduced per workgroup into
 // wgmax[] (a single-address atomic per wave saturated at ~88 per microsecond: 6.4 ms for 2^20
 // blocks), then by plan_reduce_kernel.
-constexpr u32 kNextWG = 256, kNextPer = 2048, kNextWin = 4096;
+constexpr u32 kNextWG = 256, kNextPer = kPlanNextPer, kNextTail = 512, kNextWin = kNextPer + kNextTail;
 
 // The window is staged as {kpos, vpos} relative to the workgroup's first entry (u32 pairs: one
 // ds_read_b64 per probe, and each entry's own lengths come from LDS too); a window whose bytes do
@@ -250,9 +251,11 @@ __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
   __shared__ u32 wmax[kNextWG / kWave];
   const u32 a0 = blockIdx.x * kNextPer;
   const u64 k0 = p.kpos[a0], v0 = p.vpos[a0];
-  const u32 hiw = (u32)min((u64)p.n, (u64)a0 + kNextPer - 1 + p.span);   // highest index probed
+  // the window: the workgroup's entries and kNextTail more (probes past it read global memory:
+  // blocks of more than ~kNextTail / 2 entries); a window of the whole span ahead read 40 % more
+  const u32 hiw = (u32)min((u64)p.n, (u64)a0 + kNextWin - 1);   // highest index staged
   const u32 wn = hiw - a0 + 1;
-  const bool in_lds = wn <= kNextWin && (p.kpos[hiw] - k0) + (p.vpos[hiw] - v0) + 4ull * wn < (1ull << 32);
+  const bool in_lds = (p.kpos[hiw] - k0) + (p.vpos[hiw] - v0) + 4ull * wn < (1ull << 32);
   if (in_lds) {
     // all of a thread's loads issued before the first LDS write: a loop that stores each pair
     // as it arrives waits out one memory latency per pair
@@ -297,32 +300,31 @@ __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
     } else {
       const u64 lim = sa + p.T;
       auto S = [&](u32 x) -> u64 {
-        if (!in_lds) return 4ull * (x - a0) + (p.kpos[x] - k0) + (p.vpos[x] - v0);
+        if (!in_lds || x - a0 >= wn) return 4ull * (x - a0) + (p.kpos[x] - k0) + (p.vpos[x] - v0);
         const uint2 e = sw[x - a0];
         return 4ull * (x - a0) + e.x + e.y;
       };
-      u32 lo = a + 1, hi = (u32)min((u64)p.n, (u64)a + p.span);   // S(lo) <= lim
-      if (S(hi) <= lim) {
-        lo = hi;
-      } else {   // S(lo) <= lim < S(hi): gallop from the window's mean entry size, then bisect
-        if (guess && hi - lo > 1) {
-          const u32 g = (u32)min((u64)hi - 1, max((u64)lo, (u64)a + p.T / mean));
-          if (S(g) <= lim) {
-            lo = g;
-            u32 d = 1;
-            while (d < hi - lo && S(lo + d) <= lim) { lo += d; d <<= 1; }
-            if (d < hi - lo) hi = lo + d;
-          } else {
-            hi = g;
-            u32 d = 1;
-            while (d < hi - lo && S(hi - d) > lim) { hi -= d; d <<= 1; }
-            if (d < hi - lo) lo = hi - d;
-          }
+      // the block's end b: the largest x in [a + 1, min(n, a + span)] with S(x) <= lim.
+      // Invariant: S(lo) <= lim, and hi is past the range or S(hi) > lim (hi itself is never
+      // probed while it is the range's exclusive end).
+      u32 lo = a + 1, hi = (u32)min((u64)p.n, (u64)a + p.span) + 1;
+      if (guess && hi - lo > 1) {   // gallop from the window's mean entry size
+        const u32 g = (u32)min((u64)hi - 1, max((u64)lo, (u64)a + p.T / mean));
+        if (S(g) <= lim) {
+          lo = g;
+          u32 d = 1;
+          while (d < hi - lo && S(lo + d) <= lim) { lo += d; d <<= 1; }
+          if (d < hi - lo) hi = lo + d;
+        } else {
+          hi = g;
+          u32 d = 1;
+          while (d < hi - lo && S(hi - d) > lim) { hi -= d; d <<= 1; }
+          if (d < hi - lo) lo = hi - d;
         }
-        while (hi - lo > 1) {
-          const u32 mid = lo + (hi - lo) / 2;
-          if (S(mid) <= lim) lo = mid; else hi = mid;
-        }
+      }
+      while (hi - lo > 1) {   // then bisect
+        const u32 mid = lo + (hi - lo) / 2;
+        if (S(mid) <= lim) lo = mid; else hi = mid;
       }
       len = lo - a;
     }
@@ -334,66 +336,97 @@ __global__ __launch_bounds__(kNextWG) void plan_next_kernel(PlanParams p) {
     bad = min(bad, (u32)__shfl_xor((int)bad, o));
   }
   const u32 lane = lane_id(), wid = threadIdx.x / kWave;
+  __shared__ u32 wbad[kNextWG / kWave];
   if (lane == 0) {
     wmax[wid] = mx;
-    if (bad != ~0u) atomicMin(&p.info[1], bad);    // only for inputs the reference rejects
+    wbad[wid] = bad;     // ~0u unless the reference rejects an entry
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    u32 m = 0;
-    for (u32 w = 0; w < kNextWG / kWave; w++) m = max(m, wmax[w]);
+    u32 m = 0, b = ~0u;
+    for (u32 w = 0; w < kNextWG / kWave; w++) {
+      m = max(m, wmax[w]);
+      b = min(b, wbad[w]);
+    }
     p.wgmax[blockIdx.x] = m;
+    p.wgbad[blockIdx.x] = b;
   }
 }
 
-// info[0] = the longest block in entries (max over wgmax), one workgroup.
+// info[0] = the longest block in entries (max over wgmax), info[1] = the first entry the reference
+// rejects (min over wgbad, ~0u: none); one workgroup. No host initialisation is needed.
 __global__ __launch_bounds__(1024) void plan_reduce_kernel(PlanParams p, u32 n_wg) {
-  __shared__ u32 part[1024 / kWave];
-  u32 m = 0;
-  for (u32 i = threadIdx.x; i < n_wg; i += 1024) m = max(m, p.wgmax[i]);
-  for (int o = 32; o; o >>= 1) m = max(m, (u32)__shfl_xor((int)m, o));
-  if (lane_id() == 0) part[threadIdx.x / kWave] = m;
+  __shared__ u32 part[1024 / kWave], partb[1024 / kWave];
+  u32 m = 0, b = ~0u;
+  for (u32 i = threadIdx.x; i < n_wg; i += 1024) {
+    m = max(m, p.wgmax[i]);
+    b = min(b, p.wgbad[i]);
+  }
+  for (int o = 32; o; o >>= 1) {
+    m = max(m, (u32)__shfl_xor((int)m, o));
+    b = min(b, (u32)__shfl_xor((int)b, o));
+  }
+  if (lane_id() == 0) {
+    part[threadIdx.x / kWave] = m;
+    partb[threadIdx.x / kWave] = b;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (u32 w = 0; w < 1024 / kWave; w++) m = max(m, part[w]);
+    for (u32 w = 0; w < 1024 / kWave; w++) {
+      m = max(m, part[w]);
+      b = min(b, partb[w]);
+    }
     p.info[0] = m;
+    p.info[1] = b;
+    p.info[2] = 0;
   }
+}
+
+// The longest block in entries, w = info[0] (written by plan_reduce_kernel earlier on the stream):
+// the transfer tables' row length. The host sizes them from a bound (span) and the grids stride
+// over K x w, so the plan needs no host round trip between its phases.
+__device__ __forceinline__ u32 plan_w(const PlanParams& p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // tab_a[k w + j] = where the chain entering chunk k at entry k C + j leaves it: the entry
 // offset into chunk k + 1, or -1 when it reaches the end of the entries first.
 __global__ __launch_bounds__(256) void plan_table_kernel(PlanParams p) {
-  const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (u64)p.K * p.w) return;
-  const u32 k = (u32)(t / p.w), j = (u32)(t % p.w);
-  const u64 c1 = (u64)(k + 1) * p.C;
-  u64 a = (u64)k * p.C + j;
-  int F = -1;
-  if (a < p.n) {
-    const u64 end = min((u64)p.n, c1);
-    while (a < end) a += p.nx[a];
-    F = a >= p.n ? -1 : (int)(a - c1);
+  const u32 w = plan_w(p);
+  const u64 tn = (u64)p.K * w;
+  for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x; t < tn; t += (u64)gridDim.x * 256) {
+    const u32 k = (u32)(t / w), j = (u32)(t % w);
+    const u64 c1 = (u64)(k + 1) * p.C;
+    u64 a = (u64)k * p.C + j;
+    int F = -1;
+    if (a < p.n) {
+      const u64 end = min((u64)p.n, c1);
+      while (a < end) a += p.nx[a];
+      F = a >= p.n ? -1 : (int)(a - c1);
+    }
+    p.tab_a[t] = F;
   }
-  p.tab_a[t] = F;
 }
 
 // One Hillis-Steele round: A_k <- A_k o A_{k-d} (tab_a -> tab_b).
 __global__ __launch_bounds__(256) void plan_round_kernel(PlanParams p, u32 d) {
-  const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (u64)p.K * p.w) return;
-  const u32 k = (u32)(t / p.w), j = (u32)(t % p.w);
-  int v = p.tab_a[t];
-  if (k >= d) {
-    const int x = p.tab_a[(u64)(k - d) * p.w + j];
-    v = x < 0 ? -1 : p.tab_a[(u64)k * p.w + x];
+  const u32 w = plan_w(p);
+  const u64 tn = (u64)p.K * w;
+  for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x; t < tn; t += (u64)gridDim.x * 256) {
+    const u32 k = (u32)(t / w), j = (u32)(t % w);
+    int v = p.tab_a[t];
+    if (k >= d) {
+      const int x = p.tab_a[(u64)(k - d) * w + j];
+      v = x < 0 ? -1 : p.tab_a[(u64)k * w + x];
+    }
+    p.tab_b[t] = v;
   }
-  p.tab_b[t] = v;
 }
 
 // The chain's entry into chunk k (absolute entry index), or ~0u if it ended before.
 __device__ __forceinline__ u64 chunk_entry(const PlanParams& p, u32 k) {
   if (k == 0) return 0;
-  const int e = p.tab_a[(u64)(k - 1) * p.w];
+  const int e = p.tab_a[(u64)(k - 1) * plan_w(p)];
   return e < 0 ? ~0ull : (u64)k * p.C + (u32)e;
 }
 
@@ -486,7 +519,8 @@ __global__ __launch_bounds__(256) void plan_table_lds_kernel(PlanParams p) {
   extern __shared__ u32 snx[];
   const u32 k = blockIdx.x;
   const u32 len = stage_chunk_nx(p, k, snx);
-  for (u32 j = threadIdx.x; j < p.w; j += blockDim.x) {
+  const u32 w = plan_w(p);
+  for (u32 j = threadIdx.x; j < w; j += blockDim.x) {
     int F = -1;
     if (j < len) {
       u32 r = j;
@@ -494,7 +528,7 @@ __global__ __launch_bounds__(256) void plan_table_lds_kernel(PlanParams p) {
       const u64 a = (u64)k * p.C + r;
       F = a >= p.n ? -1 : (int)(r - p.C);
     }
-    p.tab_a[(u64)k * p.w + j] = F;
+    p.tab_a[(u64)k * w + j] = F;
   }
 }
 
@@ -540,6 +574,7 @@ struct EncParams {
   const u32* first;  // n_blocks + 1
   const u64* ext;    // n_blocks + 1
   u32 n_blocks;
+  const u32* plan_info;      // non-null: tpz_plan_blocks_async's {w, bad entry, n_blocks} on the device
   const u32* crc_tables;
   uint8_t* out;      // 16-byte aligned
   u32* big_list;     // workspace: blocks for encode_big_kernel
@@ -645,8 +680,10 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
 
   const u32 nwaves = gridDim.x * kEncWaves;
   const u32 wv = blockIdx.x * kEncWaves + wid;
-  if (wv >= p.n_blocks) return;
-  const u32 nmine = (p.n_blocks - 1 - wv) / nwaves + 1;     // blocks wv + i * nwaves
+  // a plan with a rejected entry (tpz_plan_blocks_async) encodes nothing
+  const u32 n_blocks = !p.plan_info ? p.n_blocks : (uni(p.plan_info[1]) != ~0u ? 0u : uni(p.plan_info[2]));
+  if (wv >= n_blocks) return;
+  const u32 nmine = (n_blocks - 1 - wv) / nwaves + 1;       // blocks wv + i * nwaves
 
   auto load_group = [&](u32 g, BlockMeta& m) {
     const u32 i = g * kWave + lane;
@@ -864,16 +901,19 @@ hipError_t launch_plan(const PlanLaunch& a, hipStream_t s) {
   hipError_t e;
   if (a.phase == 0) {
     const u32 nwg = (u32)(((u64)a.n + kNextPer - 1) / kNextPer);
-    p.wgmax = a.nx + a.n;                 // the caller sizes nx for n + n / 2048 + 1 words
+    p.wgmax = a.nx + a.n;                 // the caller sizes nx for n + 2 (n / 2048 + 1) words
+    p.wgbad = p.wgmax + nwg;
     static const bool bisect = std::getenv("TPZ_PLAN_BISECT") != nullptr;   // A/B probe
     p.guess = bisect ? 0u : 1u;
     plan_next_kernel<<<nwg, kNextWG, 0, s>>>(p);
     plan_reduce_kernel<<<1, 1024, 0, s>>>(p, nwg);
     return hipGetLastError();
   }
-  p.w = a.w;
-  const u64 tn = (u64)p.K * p.w;
-  const u32 tg = (u32)((tn + 255) / 256);
+  // grid-stride table / round kernels over K x w (w on the device; a.w is its bound)
+  const u64 tn = (u64)p.K * a.w;
+  const u64 tg_full = (tn + 255) / 256;
+  const u32 tg = (u32)(tg_full < 2048 ? (tg_full ? tg_full : 1) : 2048);
+  p.grid = tg;
   p.tab_a = a.tab_a;
   p.tab_b = a.tab_b;
   static const bool global_walk = std::getenv("TPZ_PLAN_GLOBAL_WALK") != nullptr;   // A/B probe
@@ -914,6 +954,7 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
   p.first = a.first;
   p.ext = a.ext;
   p.n_blocks = a.n_blocks;
+  p.plan_info = a.plan_info;
   p.crc_tables = a.crc_tables;
   p.out = a.out;
   p.big_list = a.big_list;

@@ -254,9 +254,9 @@ struct PlanLaunch {
   const uint64_t* vpos;
   uint32_t n;
   uint32_t block_size;
-  uint32_t* nx;        // workspace: n + n / 2048 + 2 (nx, then per-workgroup maxima)
-  uint32_t* info;      // workspace: {max nx, first bad entry}
-  uint32_t w;          // phase 1: info[0]
+  uint32_t* nx;        // workspace: n + 2 (n / 2048 + 1) (nx, per-workgroup maxima and bad entries)
+  uint32_t* info;      // {max nx (w), first bad entry, n_blocks}: written by the kernels
+  uint32_t w;          // phase 1: an upper bound of info[0] (the tables' row capacity)
   uint32_t chunk;      // phase 1: entries per chunk (>= w)
   int* tab_a;          // phase 1 workspace: 2 x K x w
   int* tab_b;
@@ -267,6 +267,7 @@ struct PlanLaunch {
 };
 hipError_t launch_plan(const PlanLaunch& a, hipStream_t stream);
 constexpr uint32_t kPlanChunk = 2048;  // minimum entries per plan chunk
+constexpr uint32_t kPlanNextPer = 4096; // entries per plan_next_kernel workgroup
 
 struct EncodeLaunch {
   const uint8_t* keys;
@@ -277,7 +278,8 @@ struct EncodeLaunch {
   uint64_t val_bytes;
   const uint32_t* first;
   const uint64_t* ext;
-  uint32_t n_blocks;
+  uint32_t n_blocks;            // or its bound, when plan_info is set
+  const uint32_t* plan_info;    // tpz_plan_blocks_async's d_info (block count on the device), or null
   const uint32_t* crc_tables;
   uint8_t* out;
   uint32_t* big_list;   // workspace: n_blocks

@@ -97,6 +97,39 @@ def encode_blocks(ctx: Context, ent: DeviceEntries, first: torch.Tensor, ext: to
     return out
 
 
+def plan_blocks_async(ctx: Context, ent: DeviceEntries, block_size: int,
+                      stream: torch.cuda.Stream | None = None):
+    """tpz_plan_blocks_async: (first, ext, info) device tensors, no host round trip; info (int32
+    x 4) holds {widest block start, first rejected entry (-1: none), n_blocks} once the stream gets there."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    first = torch.empty(ent.n + 1, dtype=torch.int32, device=dev)
+    ext = torch.empty(ent.n + 1, dtype=torch.int64, device=dev)
+    info = torch.empty(4, dtype=torch.int32, device=dev)
+    ctx.plan_blocks_async_ptrs(ent.struct(), block_size, first.data_ptr(), ext.data_ptr(),
+                               info.data_ptr(), s.cuda_stream)
+    return first, ext, info
+
+
+def encode_bound(ent: DeviceEntries) -> int:
+    """Bytes that hold the data region of any plan of these entries (every entry its own block)."""
+    return int(ent.keys.numel()) + int(ent.vals.numel()) + 13 * ent.n + 16
+
+
+def encode_blocks_async(ctx: Context, ent: DeviceEntries, first: torch.Tensor, ext: torch.Tensor,
+                        info: torch.Tensor, out: torch.Tensor | None = None,
+                        stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """tpz_encode_blocks_async: the data region of plan_blocks_async's plan, its block count read
+    on the device; `out` defaults to encode_bound bytes."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    if out is None:
+        out = torch.empty(encode_bound(ent), dtype=torch.uint8, device=dev)
+    ctx.encode_blocks_async_ptrs(ent.struct(), first.data_ptr(), ext.data_ptr(), info.data_ptr(),
+                                 out.data_ptr(), s.cuda_stream)
+    return out
+
+
 def build_region(ctx: Context, keys, kpos, vals, vpos, block_size: int):
     """The whole write side for host entries: (data-region bytes, block extents, first entry of
     every block), as numpy arrays (the device counterpart of synth.build_blocks)."""
