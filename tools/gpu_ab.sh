@@ -8,6 +8,6 @@ if [ -n "$TESTS" ]; then
   tail -2 $OUT/pytest.log
 fi
 for c in ${CONFIGS:-4k}; do
-  timeout -k 10 400 python3 -u tools/abl_multi.py --config $c --rounds ${ROUNDS:-7} --steps 10 $VARIANTS > $OUT/abl_$c.jsonl 2> $OUT/abl_$c.err || { tail $OUT/abl_$c.err; exit 1; }
+  timeout -k 10 400 python3 -u tools/abl_multi.py --config $c --rounds ${ROUNDS:-7} --steps 10 $( [ "$c" = 64k ] && echo --blocks 65536 ) $VARIANTS > $OUT/abl_$c.jsonl 2> $OUT/abl_$c.err || { tail $OUT/abl_$c.err; exit 1; }
   echo "== $c"; cat $OUT/abl_$c.jsonl
 done

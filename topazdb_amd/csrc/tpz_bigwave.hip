@@ -63,7 +63,8 @@ constexpr u32 kStep = kStepRun * kWave;           // 4 KiB per step, one step pe
 constexpr int kSegs = 128;                        // entry-table slots per wave (2 n <= 126, + 2 sentinels)
 constexpr int kU = TPZ_BW_KU;                     // copy windows per group
 constexpr int kWaveLds = kSegs * 8 + kU * kWave;   // entry table + kU u8 chunk maps
-constexpr int kLdsBytes = kCrcRepWords * 4 + kWaves * kWaveLds;
+constexpr int kShiftWords = 4 * 256;                // the step shift's byte tables (x^(8 kStep))
+constexpr int kLdsBytes = kCrcRepWords * 4 + kWaves * kWaveLds + kShiftWords * 4;
 static_assert(kLdsBytes <= 163840, "bigwave LDS");
 constexpr u32 kOob = 0x80000000u;
 
@@ -473,7 +474,15 @@ __device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams&
     x = slice4(rep, r, x ^ v[t].z);
     x = slice4(rep, r, x ^ v[t].w);
   }
+#ifdef TPZ_BW_GFSTEP
   return i == 0 ? x : (gf_mul(p.step_shift, acc) ^ x);
+#else
+  // acc shifted by one step: four byte-table lookups instead of a 32-step GF(2) multiply
+  const u32* sh = rep + kCrcRepWords + kWaves * kWaveLds / 4;
+  const u32 t = xor3(sh[acc & 0xFF], sh[256 + ((acc >> 8) & 0xFF)], sh[512 + ((acc >> 16) & 0xFF)]) ^
+                sh[768 + (acc >> 24)];
+  return i == 0 ? x : (t ^ x);
+#endif
 }
 
 __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p) {
@@ -483,6 +492,11 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
   u32* rep = reinterpret_cast<u32*>(lds);
   for (int i = threadIdx.x; i < kCrcRepWords / 4; i += kThreads)
     reinterpret_cast<uint4*>(rep)[i] = reinterpret_cast<const uint4*>(p.rep)[i];
+  {   // shift-by-one-step tables: byte j of the CRC, value b -> gf_mul(x^(8 kStep), b << 8 j)
+    u32* sh = rep + kCrcRepWords + kWaves * kWaveLds / 4;
+    for (int i = threadIdx.x; i < kShiftWords; i += kThreads)
+      sh[i] = gf_mul(p.step_shift, (u32)(i & 255) << (8 * (i >> 8)));
+  }
   __syncthreads();
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
   Seg* seg = reinterpret_cast<Seg*>(lds + kCrcRepWords * 4 + wid * kWaveLds);

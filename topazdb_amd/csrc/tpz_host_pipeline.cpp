@@ -40,8 +40,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tpz_internal.h"
@@ -237,14 +239,40 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       !o->h_spill_off || !o->h_spill_used || (n && (!h_src || !o->h_data)) ||
       (o->ends_cap && !o->h_ends) || (o->spill_cap && !o->h_spill))
     return TPZ_ERR_INVALID_ARG;
-  for (uint32_t i = 0; i < n; i++)
-    if (h_ext[i + 1] < h_ext[i]) return TPZ_ERR_INVALID_ARG;
+  // One pass over the extents (non-decreasing) and the blocks' tag bytes (a snappy / lz4 block
+  // anywhere: the decoded extents differ from h_ext for the whole batch), on up to 16 host
+  // threads: the tags sit one per block, a page apart, and a single-thread walk over 2^20 of them
+  // cost ~20 ms of the call.
+  bool codec = false;
+  {
+    std::atomic<bool> bad{false}, any_codec{false};
+    auto scan = [&](uint32_t a, uint32_t b) {
+      bool c = false, nd = false;
+      for (uint32_t i = a; i < b; i++) {
+        nd |= h_ext[i + 1] < h_ext[i];
+        c |= h_ext[i + 1] > h_ext[i] && (h_src[h_ext[i + 1] - 1] == 2 || h_src[h_ext[i + 1] - 1] == 3);
+      }
+      if (nd) bad = true;
+      if (c) any_codec = true;
+    };
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t nt = std::min<uint32_t>({16u, hw, n / 65536 + 1});
+    if (nt <= 1) {
+      scan(0, n);
+    } else {
+      std::vector<std::thread> th;
+      const uint32_t per = (n + nt - 1) / nt;
+      for (uint32_t t = 0; t < nt; t++) {
+        const uint32_t a = std::min(n, t * per), b = std::min(n, a + per);
+        th.emplace_back(scan, a, b);
+      }
+      for (auto& t : th) t.join();
+    }
+    if (bad) return TPZ_ERR_INVALID_ARG;
+    codec = any_codec;
+  }
   o->h_first[0] = 0;
   *o->h_spill_used = 0;
-  // a snappy / lz4 block anywhere: the decoded extents differ from h_ext for the whole batch
-  bool codec = false;
-  for (uint32_t i = 0; i < n && !codec; i++)
-    codec = h_ext[i + 1] > h_ext[i] && (h_src[h_ext[i + 1] - 1] == 2 || h_src[h_ext[i + 1] - 1] == 3);
   if (codec && !o->h_dext) return TPZ_ERR_INVALID_ARG;
   if (o->h_dext && !codec)
     for (uint32_t i = 0; i <= n; i++) o->h_dext[i] = h_ext[i];
