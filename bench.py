@@ -265,7 +265,7 @@ def gpu_local_cpus(device: int) -> list[int]:
         return []
 
 
-def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps: int = 2,
+def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps: int = 5,
              chunk_blocks: int = 0) -> dict:
     """Host memory -> HBM -> host memory through the library's own pipeline
     (tpz_decode_blocks_host: chunked H2D, decode, packed ends, D2H on two streams), from and to
@@ -332,7 +332,7 @@ def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps
             "numa_cpus": len(cpus), "path": "tpz_decode_blocks_host (C ABI)"}
 
 
-def e2e_codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, reps: int = 2) -> dict:
+def e2e_codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, reps: int = 5) -> dict:
     """The host-to-host path for compressed blocks (tpz_decode_blocks_host with the codec step on
     the device, compress.rs:104-111; snappy is topazdb's default, src/opt.rs:48): 2^18 "4kc"
     blocks encoded with `codec`, pinned buffers on the GPU's NUMA node, h_data sized from

@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    src, ext, n_ent, _, _, _ = make_shard("4k", 1 << 20, 0)
+    src, ext, _, n_ent, _, _ = make_shard("4k", 1 << 20, 0)
     nb = len(ext) - 1
     cpus = gpu_local_cpus(0)
     old = os.sched_getaffinity(0)
