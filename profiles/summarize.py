@@ -59,6 +59,7 @@ def main():
                    "source": os.path.relpath(dst, os.path.dirname(root)),
                    "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024"},
                   open(os.path.join(root, "traffic.json"), "w"), indent=1)
+        shutil.copy(os.path.join(root, "traffic.json"), os.path.join(dst, "traffic.json"))
     print(json.dumps(summary, indent=1))
 
 
