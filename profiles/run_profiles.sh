@@ -5,10 +5,11 @@ set -o pipefail
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-validate --no-snappy --no-lz4"
+ONLY4K="--no-side-configs --config5-gib 0 --no-exact --no-encode"   # the headline decode alone
+B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-validate --no-snappy --no-lz4 --no-file-crc --no-seek $ONLY4K"
 # the trace pass runs 40 timed steps so that the first (slower, clock ramp-up) dispatches do not
 # skew the average the bench line is compared with
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-e2e --no-validate --no-snappy --no-lz4 --no-file-crc --no-seek > "$OUT/trace.log" 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-e2e --no-validate --no-snappy --no-lz4 --no-file-crc --no-seek $ONLY4K > "$OUT/trace.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace_codecs" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-validate --no-file-crc > "$OUT/trace_codecs.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $B > "$OUT/pmc_fetch.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT/pmc_write" -o run -- python3 $B > "$OUT/pmc_write.log" 2>&1 &&

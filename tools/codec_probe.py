@@ -77,7 +77,7 @@ def main():
                                            st.data_ptr(), stream.cuda_stream) == 0
         run()
         torch.cuda.synchronize()
-        if name == "cstamps":
+        if "stamps" in name:
             L.tpz_debug_codec_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
             buf = (C.c_ulonglong * 8)()
             L.tpz_debug_codec_stamps(buf, 1)
@@ -95,7 +95,7 @@ def main():
             ref = dst.clone()
         else:
             line["same_bytes"] = bool(torch.equal(ref, dst))
-        if name == "cstamps":
+        if "stamps" in name:
             L.tpz_debug_lane_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
             lb = (C.c_ulonglong * 8)()
             L.tpz_debug_lane_stamps(lb, 0)
