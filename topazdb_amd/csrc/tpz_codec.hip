@@ -1171,7 +1171,11 @@ __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u3
 // L1 holds no stale copy. A step issues one set of four 16-byte loads for every lane: a literal's
 // source bytes or a far copy's stored lines (one set instead of one per descriptor: 1.351 ->
 // 1.314 ms per 2^18 4kc blocks).
+#ifdef TPZ_CODEC_WG64
+constexpr u32 kRingWG = 64;
+#else
 constexpr u32 kRingWG = 256;                                 // blocks (threads) per workgroup
+#endif
 #ifdef TPZ_CODEC_RING256
 constexpr u32 kRing = 256;                                   // 2 workgroups (8 waves) per CU
 #else
@@ -1272,8 +1276,10 @@ __device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst,
 template <int kCodec>
 __device__ __forceinline__ void ring_body(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kRingWG * kRing];
+#ifndef TPZ_CODEC_PERMUTE
   __shared__ u32 fl_addr[kRingWG / kWave][kWave];
   __shared__ u32 fl_lane[kRingWG / kWave][kWave];
+#endif
   const u32 lane = lane_id(), wid = threadIdx.x >> 6;
   uint8_t* R = rings + threadIdx.x * kRing;
   const u32 b = blockIdx.x * kRingWG + threadIdx.x;
@@ -1574,6 +1580,25 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
       const u64 mk = __ballot(has);
       if (mk == 0) break;
       const u32 cnt = __builtin_popcountll(mk);
+#ifdef TPZ_CODEC_PERMUTE
+      // the k-th completed line goes to lanes 4k .. 4k + 3 (mod 64): its owner pushes fl | lane
+      // (fl is 64-aligned) to lane 4k with ds_permute, the quad broadcasts it with DPP
+      const u32 kr = __builtin_amdgcn_mbcnt_hi((u32)(mk >> 32), __builtin_amdgcn_mbcnt_lo((u32)mk, 0u));
+      for (u32 q = 0; q < cnt; q += kWave / 4) {
+        const bool send = has && kr >= q && kr < q + kWave / 4;
+        const u32 tgt = send ? 4u * (kr - q) : ((lane & ~3u) | 1u);   // others: never a quad's lane 0
+        const u32 x0 = (u32)__builtin_amdgcn_ds_permute((int)(4 * tgt), (int)(fl | lane));
+        const u32 x = (u32)__builtin_amdgcn_mov_dpp((int)x0, 0x00, 0xF, 0xF, false);
+        const u32 k = q + (lane >> 2);
+        if (k < cnt) {
+          const u32 a = x & ~63u;
+          const uint8_t* Rs = rings + (wid * kWave + (x & 63u)) * kRing;
+          const u32 o = (a & (kRing - 1)) + 16 * (lane & 3);
+          st16u(p.dst + a + 16 * (lane & 3), lds16(Rs + o));
+        }
+      }
+      if (has) fl += kRingLine;
+#else
       if (has) {
         const u32 k = __builtin_amdgcn_mbcnt_hi((u32)(mk >> 32), __builtin_amdgcn_mbcnt_lo((u32)mk, 0u));
         fl_addr[wid][k] = fl;
@@ -1595,6 +1620,7 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
       }
       __builtin_amdgcn_wave_barrier();
       if (has) fl += kRingLine;
+#endif
     }
   }
 #ifdef TPZ_CODEC_STAMPS
