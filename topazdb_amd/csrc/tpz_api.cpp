@@ -123,6 +123,7 @@ struct tpz_workspace {
                                 // [4, 4 + cap) big or codec list, [4 + cap, 4 + 2 cap) spill list,
                                 // [4 + 2 cap, 4 + 3 cap) bigwave list
   uint32_t defer_cap = 0;
+  uint32_t* d_tail = nullptr;   // the decode's tpz::kTailCounters (zero between decodes)
   uint64_t* d_big_scratch = nullptr;
   uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
   uint32_t acc_cap = 0;
@@ -151,6 +152,7 @@ namespace {
 
 void free_workspace(tpz_workspace& w) {
   if (w.d_defer) (void)hipFree(w.d_defer);
+  if (w.d_tail) (void)hipFree(w.d_tail);
   if (w.d_big_scratch) (void)hipFree(w.d_big_scratch);
   if (w.d_acc) (void)hipFree(w.d_acc);
   if (w.d_plan0) (void)hipFree(w.d_plan0);
@@ -197,6 +199,10 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
   tpz_workspace& w = c->ws[stream];
   if (!w.d_big_scratch)
     TPZ_HIP(hipMalloc(&w.d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t)));
+  if (!w.d_tail) {
+    TPZ_HIP(hipMalloc(&w.d_tail, tpz::kTailCounters * sizeof(uint32_t)));
+    TPZ_HIP(hipMemsetAsync(w.d_tail, 0, tpz::kTailCounters * sizeof(uint32_t), (hipStream_t)stream));
+  }
   if (!w.d_defer || w.defer_cap < max_blocks) {
     uint32_t* d = nullptr;
     TPZ_HIP(hipMalloc(&d, (3 * (size_t)max_blocks + 4) * 4));
@@ -319,8 +325,8 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
     tpz_err r = get_workspace(c, stream, b->n_blocks, &w);
     if (r != TPZ_SUCCESS) return r;
   }
+  uint32_t* tail = w->d_tail;
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 16, s));  // the three worklist counters
   tpz::LaunchArgs a{};
   a.src = b->d_src;
   a.ext = b->d_ext;
@@ -332,11 +338,12 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.count = o->d_count;
   a.status = o->d_status;
   a.crc = o->d_crc;
-  a.defer_count = w->d_defer;
+  a.tail = tail;
+  a.defer_count = tail + tpz::kTailBig;
   a.defer_list = w->d_defer + 4;
-  a.spill_count = w->d_defer + 1;
+  a.spill_count = tail + tpz::kTailSpill;
   a.spill_list = w->d_defer + 4 + w->defer_cap;
-  a.bw_count = w->d_defer + 2;
+  a.bw_count = tail + tpz::kTailBw;
   a.bw_list = w->d_defer + 4 + 2 * (size_t)w->defer_cap;
   a.rep = c->d_rep_tables;
   a.spill = o->d_spill;

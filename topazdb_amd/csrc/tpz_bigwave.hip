@@ -44,7 +44,7 @@
 
 namespace tpz {
 
-namespace {
+namespace bw {
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -168,7 +168,6 @@ struct BWParams {
   const u32* rep;           // replicated slice-by-4 tables (kCrcRepWords)
   const u32* tab;           // the decode tables (T_0..T_3 and the inverse table, global)
   const u32* list;
-  const u32* list_count;
   uint8_t* data;
   u32* ends;
   u32* count;
@@ -204,6 +203,15 @@ __device__ __forceinline__ u32 be16_at(const uint8_t* q) { return ((u32)q[0] << 
 
 // A block's header words: lane l < 33 holds block bytes [4 l, 4 l + 4) (n and up to 63 offsets),
 // lane 62 the four bytes of the stored CRC, lane 63 the last four bytes (the tag on top).
+// Wave-uniform reads of memory no kernel of the decode writes while the tail kernel runs (the
+// extents; the bigwave list, complete before it starts): through the constant address space, so
+// they are scalar loads even though the kernel also issues atomics and stores (the compiler
+// otherwise makes them vector loads, whose waits drained the copy pipeline: 64k 2.31 vs 2.11 ms).
+template <class T>
+__device__ __forceinline__ T ld_uniform(const T* base, u64 i) {
+  return reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(base))[i];
+}
+
 __device__ __forceinline__ u32 hdr_load(const BWParams& p, u64 s, u64 e) {
   const u32 lane = lane_id(), len = (u32)(e - s);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -485,10 +493,13 @@ __device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams&
 #endif
 }
 
-__global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p) {
-  const u32 cnt = uni(*p.list_count);
-  if (blockIdx.x * kWaves >= cnt) return;           // an empty list costs one load
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+// The cnt blocks of the bigwave list, one per wave (decode_bigwave_kernel). Wave w of every
+// workgroup takes the blocks i = w (mod kWaves) from its own ticket counter (tickets + 32 w: one
+// counter per 128-byte line), kBwBatch at a time: blocks go to the waves that are free (64k: 1.94
+// against 1.97 ms for the static split), and a counter sees one claim per workgroup at the start,
+// not one per wave. Returns the blocks the wave decoded.
+constexpr u32 kBwBatch = 2;
+__device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u32 cnt, u32* tickets) {
   u32* rep = reinterpret_cast<u32*>(lds);
   for (int i = threadIdx.x; i < kCrcRepWords / 4; i += kThreads)
     reinterpret_cast<uint4*>(rep)[i] = reinterpret_cast<const uint4*>(p.rep)[i];
@@ -501,6 +512,23 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
   Seg* seg = reinterpret_cast<Seg*>(lds + kCrcRepWords * 4 + wid * kWaveLds);
   uint8_t* cmap = reinterpret_cast<uint8_t*>(seg + kSegs);   // kU maps of 64 chunk slots
+  u32* ticket = tickets + 32 * wid;
+  auto claim = [&]() -> u32 {
+    u32 t = 0;
+    if (lane == 0) t = atomicAdd(ticket, 1u);
+    return uni(t);
+  };
+  // the wave's blocks in order: wid + kWaves (kBwBatch k + j) for its claimed batches k
+  u32 gk = claim(), gj = 0;
+  auto next_it = [&]() -> u32 {
+    const u32 r = wid + kWaves * (kBwBatch * gk + gj);
+    if (r < cnt && ++gj == kBwBatch) {
+      gj = 0;
+      gk = claim();
+    }
+    return r;
+  };
+  u32 ndone = 0;
 
 #ifdef TPZ_BW_STAMPS
   u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -509,18 +537,19 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
   // Block i's list entry and extents are loaded during block i - 1 (scalar loads), and its
   // header words (n, the offsets, the stored CRC and the tag) during block i - 1's CRC, so a
   // block's parse starts with two memory round trips (key, then value lengths) instead of six.
-  const u32 stride = gridDim.x * kWaves;
-  u32 it = blockIdx.x * kWaves + wid;
-  if (it >= cnt) return;
-  u32 b = uni(p.list[it]);
-  u64 s = p.ext[b], e = p.ext[b + 1];
+  // The wave holds the tickets of its next two blocks.
+  u32 it = next_it();
+  if (it >= cnt) return 0;
+  u32 itn = next_it();
+  u32 b = uni(ld_uniform(p.list, it));
+  u64 s = ld_uniform(p.ext, b), e = ld_uniform(p.ext, b + 1);
   u32 hw = hdr_load(p, s, e);
-  u32 bn = uni(p.list[it + stride < cnt ? it + stride : it]);
-  for (; it < cnt; it += stride) {
+  u32 bn = uni(ld_uniform(p.list, itn < cnt ? itn : it));
+  for (;;) {
     BW_ST(5);
-    const u32 itn2 = it + 2 * stride;
-    const u32 bnn = uni(p.list[itn2 < cnt ? itn2 : it]);
-    const u64 sn = p.ext[bn], en = p.ext[bn + 1];
+    const u32 itn2 = itn < cnt ? next_it() : itn;
+    const u32 bnn = uni(ld_uniform(p.list, itn2 < cnt ? itn2 : it));
+    const u64 sn = ld_uniform(p.ext, bn), en = ld_uniform(p.ext, bn + 1);
     bool hw_issued = false;
     u32 hwn = 0;
     auto issue_next_header = [&]() {
@@ -677,6 +706,10 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
       put_meta(p, b, st, bcnt, crc);
     }();
     issue_next_header();
+    ndone++;
+    if (itn >= cnt) break;
+    it = itn;
+    itn = itn2;
     b = bn;
     s = sn;
     e = en;
@@ -687,9 +720,10 @@ __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p)
   if (lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&g_bw_stamps[q], (unsigned long long)st_[q]);
 #endif
+  return ndone;
 }
 
-u32 gf_mul_host(u32 a, u32 b) {
+static u32 gf_mul_host(u32 a, u32 b) {
   u32 r = 0;
   for (int i = 0; i < 32; i++) {
     if (a & (0x80000000u >> i)) r ^= b;
@@ -697,7 +731,7 @@ u32 gf_mul_host(u32 a, u32 b) {
   }
   return r;
 }
-u32 x8n_host(u64 nbytes) {                            // x^(8 n) mod P, reflected
+static u32 x8n_host(u64 nbytes) {                            // x^(8 n) mod P, reflected
   u32 r = 0x80000000u, sq = 0x80000000u >> 8;         // x^8
   for (u64 d = nbytes; d; d >>= 1) {
     if (d & 1u) r = gf_mul_host(r, sq);
@@ -705,8 +739,6 @@ u32 x8n_host(u64 nbytes) {                            // x^(8 n) mod P, reflecte
   }
   return r;
 }
-
-}  // namespace
 
 #ifdef TPZ_BW_STAMPS
 extern "C" int tpz_debug_bw_stamps(unsigned long long* out, int reset) {
@@ -719,7 +751,7 @@ extern "C" int tpz_debug_bw_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream) {
+static BWParams bigwave_params(const BigWaveLaunch& a) {
   BWParams p{};
   p.src = a.src;
   p.ext = a.ext;
@@ -727,7 +759,6 @@ void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream) {
   p.rep = a.rep;
   p.tab = a.crc_tables;
   p.list = a.list;
-  p.list_count = a.list_count;
   p.data = a.data;
   p.ends = a.ends;
   p.count = a.count;
@@ -738,12 +769,49 @@ void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream) {
   p.big_list = a.big_list;
   p.big_count = a.big_count;
   p.efirst = a.efirst;
-  for (int l = 0; l < 64; l++) p.lane_shift[l] = x8n_host((u64)kRun * l);
-  for (int l = 0; l < 64; l++) p.step_lane_shift[l] = x8n_host((u64)kStepRun * l);
-  p.step_shift = x8n_host(kStep);
-  p.win_shift = x8n_host(kCrcWin);
-  p.half_shift = x8n_host(kRun / 2);
-  hipLaunchKernelGGL(decode_bigwave_kernel, dim3(a.grid), dim3(kThreads), 0, stream, p);
+  static const struct Shifts {     // computed once (~10^5 GF(2) steps: not per launch)
+    u32 lane[64], step_lane[64], step, win, half;
+    Shifts() {
+      for (int l = 0; l < 64; l++) lane[l] = x8n_host((u64)kRun * l);
+      for (int l = 0; l < 64; l++) step_lane[l] = x8n_host((u64)kStepRun * l);
+      step = x8n_host(kStep);
+      win = x8n_host(kCrcWin);
+      half = x8n_host(kRun / 2);
+    }
+  } sh;
+  for (int l = 0; l < 64; l++) p.lane_shift[l] = sh.lane[l];
+  for (int l = 0; l < 64; l++) p.step_lane_shift[l] = sh.step_lane[l];
+  p.step_shift = sh.step;
+  p.win_shift = sh.win;
+  p.half_shift = sh.half;
+  return p;
+}
+
+// The bigwave list's kernel (before decode_tail_kernel, tpz_decode.hip): one workgroup per CU.
+// (Its own unit on purpose: compiled into tpz_decode.hip, the same loop code ran 10 % slower on
+// the 64k config, profiles/r3/tail_merge.jsonl.)
+__global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p, u32* ctr) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ u32 any;
+  const u32 na = uni(tail_load(ctr + kTailBw));
+  if (!na) return;                                   // an empty list costs one load
+  if (threadIdx.x == 0) {                            // blocks left to claim (else: no table upload)
+    u32 a = 0;
+    for (u32 w = 0; w < (u32)kWaves; w++)
+      a |= w + kWaves * kBwBatch * tail_load(ctr + kTailBwTickets + 32 * w) < na ? 1u : 0u;
+    any = a;
+  }
+  __syncthreads();
+  if (!uni(any)) return;
+  bigwave_phase(p, lds, na, ctr + kTailBwTickets);
+}
+
+}  // namespace bw
+
+void launch_bigwave(const BigWaveLaunch& a, uint32_t* ctr, uint32_t grid, hipStream_t stream) {
+  static_assert(bw::kWaves <= 16, "one ticket counter per wave (tpz_internal.h kTailBwTickets)");
+  hipLaunchKernelGGL(bw::decode_bigwave_kernel, dim3(grid), dim3(bw::kThreads), 0, stream,
+                     bw::bigwave_params(a), ctr);
 }
 
 }  // namespace tpz

@@ -36,6 +36,8 @@
 #include <stdint.h>
 
 #include "tpz_internal.h"
+// the tail kernel's spill phase (namespace tpz::sp), compiled into this unit
+#include "tpz_spill.hip"
 
 namespace tpz {
 
@@ -1100,7 +1102,7 @@ constexpr u32 kOnchipMask = 4095;
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill kernel runs after
+  if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
   load_tables(tab, p.crc_tables);
 
   const u32 wid = uni(threadIdx.x >> 6);
@@ -1490,10 +1492,11 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
   }
 }
 
-__global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
-  const u32 cnt = uni(*p.out.defer_count);
-  if (blockIdx.x >= cnt) return;   // an empty worklist costs one load, not a table upload
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kBigLds];
+// Phase B of decode_tail_kernel: the cnt blocks of the big list, one per workgroup, claimed
+// from the ticket counter (a workgroup only ever waits on blocks that running workgroups hold);
+// *done counts the finished ones. Every thread of the workgroup calls it.
+__device__ __forceinline__ void big_phase(const Params& p, uint8_t* lds, u32 cnt, u32* ticket,
+                                          u32* done, u32* bcast) {
   u32* tab = reinterpret_cast<u32*>(lds);
   load_tables(tab, p.crc_tables);
   const u32 tid = threadIdx.x, wid = uni(tid >> 6), lane = lane_id();
@@ -1507,28 +1510,21 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
   gsum.vb = gsum.kb + kBigMaxGroups;
   gsum.cnt = reinterpret_cast<uint16_t*>(gsum.vb + kBigMaxGroups);
   if (tid < kGuard / 16) reinterpret_cast<uint4*>(win - kGuard)[tid] = make_uint4(0, 0, 0, 0);
-  const u32 grid = gridDim.x;
-  // This workgroup's blocks, 64 at a time: lane l holds the list entry and extent of its block
-  // 64 g + l (list position blockIdx.x + (64 g + l) * grid, clamped to the list).
-  u32 gb;
-  u64 gs, ge;
-  auto load_group = [&](u64 first) {
-    u64 pos = first + (u64)lane * grid;
-    pos = pos < cnt ? pos : cnt - 1;
-    gb = p.out.defer_list[pos];
-    gs = p.ext[gb];
-    ge = p.ext[gb + 1];
+  auto claim = [&]() -> u32 {
+    __syncthreads();
+    if (tid == 0) *bcast = atomicAdd(ticket, 1u);
+    __syncthreads();
+    return uni(*bcast);
   };
-  auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
   // The next block's bytes are loaded into registers while this one decodes (16 B x <= 6 per
   // thread); workgroup barriers only wait for LDS, so the loads stay in flight across them.
   uint4 t[kBigStage];
   u32 b_nx = 0;
   u64 s_nx = 0, e_nx = 0;
-  auto issue = [&](u32 k) {
-    b_nx = readlane(gb, k & 63);
-    s_nx = lane64(gs, k & 63);
-    e_nx = lane64(ge, k & 63);
+  auto issue = [&](u32 it) {
+    b_nx = uni(p.out.defer_list[it]);
+    s_nx = p.ext[b_nx];
+    e_nx = p.ext[b_nx + 1];
     const u64 ws = s_nx & ~15ull;
     const u32 nbytes = (u32)(e_nx - ws);
     const u64 e16 = (e_nx + 15) & ~(u64)15;
@@ -1540,14 +1536,15 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
                           : make_uint4(0, 0, 0, 0);
     }
   };
-  load_group(blockIdx.x);
-  issue(0);
+  const u32 it0 = claim();
+  if (it0 >= cnt) return;
+  issue(it0);
+  u32 nxt = claim();                       // the block after the one in flight
   Stamps S;
 #ifdef TPZ_ABL_STAMPS
   S.last = stamp_now();
 #endif
-  u32 k = 0;
-  for (u32 it = blockIdx.x; it < cnt; it += grid, k++) {
+  for (;;) {
     const u32 b = b_nx;
     const u64 s = s_nx, e = e_nx;
     const u32 len = (u32)(e - s);
@@ -1570,39 +1567,85 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_big_kernel(Params p) {
     }
     __syncthreads();
     TPZ_STAMP(S, 0);
-    if ((u64)it + grid < cnt) {
-      if (((k + 1) & 63) == 0) load_group((u64)it + grid);
-      issue(k + 1);
-    }
-    const u32 a0 = (u32)(s & 15u);
+    const bool more = nxt < cnt;
+    if (more) issue(nxt);
+    [&]() {
+      const u32 a0 = (u32)(s & 15u);
 #ifdef TPZ_ABL_LOADONLY
-    if (wid == 0) put_meta(p.out, b, TPZ_BLOCK_OK, win[a0], 0);
-    continue;
+      if (wid == 0) put_meta(p.out, b, TPZ_BLOCK_OK, win[a0], 0);
+      return;
 #endif
-    const u32 tag = win[(int)(a0 + len) - 1];                                  // compress.rs:99
-    const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));    // block.rs:51
-    const u32 n = lds_be16(win, a0);                                           // block.rs:54
-    u32 st0 = 0;
-    if (len == 0) st0 = TPZ_BLOCK_EMPTY;                                       // compress.rs:96
-    else if (tag == 0 || tag > 3) st0 = TPZ_BLOCK_BAD_TAG;                      // :44-53,102
-    else if (tag != 1) st0 = TPZ_BLOCK_UNSUPPORTED_CODEC;
-    else if (len - 1 < 4) st0 = TPZ_BLOCK_MALFORMED;                            // block.rs:49
-    if (st0) {
-      if (wid == 0) put_meta(p.out, b, st0, 0, 0);
-      continue;
-    }
-    if (2 * n + 1 <= (u32)kBigLdsSlots)
-      big_block<ColLds, false>(p, tab, win, ColLds{ltab}, map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
-    else
-      big_block<ColBig, true>(p, tab, win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
-                              map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
+      const u32 tag = win[(int)(a0 + len) - 1];                                  // compress.rs:99
+      const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));    // block.rs:51
+      const u32 n = lds_be16(win, a0);                                           // block.rs:54
+      u32 st0 = 0;
+      if (len == 0) st0 = TPZ_BLOCK_EMPTY;                                       // compress.rs:96
+      else if (tag == 0 || tag > 3) st0 = TPZ_BLOCK_BAD_TAG;                      // :44-53,102
+      else if (tag != 1) st0 = TPZ_BLOCK_UNSUPPORTED_CODEC;
+      else if (len - 1 < 4) st0 = TPZ_BLOCK_MALFORMED;                            // block.rs:49
+      if (st0) {
+        if (wid == 0) put_meta(p.out, b, st0, 0, 0);
+        return;
+      }
+      if (2 * n + 1 <= (u32)kBigLdsSlots)
+        big_block<ColLds, false>(p, tab, win, ColLds{ltab}, map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
+      else
+        big_block<ColBig, true>(p, tab, win, ColBig{p.big_scratch + (u64)blockIdx.x * 2 * kBigMaxSlots},
+                                map, gsum, wmax, xs, a0, len, n, stored, b, s, S);
+    }();
     TPZ_STAMP(S, 5);
+    __threadfence();                       // the block's outputs and spill-list entry, then its count
+    __syncthreads();
+    if (tid == 0) atomicAdd(done, 1u);
+    if (!more) break;
+    nxt = claim();
   }
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kBigWaves + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
     for (int q = 0; q < 6; q++) g_stamps[(kStampWaves + gw) * 8 + q] = S.t[q];
 #endif
+  (void)lane;
+}
+
+// Everything after the wave path, in one launch (an empty worklist costs a counter load, not a
+// launch): A, the bigwave list (it may hand blocks with 64+ entries to the big list and blocks
+// with bad entries to the spill list); B, the big list (it may hand blocks to the spill list);
+// C, the spill list. A phase starts once every block of the one before is done; blocks are
+// claimed from ticket counters, so a workgroup only waits on blocks running workgroups hold.
+constexpr int kTailLds = (int)sizeof(sp::SpillLds) > kBigLds ? (int)sizeof(sp::SpillLds) : kBigLds;
+static_assert(kTailLds + 16 <= 163840, "tail LDS");
+static_assert(sp::kThreads == kBigThreads, "tail workgroup shape");
+
+__global__ __launch_bounds__(kBigThreads, 1) void decode_tail_kernel(Params p, sp::SpillParams spp,
+                                                                    u32* ctr) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kTailLds];
+  __shared__ u32 bcast;
+  // whether blocks of a phase are left to claim (a workgroup that finds none skips the phase's
+  // table upload)
+  auto open = [&](const u32* ticket, u32 n) -> bool {
+    __syncthreads();
+    if (threadIdx.x == 0) bcast = tail_load(ticket) < n ? 1u : 0u;
+    __syncthreads();
+    return uni(bcast) != 0;
+  };
+  // both list lengths in one round trip (the bigwave kernel before this one has appended to them);
+  // the spill list is read again only after the big phase, which can append to it
+  const u32 nb = uni(tail_load(ctr + kTailBig)), nc0 = uni(tail_load(ctr + kTailSpill));
+  if (nb) {
+    if (open(ctr + kTailBigTicket, nb)) big_phase(p, lds, nb, ctr + kTailBigTicket, ctr + kTailBigDone, &bcast);
+    tail_wait(ctr + kTailBigDone, nb);
+  }
+  const u32 nc = nb ? uni(tail_load(ctr + kTailSpill)) : nc0;
+  if (nc && open(ctr + kTailSpillTicket, nc)) sp::spill_phase(spp, lds, nc, ctr + kTailSpillTicket);
+  // the last workgroup out zeroes the counters (the bigwave tickets included) for the next decode
+  // on the stream: no memset launch, and a captured graph replays correctly
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(ctr + kTailExit, 1u) == gridDim.x - 1) {
+    for (int i = 0; i < kTailBwTickets; i++) __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int w = 0; w < 16; w++)
+      __hip_atomic_store(ctr + kTailBwTickets + 32 * w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // x^(8 * 5120 r) mod P (reflected), r < kBigSuper: bit by bit from x^0 (0x80000000).
@@ -1654,17 +1697,16 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
-  if (a.bw_list) {
-    // before the big kernel: it may hand a block with 64+ entries to the big list
-    BigWaveLaunch bw{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.bw_count,
-                     a.data, a.ends, a.count, a.status, a.crc, a.spill_list, a.spill_count,
-                     a.defer_list, a.defer_count, a.num_cus, a.efirst};
-    launch_bigwave(bw, stream);
-  }
-  hipLaunchKernelGGL(decode_big_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p);
-  SpillLaunch sp{a.src, a.ext, a.src_bytes, a.crc_tables, a.spill_list, a.spill_count, a.spill,
-                 a.spill_cap, a.spill_off, a.spill_used, a.count, a.status, a.crc, a.num_cus};
-  launch_spill(sp, stream);
+  if (a.bw_list)
+    launch_bigwave(BigWaveLaunch{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.data, a.ends,
+                                 a.count, a.status, a.crc, a.spill_list, a.spill_count, a.defer_list,
+                                 a.defer_count, a.efirst},
+                   a.tail, a.big_grid, stream);
+  const sp::SpillParams spp = sp::spill_params(SpillLaunch{a.src, a.ext, a.src_bytes, a.crc_tables,
+                                                           a.spill_list, a.spill, a.spill_cap,
+                                                           a.spill_off, a.spill_used, a.count,
+                                                           a.status, a.crc});
+  hipLaunchKernelGGL(decode_tail_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p, spp, a.tail);
 }
 
 }  // namespace tpz

@@ -80,20 +80,22 @@ struct LaunchArgs {
   uint8_t* status;
   uint32_t* crc;
   uint32_t* defer_list;   // workspace: n_blocks entries
-  uint32_t* defer_count;  // workspace: one u32, zeroed before the launch
+  uint32_t* defer_count;  // tail + kTailBig
   uint32_t num_cus;
   uint64_t* big_scratch;  // big_grid x 2 x kBigMaxSlots
   uint32_t big_grid;
   uint32_t* spill_list;   // workspace: n_blocks entries (blocks for the spill path)
-  uint32_t* spill_count;  // workspace: one u32, zeroed before the launch
+  uint32_t* spill_count;  // tail + kTailSpill
   uint8_t* spill;         // the caller's spill arena (tpz_columns)
   uint64_t spill_cap;
   uint64_t* spill_off;
   uint64_t* spill_used;   // zeroed before the launch
   uint32_t* bw_list;      // workspace: n_blocks entries (blocks for the bigwave kernel)
-  uint32_t* bw_count;     // workspace: one u32, zeroed before the launch
-  const uint32_t* rep;    // replicated slice-by-4 tables (the bigwave kernel's CRC)
+  uint32_t* bw_count;     // tail + kTailBw
+  const uint32_t* rep;    // replicated slice-by-4 tables (the bigwave phase's CRC)
   const uint64_t* efirst; // exact ends layout (tpz_columns.d_entry_first) or null
+  uint32_t* tail;         // workspace: kTailCounters, zero at the launch (the tail kernel
+                          // leaves them zero)
 };
 // Pair index of block b's first {kend, vend}: the exact layout's d_entry_first[b], or the
 // slotted tpz_entry_base.
@@ -103,6 +105,31 @@ __host__ __device__ inline uint64_t ends_base(const uint64_t* efirst, uint64_t e
 
 void launch_decode(const LaunchArgs& a, hipStream_t stream);
 
+// The decode's worklist counters (tpz_decode.hip decode_tail_kernel): zero before a decode, and
+// zeroed again by the tail kernel's last workgroup.
+enum TailCounter : int {
+  kTailBig = 0,        // big list length
+  kTailSpill,          // spill list length
+  kTailBw,             // bigwave list length
+  kTailBigTicket,      // big blocks claimed
+  kTailBigDone,        // big blocks finished
+  kTailSpillTicket,    // spill blocks claimed
+  kTailExit,           // tail-kernel workgroups finished
+  kTailBwTickets = 32, // 16 bigwave ticket counters (wave w's at 32 w: one per 128-byte line)
+  kTailCounters = kTailBwTickets + 32 * 16
+};
+__device__ __forceinline__ uint32_t tail_load(const uint32_t* c) {
+  return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every thread of the workgroup: wait until *done reaches n, then see what the finished blocks
+// wrote. Bounded (about a second), so a counting bug cannot hang the device.
+__device__ __forceinline__ void tail_wait(const uint32_t* done, uint32_t n) {
+  if (threadIdx.x == 0)
+    for (uint32_t i = 0; i < (1u << 22) && tail_load(done) < n; i++) __builtin_amdgcn_s_sleep(2);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 // Long blocks with few entries (tpz_bigwave.hip): one wave per block, straight from HBM.
 struct BigWaveLaunch {
   const uint8_t* src;
@@ -111,7 +138,6 @@ struct BigWaveLaunch {
   const uint32_t* rep;          // replicated slice-by-4 tables
   const uint32_t* crc_tables;   // the decode tables (small shifts, inverse table)
   const uint32_t* list;
-  const uint32_t* list_count;
   uint8_t* data;
   uint32_t* ends;
   uint32_t* count;
@@ -121,19 +147,19 @@ struct BigWaveLaunch {
   uint32_t* spill_count;
   uint32_t* big_list;
   uint32_t* big_count;
-  uint32_t grid;
   const uint64_t* efirst;
 };
-void launch_bigwave(const BigWaveLaunch& a, hipStream_t stream);
+// Launched between the wave kernel and decode_tail_kernel; ctr = the decode's tail counters.
+void launch_bigwave(const BigWaveLaunch& a, uint32_t* ctr, uint32_t grid, hipStream_t stream);
 
-// The spill path (tpz_spill.hip): blocks the LDS paths hand over, decoded into the arena.
+// The spill path (tpz_spill.hip, phase C of the tail kernel): blocks the LDS paths hand over,
+// decoded into the arena.
 struct SpillLaunch {
   const uint8_t* src;
   const uint64_t* ext;
   uint64_t src_bytes;
   const uint32_t* crc_tables;
   const uint32_t* list;
-  const uint32_t* list_count;
   uint8_t* spill;
   uint64_t spill_cap;
   uint64_t* spill_off;
@@ -141,9 +167,7 @@ struct SpillLaunch {
   uint32_t* count;
   uint8_t* status;
   uint32_t* crc;
-  uint32_t grid;
 };
-void launch_spill(const SpillLaunch& a, hipStream_t stream);
 
 struct CrcLaunch {
   const uint8_t* src;

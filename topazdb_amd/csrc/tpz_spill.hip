@@ -36,7 +36,8 @@
 
 namespace tpz {
 
-namespace {
+// Compiled as part of tpz_decode.hip (its decode_tail_kernel runs spill_phase).
+namespace sp {
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -66,7 +67,6 @@ struct SpillParams {
   u64 src_bytes;
   const u32* tables;     // the decode tables; ids 0..15 = T_0..T_15 (slice-by-16)
   const u32* list;       // spill worklist
-  const u32* list_count;
   uint8_t* spill;
   u64 spill_cap;
   u64* spill_off;
@@ -193,160 +193,181 @@ __device__ __forceinline__ void put_meta(const SpillParams& p, u32 b, u32 st, u3
   }
 }
 
-__global__ __launch_bounds__(kThreads, 1) void decode_spill_kernel(SpillParams p) {
-  const u32 cnt = *p.list_count;
-  if (blockIdx.x >= cnt) return;                     // nothing to do: no table load
-  __shared__ u32 tab[16 * 256];
-  __shared__ u64 red[kWaves];
-  __shared__ u64 shared_off;
-  __shared__ u32 e_kst[kThreads], e_vst[kThreads];  // this round's key/value stream starts
-  const u32 tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
-  for (u32 i = tid; i < 16 * 256; i += kThreads) tab[i] = p.tables[i];
-  __syncthreads();
+// The phase's LDS (carved from decode_tail_kernel's buffer).
+struct SpillLds {
+  u32 tab[16 * 256];
+  u64 red[kWaves];
+  u64 shared_off;
+  u32 e_kst[kThreads], e_vst[kThreads];  // this round's key/value stream starts
+  u32 ticket;
+};
 
-  for (u32 it = blockIdx.x; it < cnt; it += gridDim.x) {
-    const u32 b = p.list[it];
-    const u64 s = p.ext[b], e = p.ext[b + 1], len = e - s;
-    const uint8_t* blk = p.src + s;
-    // compress::decode tag dispatch (compress.rs:95-113), the CRC split (block.rs:49-51)
-    const u32 tag = len ? blk[len - 1] : 0u;
-    if (len == 0 || tag == 0 || tag > 3 || tag != 1 || len - 1 < 4) {
-      put_meta(p, b, len == 0 ? TPZ_BLOCK_EMPTY
-                     : (tag == 0 || tag > 3) ? TPZ_BLOCK_BAD_TAG
-                     : tag != 1 ? TPZ_BLOCK_UNSUPPORTED_CODEC : TPZ_BLOCK_MALFORMED, 0, 0);
-      continue;
-    }
-    const u64 P = len - 5;
-    const u32 stored = (u32)blk[P] << 24 | (u32)blk[P + 1] << 16 | (u32)blk[P + 2] << 8 | blk[P + 3];
+// One spill-list entry (list position it) by the whole workgroup.
+__device__ __forceinline__ void spill_block(const SpillParams& p, SpillLds& L, u32 it) {
+  u32* tab = L.tab;
+  u64* red = L.red;
+  u32* e_kst = L.e_kst;
+  u32* e_vst = L.e_vst;
+  const u32 tid = threadIdx.x, wid = tid >> 6;
+  const u32 b = p.list[it];
+  const u64 s = p.ext[b], e = p.ext[b + 1], len = e - s;
+  const uint8_t* blk = p.src + s;
+  // compress::decode tag dispatch (compress.rs:95-113), the CRC split (block.rs:49-51)
+  const u32 tag = len ? blk[len - 1] : 0u;
+  if (len == 0 || tag == 0 || tag > 3 || tag != 1 || len - 1 < 4) {
+    put_meta(p, b, len == 0 ? TPZ_BLOCK_EMPTY
+                   : (tag == 0 || tag > 3) ? TPZ_BLOCK_BAD_TAG
+                   : tag != 1 ? TPZ_BLOCK_UNSUPPORTED_CODEC : TPZ_BLOCK_MALFORMED, 0, 0);
+    return;
+  }
+  const u64 P = len - 5;
+  const u32 stored = (u32)blk[P] << 24 | (u32)blk[P + 1] << 16 | (u32)blk[P + 2] << 8 | blk[P + 3];
 
-    // ---- CRC-32 of the payload [s, s + P) (checksum.rs:6-21)
-    const u64 A0 = s & ~15ull, Aend = s + P;
-    const u64 npc = (Aend - A0 + 15) >> 4;             // 16-byte pieces from A0
-    const u64 pp = (npc + kThreads - 1) / kThreads;
-    const u64 k0 = (u64)tid * pp, k1 = k0 + pp < npc ? k0 + pp : npc;
-    // the thread's own descriptor starts at its first piece, so a block of any length is read
-    // whole (a thread's run is npc / 1024 pieces: under 2 GiB for blocks under 2 TiB)
-    const u64 T0 = A0 + 16 * k0;
-    u64 rem = p.src_bytes > T0 ? p.src_bytes - T0 : 0;
-    rem = rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(p.src + T0), (short)0, (int)rem, 0x00020000);
-    u32 c = 0;
-    for (u64 k = k0; k < k1; k++) {
-      const u64 a = A0 + 16 * k;
-      uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(16 * (k - k0)), 0, 0));
-      if (a < s) {                                     // bytes before the payload: zero (a raw
-        const u32 z = (u32)(s - a);                    // CRC ignores leading zeros)
-        u32 w[4] = {v.x, v.y, v.z, v.w};
+  // ---- CRC-32 of the payload [s, s + P) (checksum.rs:6-21)
+  const u64 A0 = s & ~15ull, Aend = s + P;
+  const u64 npc = (Aend - A0 + 15) >> 4;             // 16-byte pieces from A0
+  const u64 pp = (npc + kThreads - 1) / kThreads;
+  const u64 k0 = (u64)tid * pp, k1 = k0 + pp < npc ? k0 + pp : npc;
+  // the thread's own descriptor starts at its first piece, so a block of any length is read
+  // whole (a thread's run is npc / 1024 pieces: under 2 GiB for blocks under 2 TiB)
+  const u64 T0 = A0 + 16 * k0;
+  u64 rem = p.src_bytes > T0 ? p.src_bytes - T0 : 0;
+  rem = rem < 0x7FFFFFF0ull ? rem : 0x7FFFFFF0ull;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src + T0), (short)0, (int)rem, 0x00020000);
+  u32 c = 0;
+  for (u64 k = k0; k < k1; k++) {
+    const u64 a = A0 + 16 * k;
+    uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(16 * (k - k0)), 0, 0));
+    if (a < s) {                                     // bytes before the payload: zero (a raw
+      const u32 z = (u32)(s - a);                    // CRC ignores leading zeros)
+      u32 w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int lo = 4 * q;
-          const u32 m = (int)z >= lo + 4 ? 0u : ((int)z <= lo ? ~0u : (~0u << (8 * (z - lo))));
-          w[q] &= m;
-        }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
+      for (int q = 0; q < 4; q++) {
+        const int lo = 4 * q;
+        const u32 m = (int)z >= lo + 4 ? 0u : ((int)z <= lo ? ~0u : (~0u << (8 * (z - lo))));
+        w[q] &= m;
       }
-      if (a + 16 <= Aend) {
-        c = slice16(tab, v.x ^ c, v.y, v.z, v.w);
-      } else {                                         // the payload's last piece
-        const u32 w[4] = {v.x, v.y, v.z, v.w};
-        for (u32 j = 0; j < (u32)(Aend - a); j++) {
-          const u32 byte = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
-          c = (c >> 8) ^ tab[(c ^ byte) & 0xFF];
-        }
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (a + 16 <= Aend) {
+      c = slice16(tab, v.x ^ c, v.y, v.z, v.w);
+    } else {                                         // the payload's last piece
+      const u32 w[4] = {v.x, v.y, v.z, v.w};
+      for (u32 j = 0; j < (u32)(Aend - a); j++) {
+        const u32 byte = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
+        c = (c >> 8) ^ tab[(c ^ byte) & 0xFF];
       }
     }
-    u32 contrib = 0;
-    if (k0 < k1) {
-      const u64 end_t = A0 + 16 * k1 < Aend ? A0 + 16 * k1 : Aend;
-      contrib = Aend == end_t ? c : gf_mul(x8n(p, Aend - end_t), c);
-    }
-    const u32 R = wg_xor(contrib, red);
-    const u32 crc = ~(R ^ gf_mul(x8n(p, P), 0xFFFFFFFFu));
-    if (crc != stored) {                                                         // checksum.rs:17
-      put_meta(p, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc);
-      continue;
-    }
-    // ---- n and the offsets (block.rs:54-59)
-    if (P < 2) {
-      put_meta(p, b, TPZ_BLOCK_MALFORMED, 0, crc);
-      continue;
-    }
-    const u32 n = be16(blk);
-    if (P < 2 + 2 * (u64)n) {
-      put_meta(p, b, TPZ_BLOCK_MALFORMED, 0, crc);
-      continue;
-    }
-    const u64 db = 2 + 2 * (u64)n, dl = P - db;
-    // ---- pass 1: every entry's bounds (iterator.rs:74-82) and the key/value totals
-    u64 kt = 0, vt = 0, bad = 0;
-    for (u32 i = tid; i < n; i += kThreads) {
-      const Entry en = parse(blk, db, dl, i);
-      kt += en.kl;
-      vt += en.vl;
-      bad |= en.cls != TPZ_ENTRY_OK ? 1u : 0u;
-    }
-    const u64 K = wg_sum64(kt, red), V = wg_sum64(vt, red), B = wg_sum64(bad, red);
-    // ---- the record: ends, then the stream (keys | values from value_start(K)), then for a
-    // block with bad entries their classes (Ok(Block) either way: block.rs:46-65)
-    const u64 need = spill_record_bytes(n, K, V) + (B ? (((u64)n + 127u) & ~127ull) : 0u);
-    if (tid == 0) {
-      const u64 off = atomicAdd(reinterpret_cast<unsigned long long*>(p.spill_used),
-                                (unsigned long long)need);
-      const bool fits = off + need <= p.spill_cap;
-      shared_off = fits ? off : ~0ull;
-      p.spill_off[b] = fits ? off : need;
+  }
+  u32 contrib = 0;
+  if (k0 < k1) {
+    const u64 end_t = A0 + 16 * k1 < Aend ? A0 + 16 * k1 : Aend;
+    contrib = Aend == end_t ? c : gf_mul(x8n(p, Aend - end_t), c);
+  }
+  const u32 R = wg_xor(contrib, red);
+  const u32 crc = ~(R ^ gf_mul(x8n(p, P), 0xFFFFFFFFu));
+  if (crc != stored) {                                                         // checksum.rs:17
+    put_meta(p, b, TPZ_BLOCK_CHECKSUM_MISMATCH, 0, crc);
+    return;
+  }
+  // ---- n and the offsets (block.rs:54-59)
+  if (P < 2) {
+    put_meta(p, b, TPZ_BLOCK_MALFORMED, 0, crc);
+    return;
+  }
+  const u32 n = be16(blk);
+  if (P < 2 + 2 * (u64)n) {
+    put_meta(p, b, TPZ_BLOCK_MALFORMED, 0, crc);
+    return;
+  }
+  const u64 db = 2 + 2 * (u64)n, dl = P - db;
+  // ---- pass 1: every entry's bounds (iterator.rs:74-82) and the key/value totals
+  u64 kt = 0, vt = 0, bad = 0;
+  for (u32 i = tid; i < n; i += kThreads) {
+    const Entry en = parse(blk, db, dl, i);
+    kt += en.kl;
+    vt += en.vl;
+    bad |= en.cls != TPZ_ENTRY_OK ? 1u : 0u;
+  }
+  const u64 K = wg_sum64(kt, red), V = wg_sum64(vt, red), B = wg_sum64(bad, red);
+  // ---- the record: ends, then the stream (keys | values from value_start(K)), then for a
+  // block with bad entries their classes (Ok(Block) either way: block.rs:46-65)
+  const u64 need = spill_record_bytes(n, K, V) + (B ? (((u64)n + 127u) & ~127ull) : 0u);
+  if (tid == 0) {
+    const u64 off = atomicAdd(reinterpret_cast<unsigned long long*>(p.spill_used),
+                              (unsigned long long)need);
+    const bool fits = off + need <= p.spill_cap;
+    L.shared_off = fits ? off : ~0ull;
+    p.spill_off[b] = fits ? off : need;
+  }
+  __syncthreads();
+  const u64 roff = L.shared_off;
+  if (roff == ~0ull) {
+    put_meta(p, b, TPZ_BLOCK_SPILL_FULL, n, crc);
+    return;
+  }
+  u32* ends = reinterpret_cast<u32*>(p.spill + roff);
+  uint8_t* stream = p.spill + roff + spill_stream(n);
+  uint8_t* classes = p.spill + roff + spill_record_bytes(n, K, V);
+  const u64 vs = value_start(K);
+  u32 kc = 0, vc = 0;
+  for (u32 r0 = 0; r0 < n; r0 += kThreads) {
+    const u32 i = r0 + tid;
+    const Entry en = i < n ? parse(blk, db, dl, i) : Entry{0, 0, 0, TPZ_ENTRY_OK};
+    u32 ktot, vtot;
+    const u32 ki = wg_scan(en.kl, red, ktot) + kc;
+    const u32 vi = wg_scan(en.vl, red, vtot) + vc;
+    if (i < n) {
+      *reinterpret_cast<uint2*>(ends + 2 * (u64)i) = make_uint2(ki, vi);
+      if (B) classes[i] = (uint8_t)en.cls;
+      e_kst[tid] = ki - en.kl;
+      e_vst[tid] = vi - en.vl;
     }
     __syncthreads();
-    const u64 roff = shared_off;
-    if (roff == ~0ull) {
-      put_meta(p, b, TPZ_BLOCK_SPILL_FULL, n, crc);
-      continue;
+    // one wave per entry: its key, then its value (src/block/iterator.rs:78-82)
+    const u32 m = n - r0 < (u32)kThreads ? n - r0 : (u32)kThreads;
+    for (u32 j = wid; j < m; j += kWaves) {
+      const Entry ej = parse(blk, db, dl, r0 + j);
+      wave_copy(stream + e_kst[j], blk + db + ej.off + 2, ej.kl);
+      wave_copy(stream + vs + e_vst[j], blk + db + ej.off + 4 + ej.kl, ej.vl);
     }
-    u32* ends = reinterpret_cast<u32*>(p.spill + roff);
-    uint8_t* stream = p.spill + roff + spill_stream(n);
-    uint8_t* classes = p.spill + roff + spill_record_bytes(n, K, V);
-    const u64 vs = value_start(K);
-    u32 kc = 0, vc = 0;
-    for (u32 r0 = 0; r0 < n; r0 += kThreads) {
-      const u32 i = r0 + tid;
-      const Entry en = i < n ? parse(blk, db, dl, i) : Entry{0, 0, 0, TPZ_ENTRY_OK};
-      u32 ktot, vtot;
-      const u32 ki = wg_scan(en.kl, red, ktot) + kc;
-      const u32 vi = wg_scan(en.vl, red, vtot) + vc;
-      if (i < n) {
-        *reinterpret_cast<uint2*>(ends + 2 * (u64)i) = make_uint2(ki, vi);
-        if (B) classes[i] = (uint8_t)en.cls;
-        e_kst[tid] = ki - en.kl;
-        e_vst[tid] = vi - en.vl;
-      }
-      __syncthreads();
-      // one wave per entry: its key, then its value (src/block/iterator.rs:78-82)
-      const u32 m = n - r0 < (u32)kThreads ? n - r0 : (u32)kThreads;
-      for (u32 j = wid; j < m; j += kWaves) {
-        const Entry ej = parse(blk, db, dl, r0 + j);
-        wave_copy(stream + e_kst[j], blk + db + ej.off + 2, ej.kl);
-        wave_copy(stream + vs + e_vst[j], blk + db + ej.off + 4 + ej.kl, ej.vl);
-      }
-      kc += ktot;
-      vc += vtot;
-      __syncthreads();
-    }
-    put_meta(p, b, B ? TPZ_BLOCK_BAD_ENTRY : TPZ_BLOCK_OK_SPILLED, n, crc);
-    (void)lane;
+    kc += ktot;
+    vc += vtot;
+    __syncthreads();
   }
+  put_meta(p, b, B ? TPZ_BLOCK_BAD_ENTRY : TPZ_BLOCK_OK_SPILLED, n, crc);
 }
 
-}  // namespace
+// Phase C of decode_tail_kernel (tpz_decode.hip): the cnt blocks of the spill list, one per
+// workgroup, claimed from the ticket counter. Every thread of the workgroup calls it.
+__device__ __forceinline__ void spill_phase(const SpillParams& p, uint8_t* lds_bytes, u32 cnt,
+                                            u32* ticket) {
+  SpillLds& L = *reinterpret_cast<SpillLds*>(lds_bytes);
+  u32* tab = L.tab;
+  u64* red = L.red;
+  const u32 tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+  for (u32 i = tid; i < 16 * 256; i += kThreads) tab[i] = p.tables[i];
 
-void launch_spill(const SpillLaunch& a, hipStream_t stream) {
+  for (;;) {
+    __syncthreads();                                  // the previous block's LDS reads are done
+    if (tid == 0) L.ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const u32 it = __builtin_amdgcn_readfirstlane(L.ticket);
+    if (it >= cnt) break;
+    spill_block(p, L, it);
+  }
+  (void)lane;
+  (void)wid;
+}
+
+SpillParams spill_params(const SpillLaunch& a) {
   SpillParams p{};
   p.src = a.src;
   p.ext = a.ext;
   p.src_bytes = a.src_bytes;
   p.tables = a.crc_tables;
   p.list = a.list;
-  p.list_count = a.list_count;
   p.spill = a.spill;
   p.spill_cap = a.spill ? a.spill_cap : 0;
   p.spill_off = a.spill_off;
@@ -366,7 +387,8 @@ void launch_spill(const SpillLaunch& a, hipStream_t stream) {
     }
     x = r;
   }
-  hipLaunchKernelGGL(decode_spill_kernel, dim3(a.grid), dim3(kThreads), 0, stream, p);
+  return p;
 }
 
+}  // namespace sp
 }  // namespace tpz
