@@ -1,11 +1,11 @@
 // tpz_bigwave.hip — gfx950 kernel for long blocks with few entries (the 64 KiB config:
 // block_size 65536, 61 entries of 32-B keys and 1 KiB values), one wavefront per block.
 //
-// The LDS big path (decode_big_kernel) stages a whole block in a 92 KiB window, so a CU holds one
-// block at a time and its CRC, parse and copy run back to back with the next block's bytes only in
-// flight: 0.31 of the HBM roofline on the 64k config, 0.35 for its memory skeleton alone. Here
-// nothing is staged. Each wave of a 16-wave workgroup decodes its own block straight from HBM,
-// so a CU keeps 16 blocks in flight:
+// The LDS big path (tpz_decode.hip, the tail kernel's big phase) stages a whole block in a 92 KiB
+// window, so a CU holds one block at a time and its CRC, parse and copy run back to back with the
+// next block's bytes only in flight: 0.31 of the HBM roofline on the 64k config, 0.35 for its
+// memory skeleton alone. Here nothing is staged. Each wave of a 16-wave workgroup decodes its own
+// block straight from HBM, so a CU keeps 16 blocks in flight:
 //   * parse (Block::decode, src/block.rs:46-65, and BlockIterator::seek_to's bounds checks,
 //     src/block/iterator.rs:74-82): lane i reads offset i, then key and value lengths, from
 //     global memory; DPP-free shuffles scan them into the {kend, vend} ends and a per-wave entry
