@@ -54,6 +54,10 @@ constexpr int kWavesPerWG = 12;
 constexpr int kWavesPerWG = 16;
 #endif
 constexpr int kWGThreads = kWave * kWavesPerWG;
+// Blocks a wave of the wave path claims at a time (decode_wave_kernel): 2^chunk_shift, chosen
+// per launch (launch_decode); TPZ_WAVE_CHUNK forces one (diagnostic builds).
+static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
+constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
@@ -1091,6 +1095,7 @@ struct Params {
   Out out;
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
+  u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
 };
 
 // ------------------------------------------------------------------ wave path kernel
@@ -1099,10 +1104,19 @@ struct Params {
 // stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
 constexpr u32 kOnchipMask = 4095;
 #endif
+#ifdef TPZ_ABL_WAVEENDS
+// diagnostic: each wave's start and end time (s_memrealtime, 100 MHz) and block count
+__device__ unsigned long long g_wave_ends[3 * 8192];
+#endif
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
+  __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
+  if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
+#ifdef TPZ_ABL_WAVEENDS
+  const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   load_tables(tab, p.crc_tables);
 
   const u32 wid = uni(threadIdx.x >> 6);
@@ -1119,22 +1133,40 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   const u32 nw = gridDim.x * kWavesPerWG;
-  u32 b = blockIdx.x * kWavesPerWG + wid;
   Stamps S;
 #ifdef TPZ_ABL_STAMPS
   S.last = stamp_now();
 #endif
 
-  // Extents of this wave's blocks, 64 at a time: lane l of a group holds ext[] of the wave's
-  // block 64 g + l (block index b0 + k nw). The next group is loaded one group ahead with vector
-  // loads that complete behind the block prefetch, so a block's extent is two readlanes instead
-  // of a memory round trip on the critical path.
-  const u32 b0 = b;
+  // The workgroup's blocks are the rows q nw + kWavesPerWG blockIdx.x + [0, kWavesPerWG), in
+  // chunks of kChunk consecutive blocks. A wave takes the next chunk from an LDS counter when it
+  // finishes one: the waves of a CU do not run at one speed (with a fixed block per wave, the
+  // first four waves of each workgroup finished at 1.66 ms and the last four at 2.21 ms of a
+  // 2.26 ms launch, tools/wave_ends.py), so a fixed split left the fast waves idle while the slow
+  // ones finished. Lane l of a chunk's extent group holds ext[] of the chunk's block l (loaded
+  // one chunk ahead, so a block's extent is two readlanes instead of a memory round trip).
+#ifdef TPZ_WAVE_CHUNK
+  const u32 cshift = __builtin_ctz((u32)TPZ_WAVE_CHUNK);
+#else
+  const u32 cshift = uni(p.chunk_shift);
+#endif
+  const u32 kChunk = 1u << cshift, rshift = kRowShift - cshift;   // chunks per row: 2^rshift
+  // (saturated at n_blocks: a chunk past the batch is empty)
+  const u32 row0 = blockIdx.x * kWavesPerWG;
+  auto chunk_first = [&](u32 q) -> u32 {
+    const u64 f = (u64)(q >> rshift) * nw + row0 + ((q & ((1u << rshift) - 1u)) << cshift);
+    return f < p.n_blocks ? (u32)f : p.n_blocks;
+  };
+  auto claim_chunk = [&]() -> u32 {
+    u32 q = 0;
+    if (lane == 0) q = atomicAdd(&chunk_next, 1u);
+    return uni(q);
+  };
   u64 gs_cur, ge_cur, gs_nxt, ge_nxt;
-  auto load_group = [&](u32 g, u64& gs, u64& ge) {
-    // lanes past the batch re-read the last extent (unconditional: the load writes its
-    // destination registers directly, nothing waits for it until the group is used)
-    u64 bb = (u64)b0 + ((u64)g * 64 + lane) * nw;
+  auto load_group = [&](u32 q, u64& gs, u64& ge) {
+    // lanes past the chunk or the batch re-read an extent (unconditional: the loads write their
+    // destination registers directly, nothing waits for them until the chunk is used)
+    u32 bb = chunk_first(q) + (lane < kChunk ? lane : 0u);
     bb = bb < p.n_blocks ? bb : p.n_blocks - 1;
 #ifdef TPZ_ABL_ONCHIP
     bb &= kOnchipMask;   // timing build: the same 4096 blocks over and over (L2/MALL-resident)
@@ -1143,13 +1175,12 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     ge = p.ext[bb + 1];
   };
   auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
-  // Blocks that do not fit a wave slot are sent to their worklist when their extent group
-  // becomes current, 64 at a time: fewer than 64 entries -> the one-wave-per-block kernel,
-  // past the big path's window -> the spill path, else the LDS big path. The decode loop then
-  // skips them.
-  auto triage_group = [&](u32 g, u64 gs, u64 ge) {
-    const u64 bb = (u64)b0 + ((u64)g * 64 + lane) * nw;
-    const bool lng = bb < p.n_blocks && ge - gs > kWaveMaxLen;
+  // Blocks that do not fit a wave slot are sent to their worklist when their chunk becomes
+  // current: fewer than 64 entries -> the one-wave-per-block kernel, past the big path's window
+  // -> the spill path, else the LDS big path. The decode loop then skips them.
+  auto triage_group = [&](u32 q, u64 gs, u64 ge) {
+    const u32 cf = chunk_first(q), bb = cf + lane;     // (lane < n_blocks - cf: no wrap)
+    const bool lng = lane < kChunk && lane < p.n_blocks - cf && ge - gs > kWaveMaxLen;
     if (!__ballot(lng)) return;
     u32 nent = 0xFFFFu;
     if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
@@ -1159,17 +1190,20 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     defer_lanes(p.out.spill_list, p.out.spill_count, to_spill, (u32)bb);
     defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
-  load_group(0, gs_cur, ge_cur);
-  load_group(1, gs_nxt, ge_nxt);
-  triage_group(0, gs_cur, ge_cur);
+  u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
+  load_group(q_cur, gs_cur, ge_cur);
+  load_group(q_nxt, gs_nxt, ge_nxt);
+  triage_group(q_cur, gs_cur, ge_cur);
+  u32 j = 0;                              // the block's position in its chunk
+  u32 b = chunk_first(q_cur);
 
   // prefetch state for block b
   uint4 v[kWinRounds];
   u64 s_cur = 0, e_cur = 0;
-  auto issue = [&](u32 bb, u32 k, u64& s, u64& e) {
+  auto issue = [&](u32 bb, u32 jj, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
-    s = lane64(gs_cur, k & 63);
-    e = lane64(ge_cur, k & 63);
+    s = lane64(gs_cur, jj);
+    e = lane64(ge_cur, jj);
     const u64 len = e - s;
     if (len > kWaveMaxLen) return;
     const u64 ws = s & ~15ull;
@@ -1192,7 +1226,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
         if ((u32)r < rounds) fix_tail(v[r], p.src, ws + r * 1024 + lane * 16, p.src_bytes);
     }
   };
+#ifdef TPZ_ABL_WAVEENDS
   u32 k = 0;  // this wave's block counter
+#endif
   PendingCrc pd{0u, 0u, 0u, 0u, 0u, 0u, 0u};
   issue(b, 0, s_cur, e_cur);
   vm_pad<kVmAfter>(p.out);
@@ -1211,15 +1247,21 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     }
     TPZ_STAMP(S, 0);
     const u32 bcur = b;
-    b += nw;
+#ifdef TPZ_ABL_WAVEENDS
     k++;
-    if ((k & 63) == 0) {             // next extent group (its loads completed long ago)
+#endif
+    if (++j == kChunk) {              // next chunk (its extent loads completed long ago)
+      j = 0;
+      q_cur = q_nxt;
       gs_cur = gs_nxt;
       ge_cur = ge_nxt;
-      load_group((k >> 6) + 1, gs_nxt, ge_nxt);
-      triage_group(k >> 6, gs_cur, ge_cur);
+      q_nxt = claim_chunk();
+      load_group(q_nxt, gs_nxt, ge_nxt);
+      triage_group(q_cur, gs_cur, ge_cur);
     }
-    issue(b, k, s_cur, e_cur);       // next block's loads fly while this one decodes
+    b = chunk_first(q_cur) + j;
+    b = b < p.n_blocks ? b : p.n_blocks;
+    issue(b, j, s_cur, e_cur);       // next block's loads fly while this one decodes
     vm_pad<kVmAfter>(p.out);
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
@@ -1236,6 +1278,17 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     TPZ_STAMP(S, 5);
   }
   finish_pending(tab, p.out, pd);    // the wave's last block
+#ifdef TPZ_ABL_WAVEENDS
+  {
+    const u32 gw = blockIdx.x * kWavesPerWG + wid;
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && gw < 8192) {
+      g_wave_ends[3 * gw] = we_t0;
+      g_wave_ends[3 * gw + 1] = t1;
+      g_wave_ends[3 * gw + 2] = k;
+    }
+  }
+#endif
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kWavesPerWG + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
@@ -1693,6 +1746,14 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   const u32* ls = lane_run_shifts();
   for (int l = 0; l < 64; l++) p.lane_shift[l] = ls[l];
+  // Blocks claimed at a time by a wave of the wave path: single blocks balance the waves of a CU
+  // best (the first waves issue first; same box, 4k: 1.875 ms with 1, 1.89 with 2 or 4, 1.95
+  // with 16, 2.10 with a fixed split; zipf 2.04 against 2.28). A batch of long blocks (the 64k
+  // config, where the wave path only routes blocks to the bigwave kernel) takes whole rows: its
+  // per-chunk extent and header round trips are not hidden by any decode (64k: 2.07 ms with 16,
+  // 2.20 with 4, 2.78 with 1; profiles/r3/wave_chunks.jsonl).
+  const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
+  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
@@ -1711,6 +1772,12 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
 
 }  // namespace tpz
 
+#ifdef TPZ_ABL_WAVEENDS
+extern "C" int tpz_debug_wave_ends(unsigned long long* host, int n_waves) {
+  if (n_waves > 8192) n_waves = 8192;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tpz::g_wave_ends), (size_t)n_waves * 3 * 8);
+}
+#endif
 #ifdef TPZ_ABL_STAMPS
 // Diagnostic build only: copies the per-wave phase sums (8 u64 per wave, 6 used) to the host.
 extern "C" int tpz_debug_stamps(unsigned long long* host, int n_waves) {
