@@ -676,19 +676,36 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
   for (int i = threadIdx.x; i < kTableBytes / 16; i += kEncThreads)
     reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(p.crc_tables)[i];
   for (int i = lane; i < kEncGuard / 16; i += kWave) reinterpret_cast<uint4*>(slot)[i] = make_uint4(0, 0, 0, 0);
+  __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
+  if (threadIdx.x == 0) chunk_next = 0;
   __syncthreads();
 
   const u32 nwaves = gridDim.x * kEncWaves;
-  const u32 wv = blockIdx.x * kEncWaves + wid;
   // a plan with a rejected entry (tpz_plan_blocks_async) encodes nothing
   const u32 n_blocks = !p.plan_info ? p.n_blocks : (uni(p.plan_info[1]) != ~0u ? 0u : uni(p.plan_info[2]));
-  if (wv >= n_blocks) return;
-  const u32 nmine = (n_blocks - 1 - wv) / nwaves + 1;       // blocks wv + i * nwaves
-
-  auto load_group = [&](u32 g, BlockMeta& m) {
-    const u32 i = g * kWave + lane;
-    if (i < nmine) {
-      const u32 b = wv + i * nwaves;
+  // The workgroup's blocks are the rows r nwaves + kEncWaves blockIdx.x + [0, kEncWaves), in
+  // chunks of kEncChunk; a wave takes the next chunk from an LDS counter when it finishes one
+  // (the waves of a CU do not run at one speed: the decode's wave path, tpz_decode.hip). Lane l
+  // of a chunk's group holds first[] / ext[] of the chunk's block l.
+#ifndef TPZ_ENC_CHUNK
+#define TPZ_ENC_CHUNK 4
+#endif
+  constexpr u32 kEncChunk = TPZ_ENC_CHUNK, kPerRow = kEncWaves / kEncChunk;
+  static_assert(kEncWaves % kEncChunk == 0 && kEncChunk >= 2, "block i + 2 is in the next chunk at most");
+  const u32 row0 = blockIdx.x * kEncWaves;
+  auto chunk_first = [&](u32 q) -> u32 {
+    const u64 f = (u64)(q / kPerRow) * nwaves + row0 + (q % kPerRow) * kEncChunk;
+    return f < n_blocks ? (u32)f : n_blocks;
+  };
+  auto claim_chunk = [&]() -> u32 {
+    u32 q = 0;
+    if (lane == 0) q = atomicAdd(&chunk_next, 1u);
+    return uni(q);
+  };
+  auto load_group = [&](u32 q, BlockMeta& m) {
+    const u32 cf = chunk_first(q);
+    if (lane < kEncChunk && lane < n_blocks - cf) {
+      const u32 b = cf + lane;
       m.a = p.first[b];
       m.e = p.first[b + 1];
       m.o0 = p.ext[b];
@@ -703,29 +720,34 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     r.o1 = ((u64)readlane((u32)(m.o1 >> 32), (int)l) << 32) | readlane((u32)m.o1, (int)l);
     return r;
   };
-  BlockMeta gA{0, 0, 0, 0}, gB{0, 0, 0, 0};                 // groups i / 64 and i / 64 + 1
-  load_group(0, gA);
-  load_group(1, gB);
-  auto meta_of = [&](u32 j, u32 g) { return (j / kWave == g) ? pick(gA, j & 63) : pick(gB, j & 63); };
+  BlockMeta gA{0, 0, 0, 0}, gB{0, 0, 0, 0};                 // chunks qa and qb
+  u32 qa = claim_chunk(), qb = claim_chunk();
+  load_group(qa, gA);
+  load_group(qb, gB);
+  u32 fa = chunk_first(qa), fb = chunk_first(qb);
+  // block t of the wave's two chunks (t < 2 kEncChunk): its index (n_blocks: none) and meta
+  auto block_of = [&](u32 t) -> u32 {
+    const u32 bb = t < kEncChunk ? fa + t : fb + (t - kEncChunk);
+    return bb < n_blocks ? bb : n_blocks;
+  };
+  auto meta_of = [&](u32 t) { return t < kEncChunk ? pick(gA, t) : pick(gB, t - kEncChunk); };
+  if (block_of(0) >= n_blocks) return;
 
-  BlockMeta m0 = meta_of(0, 0), m1 = meta_of(1 < nmine ? 1 : 0, 0);
+  const bool has1 = block_of(1) < n_blocks;
+  BlockMeta m0 = meta_of(0), m1 = meta_of(has1 ? 1 : 0);
   EntryRegs cur = load_entry(p, m0.a, m0.e, true);
-  EntryRegs nxt = load_entry(p, m1.a, m1.e, 1 < nmine);
+  EntryRegs nxt = load_entry(p, m1.a, m1.e, has1);
   u128 pf[kPre];
   issue_pieces(p, cur, pf);
 
-  for (u32 i = 0; i < nmine; i++) {
-    const u32 g = i / kWave;
-    if (i && (i & 63) == 0) {
-      gA = gB;
-      load_group(g + 1, gB);
-    }
-    const BlockMeta m = meta_of(i, g);
-    const bool has2 = i + 2 < nmine;
-    const BlockMeta m2 = meta_of(has2 ? i + 2 : i, g);
+  for (u32 j = 0;;) {                                        // block j of chunk qa
+    const u32 b = block_of(j);
+    if (b >= n_blocks) break;
+    const BlockMeta m = meta_of(j);
+    const bool has2 = block_of(j + 2) < n_blocks;
+    const BlockMeta m2 = meta_of(has2 ? j + 2 : j);
     const EntryRegs nn = load_entry(p, m2.a, m2.e, has2);   // block i + 2's kpos / vpos
 
-    const u32 b = wv + i * nwaves;
     const u32 a = m.a, nb = m.e - m.a;
     const u64 o0 = m.o0;
     const u32 A = (u32)(o0 & 15);
@@ -795,6 +817,15 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     }
     cur = nxt;
     nxt = nn;
+    if (++j == kEncChunk) {          // next chunk (its meta loaded a chunk ago)
+      j = 0;
+      qa = qb;
+      fa = fb;
+      gA = gB;
+      qb = claim_chunk();
+      fb = chunk_first(qb);
+      load_group(qb, gB);
+    }
   }
 }
 
