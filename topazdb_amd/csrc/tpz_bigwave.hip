@@ -493,13 +493,12 @@ __device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams&
 #endif
 }
 
-// The cnt blocks of the bigwave list, one per wave (decode_bigwave_kernel). Wave w of every
-// workgroup takes the blocks i = w (mod kWaves) from its own ticket counter (tickets + 32 w: one
-// counter per 128-byte line), kBwBatch at a time: blocks go to the waves that are free (64k: 1.94
-// against 1.97 ms for the static split), and a counter sees one claim per workgroup at the start,
-// not one per wave. Returns the blocks the wave decoded.
-constexpr u32 kBwBatch = 2;
-__device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u32 cnt, u32* tickets) {
+// The list entries [lo, hi) (this workgroup's share of the bigwave list), one block per wave:
+// waves claim them one at a time from an LDS counter (*pool, starting at lo), so a CU's faster
+// waves take more blocks (its waves do not run at one speed: tpz_decode.hip decode_wave_kernel).
+// Returns the blocks the wave decoded.
+__device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u32 lo, u32 cnt,
+                                             u32* pool) {
   u32* rep = reinterpret_cast<u32*>(lds);
   for (int i = threadIdx.x; i < kCrcRepWords / 4; i += kThreads)
     reinterpret_cast<uint4*>(rep)[i] = reinterpret_cast<const uint4*>(p.rep)[i];
@@ -512,21 +511,10 @@ __device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u3
   const u32 wid = uni(threadIdx.x >> 6), lane = lane_id();
   Seg* seg = reinterpret_cast<Seg*>(lds + kCrcRepWords * 4 + wid * kWaveLds);
   uint8_t* cmap = reinterpret_cast<uint8_t*>(seg + kSegs);   // kU maps of 64 chunk slots
-  u32* ticket = tickets + 32 * wid;
-  auto claim = [&]() -> u32 {
+  auto next_it = [&]() -> u32 {        // the next entry, or >= cnt: none left
     u32 t = 0;
-    if (lane == 0) t = atomicAdd(ticket, 1u);
+    if (lane == 0) t = atomicAdd(pool, 1u);
     return uni(t);
-  };
-  // the wave's blocks in order: wid + kWaves (kBwBatch k + j) for its claimed batches k
-  u32 gk = claim(), gj = 0;
-  auto next_it = [&]() -> u32 {
-    const u32 r = wid + kWaves * (kBwBatch * gk + gj);
-    if (r < cnt && ++gj == kBwBatch) {
-      gj = 0;
-      gk = claim();
-    }
-    return r;
   };
   u32 ndone = 0;
 
@@ -537,7 +525,7 @@ __device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u3
   // Block i's list entry and extents are loaded during block i - 1 (scalar loads), and its
   // header words (n, the offsets, the stored CRC and the tag) during block i - 1's CRC, so a
   // block's parse starts with two memory round trips (key, then value lengths) instead of six.
-  // The wave holds the tickets of its next two blocks.
+  // The wave holds the entries of its next two blocks.
   u32 it = next_it();
   if (it >= cnt) return 0;
   u32 itn = next_it();
@@ -792,24 +780,19 @@ static BWParams bigwave_params(const BigWaveLaunch& a) {
 // the 64k config, profiles/r3/tail_merge.jsonl.)
 __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p, u32* ctr) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  __shared__ u32 any;
+  __shared__ u32 pool;
   const u32 na = uni(tail_load(ctr + kTailBw));
-  if (!na) return;                                   // an empty list costs one load
-  if (threadIdx.x == 0) {                            // blocks left to claim (else: no table upload)
-    u32 a = 0;
-    for (u32 w = 0; w < (u32)kWaves; w++)
-      a |= w + kWaves * kBwBatch * tail_load(ctr + kTailBwTickets + 32 * w) < na ? 1u : 0u;
-    any = a;
-  }
-  __syncthreads();
-  if (!uni(any)) return;
-  bigwave_phase(p, lds, na, ctr + kTailBwTickets);
+  // this workgroup's share of the list: entries [lo, hi)
+  const u32 per = (na + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * per;
+  const u32 hi = lo + per < na ? lo + per : na;
+  if (lo >= hi) return;                              // an empty list costs one load
+  if (threadIdx.x == 0) pool = lo;                   // (the table upload's barrier publishes it)
+  bigwave_phase(p, lds, lo, hi, &pool);
 }
 
 }  // namespace bw
 
 void launch_bigwave(const BigWaveLaunch& a, uint32_t* ctr, uint32_t grid, hipStream_t stream) {
-  static_assert(bw::kWaves <= 16, "one ticket counter per wave (tpz_internal.h kTailBwTickets)");
   hipLaunchKernelGGL(bw::decode_bigwave_kernel, dim3(grid), dim3(bw::kThreads), 0, stream,
                      bw::bigwave_params(a), ctr);
 }

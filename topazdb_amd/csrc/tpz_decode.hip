@@ -1691,14 +1691,11 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_tail_kernel(Params p, s
   }
   const u32 nc = nb ? uni(tail_load(ctr + kTailSpill)) : nc0;
   if (nc && open(ctr + kTailSpillTicket, nc)) sp::spill_phase(spp, lds, nc, ctr + kTailSpillTicket);
-  // the last workgroup out zeroes the counters (the bigwave tickets included) for the next decode
-  // on the stream: no memset launch, and a captured graph replays correctly
+  // the last workgroup out zeroes the counters for the next decode on the stream: no memset
+  // launch, and a captured graph replays correctly
   __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(ctr + kTailExit, 1u) == gridDim.x - 1) {
-    for (int i = 0; i < kTailBwTickets; i++) __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int w = 0; w < 16; w++)
-      __hip_atomic_store(ctr + kTailBwTickets + 32 * w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0 && atomicAdd(ctr + kTailExit, 1u) == gridDim.x - 1)
+    for (int i = 0; i < kTailCounters; i++) __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // x^(8 * 5120 r) mod P (reflected), r < kBigSuper: bit by bit from x^0 (0x80000000).

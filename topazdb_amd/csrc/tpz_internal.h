@@ -115,8 +115,7 @@ enum TailCounter : int {
   kTailBigDone,        // big blocks finished
   kTailSpillTicket,    // spill blocks claimed
   kTailExit,           // tail-kernel workgroups finished
-  kTailBwTickets = 32, // 16 bigwave ticket counters (wave w's at 32 w: one per 128-byte line)
-  kTailCounters = kTailBwTickets + 32 * 16
+  kTailCounters
 };
 __device__ __forceinline__ uint32_t tail_load(const uint32_t* c) {
   return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
