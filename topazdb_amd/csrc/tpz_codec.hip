@@ -1347,7 +1347,20 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
   u64 trips = 0, gtrips = 0, elems = 0;
 #endif
 
+  // Every block of the batch is in flight at once, one per lane, so no wave can take over the
+  // blocks of a slower one: the kernel lasts as long as its slowest waves. The issue arbiter
+  // favours the oldest wave, so the waves of a CU do not progress at one speed (the decode's wave
+  // path: the first four finished 0.58 ms before the last four). The wave's priority rotates
+  // every trip instead (offset per wave): snappy 1.19/1.15 -> 1.14/1.12 ms, LZ4 1.23 -> 1.19 ms
+  // per 2^18 4kc blocks (profiles/r3/wave_chunks.jsonl).
+  u32 rot = blockIdx.x * 4u + (threadIdx.x >> 6);
   while (__ballot(live)) {
+    switch (uni(rot++) & 3u) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
 #ifdef TPZ_CODEC_STAMPS
     trips++;
 #endif

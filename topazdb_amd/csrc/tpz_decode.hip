@@ -1233,7 +1233,18 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   issue(b, 0, s_cur, e_cur);
   vm_pad<kVmAfter>(p.out);
 
+#ifdef TPZ_ABL_ROTPRIO   // diagnostic: rotate the wave's issue priority every block
+  u32 rot = blockIdx.x * kWavesPerWG + wid;
+#endif
   while (b < p.n_blocks) {
+#ifdef TPZ_ABL_ROTPRIO
+    switch (uni(rot++) & 3u) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#endif
     const u64 s = s_cur, e = e_cur;
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
     const bool fits = (e - s) <= kWaveMaxLen;
