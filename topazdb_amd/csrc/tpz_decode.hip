@@ -1096,6 +1096,7 @@ struct Params {
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
   u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
+  u32* wave_ctr;      // (diagnostic XGLOBAL builds) the global chunk counter, a tail counter
 };
 
 // ------------------------------------------------------------------ wave path kernel
@@ -1113,6 +1114,16 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   u32* tab = reinterpret_cast<u32*>(lds);
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
+#ifdef TPZ_ABL_XGLOBAL
+  __shared__ u32 gchunk[8], gready[8];
+  if (threadIdx.x < 8) gready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    gchunk[0] = atomicAdd(p.wave_ctr, 1u);
+    gready[0] = 1;
+    gchunk[1] = atomicAdd(p.wave_ctr, 1u);
+    gready[1] = 2;
+  }
+#endif
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1153,6 +1164,33 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 kChunk = 1u << cshift, rshift = kRowShift - cshift;   // chunks per row: 2^rshift
   // (saturated at n_blocks: a chunk past the batch is empty)
   const u32 row0 = blockIdx.x * kWavesPerWG;
+#ifdef TPZ_ABL_XGLOBAL
+  // diagnostic: single blocks from global 64-block chunks (claimed by the workgroups in turn,
+  // each published two chunks ahead), so the balance is across CUs too
+  (void)rshift;
+  (void)row0;
+  auto chunk_first = [&](u32 q) -> u32 { return q < p.n_blocks ? q : p.n_blocks; };
+  auto claim_chunk = [&]() -> u32 {
+    u32 t = 0;
+    if (lane == 0) t = atomicAdd(&chunk_next, 1u);
+    t = uni(t);
+    const u32 k = t >> 6, j = t & 63u;
+    if (j == 32u) {
+      u32 g = 0;
+      if (lane == 0) g = atomicAdd(p.wave_ctr, 1u);
+      g = uni(g);
+      if (lane == 0) {
+        __hip_atomic_store(&gchunk[(k + 2) & 7u], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&gready[(k + 2) & 7u], k + 3, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    for (u32 i = 0; i < (1u << 24); i++)
+      if (uni(__hip_atomic_load(&gready[k & 7u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == k + 1) break;
+    const u32 g = uni(__hip_atomic_load(&gchunk[k & 7u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    const u64 bb = (u64)g * 64 + j;
+    return bb < p.n_blocks ? (u32)bb : p.n_blocks;
+  };
+#else
   auto chunk_first = [&](u32 q) -> u32 {
     const u64 f = (u64)(q >> rshift) * nw + row0 + ((q & ((1u << rshift) - 1u)) << cshift);
     return f < p.n_blocks ? (u32)f : p.n_blocks;
@@ -1162,6 +1200,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     return uni(q);
   };
+#endif
   u64 gs_cur, ge_cur, gs_nxt, ge_nxt;
   auto load_group = [&](u32 q, u64& gs, u64& ge) {
     // lanes past the chunk or the batch re-read an extent (unconditional: the loads write their
@@ -1191,6 +1230,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
   u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
+#ifdef TPZ_ABL_CLAIM2
+  u32 q_nxt2 = claim_chunk();   // diagnostic: the claim one chunk further ahead
+#endif
   load_group(q_cur, gs_cur, ge_cur);
   load_group(q_nxt, gs_nxt, ge_nxt);
   triage_group(q_cur, gs_cur, ge_cur);
@@ -1266,7 +1308,12 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       q_cur = q_nxt;
       gs_cur = gs_nxt;
       ge_cur = ge_nxt;
+#ifdef TPZ_ABL_CLAIM2
+      q_nxt = q_nxt2;
+      q_nxt2 = claim_chunk();
+#else
       q_nxt = claim_chunk();
+#endif
       load_group(q_nxt, gs_nxt, ge_nxt);
       triage_group(q_cur, gs_cur, ge_cur);
     }
@@ -1762,6 +1809,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // 2.20 with 4, 2.78 with 1; profiles/r3/wave_chunks.jsonl).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
   p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
+  p.wave_ctr = a.tail + kTailWave;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;

@@ -115,6 +115,7 @@ enum TailCounter : int {
   kTailBigDone,        // big blocks finished
   kTailSpillTicket,    // spill blocks claimed
   kTailExit,           // tail-kernel workgroups finished
+  kTailWave,           // (diagnostic builds) the wave path's global chunk counter
   kTailCounters
 };
 __device__ __forceinline__ uint32_t tail_load(const uint32_t* c) {
