@@ -1355,7 +1355,11 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
   // per 2^18 4kc blocks (profiles/r3/wave_chunks.jsonl).
   u32 rot = blockIdx.x * 4u + (threadIdx.x >> 6);
   while (__ballot(live)) {
+#ifdef TPZ_CODEC_ROT2   // diagnostic: rotate every second trip
+    switch ((uni(rot++) >> 1) & 3u) {
+#else
     switch (uni(rot++) & 3u) {
+#endif
       case 0: __builtin_amdgcn_s_setprio(0); break;
       case 1: __builtin_amdgcn_s_setprio(1); break;
       case 2: __builtin_amdgcn_s_setprio(2); break;

@@ -740,9 +740,20 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
   u128 pf[kPre];
   issue_pieces(p, cur, pf);
 
+#ifdef TPZ_ENC_ABL_ROTPRIO   // diagnostic: rotate the wave's issue priority every block
+  u32 rot = blockIdx.x * kEncWaves + wid;
+#endif
   for (u32 j = 0;;) {                                        // block j of chunk qa
     const u32 b = block_of(j);
     if (b >= n_blocks) break;
+#ifdef TPZ_ENC_ABL_ROTPRIO
+    switch (uni(rot++) & 3u) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3); break;
+    }
+#endif
     const BlockMeta m = meta_of(j);
     const bool has2 = block_of(j + 2) < n_blocks;
     const BlockMeta m2 = meta_of(has2 ? j + 2 : j);
