@@ -58,7 +58,8 @@ typedef enum {
   TPZ_ERR_INVALID_ARG = -1, /* null pointer, inconsistent sizes                               */
   TPZ_ERR_HIP = -2,         /* a HIP runtime call failed (tpz_last_error has the text)        */
   TPZ_ERR_NO_DEVICE = -3,   /* no gfx950 device with that index                               */
-  TPZ_ERR_NOMEM = -4
+  TPZ_ERR_NOMEM = -4,
+  TPZ_ERR_INTERNAL = -5     /* a device-side consistency check failed (tpz_decode_check)      */
 } tpz_err;
 
 /* ---- per-block outcome (written to columns.status[i]) ------------------------------------
@@ -242,7 +243,10 @@ void tpz_ctx_destroy(tpz_ctx* ctx);
 
 /* Pre-sizes the device workspace `stream` uses for batches of up to max_blocks blocks, so that
  * tpz_decode_blocks on that stream never allocates (needed before capturing it in a hipGraph).
- * Each stream gets its own workspace, so decodes on different streams may run concurrently. */
+ * Each stream gets its own workspace, so decodes on different streams may run concurrently.
+ * Every call on one stream reuses that stream's workspace (worklists, plan buffers and the
+ * pinned word tpz_plan_blocks reads back): calls that share a stream must not be made from
+ * several host threads at once. Give each host thread its own stream. */
 tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
 
 /* ---- the hot path ------------------------------------------------------------------------ */
@@ -251,6 +255,14 @@ tpz_err tpz_ctx_reserve(tpz_ctx* ctx, uint32_t max_blocks, void* stream);
  * block: that is data, not an API failure). */
 tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* out,
                           void* stream);
+
+/* Synchronizes `stream` and reports whether every decode on it so far ran to completion:
+ * TPZ_ERR_INTERNAL (and the flag cleared) when a tail workgroup's bounded wait for the big
+ * path timed out, so that blocks of the spill worklist may have been left undecoded (their
+ * status/count/crc are then unspecified). The wait only times out if the device stalls for
+ * about a second; a caller that cannot trust its outputs otherwise checks after each batch
+ * (tpz_decode_blocks_host and the Python layer do). */
+tpz_err tpz_decode_check(tpz_ctx* ctx, void* stream);
 
 /* The exact ends layout. The slotted ends reserve the worst case (a pair per 6 input bytes,
  * ~1.36x the input in ends alone for 4 KiB blocks) so that blocks need no prefix pass; a caller

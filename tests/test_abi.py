@@ -202,3 +202,54 @@ def test_unaligned_src_is_rejected():
         _lib.ERR_INVALID_ARG
     assert L.tpz_decompressed_sizes(C.c_void_p(0x10), C.byref(b), C.c_void_p(0x8000), None) == \
         _lib.ERR_INVALID_ARG
+
+
+def _host_bound(blocks: list[bytes]) -> int:
+    src = np.frombuffer(b"".join(blocks) or b"\0", np.uint8).copy()
+    ext = np.zeros(len(blocks) + 1, np.uint64)
+    ext[1:] = np.cumsum([len(b) for b in blocks])
+    out = C.c_uint64()
+    _lib.check(_lib.lib().tpz_host_decoded_bound(src.ctypes.data, ext.ctypes.data, len(blocks),
+                                                  C.byref(out)), "tpz_host_decoded_bound")
+    return out.value
+
+
+def _varint(v: int, pad_to: int = 0) -> bytes:
+    """LEB128 of v, padded with redundant continuation bytes to pad_to bytes (snap accepts up
+    to 10 bytes)."""
+    out = []
+    while True:
+        out.append(v & 0x7F)
+        v >>= 7
+        if not v:
+            break
+    while len(out) < pad_to:
+        out.append(0)
+    return bytes([b | 0x80 for b in out[:-1]] + [out[-1]])
+
+
+@pytest.mark.parametrize("value,nbytes", [(0, 1), (300, 2), (300, 6), (4000, 10), (0xFFFFFFFF, 5),
+                                          (0xFFFFFFFF, 10), (1 << 32, 5), (1 << 40, 7)])
+def test_host_decoded_bound_follows_snaps_header_rule(value, nbytes):
+    """tpz_host_decoded_bound on a snappy block reads the varint preamble the way snap does
+    (compress.rs:104-107 -> snap's Header: up to 10 bytes, a value past u32 is TooBig) and
+    agrees with the oracle's header parse: a block snap rejects decodes to 1 byte (its tag-0
+    form), one it accepts to its declared length + the tag byte (VERDICT r3 weak #8)."""
+    pre = _varint(value, nbytes)
+    assert len(pre) == nbytes
+    blk = pre + b"\x00" * 4 + b"\x02"                 # preamble, some body bytes, tag 2
+    want = C.c_uint64()
+    body = np.frombuffer(blk[:-1], np.uint8).copy()
+    ok = O.lib().tpzo_snappy_uncompressed_len(body.ctypes.data, len(body), C.byref(want)) == 0
+    assert ok == (value <= 0xFFFFFFFF)
+    assert _host_bound([blk]) == (want.value + 1 if ok else 1)
+
+
+def test_host_decoded_bound_truncated_and_other_tags():
+    trunc = b"\x80\x80\x80" + b"\x02"                  # varint never ends inside the block
+    eleven = b"\x80" * 10 + b"\x01" + b"\x02"          # 11 varint bytes: snap's Header error
+    lz4 = (1000).to_bytes(4, "little") + b"\x00" * 3 + b"\x03"
+    plain = b"\x00" * 20 + b"\x01"
+    assert _host_bound([trunc]) == 1 and _host_bound([eleven]) == 1
+    assert _host_bound([lz4]) == 1001 and _host_bound([plain]) == 21
+    assert _host_bound([trunc, lz4, plain, b""]) == 1 + 1001 + 21 + 0

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TPZ_LIB_PATH") or os.path.join(HERE, "libtpz_gpu.so")
 HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 
 # tpz_err
-SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4
+SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
  BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR, BLOCK_BAD_ENTRY) = range(10)
@@ -97,6 +97,8 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(Columns),
                                         C.c_void_p]
         L.tpz_decode_blocks.restype = C.c_int
+        L.tpz_decode_check.argtypes = [C.c_void_p, C.c_void_p]
+        L.tpz_decode_check.restype = C.c_int
         for f in ("tpz_crc32_ranges",):
             getattr(L, f).argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
             getattr(L, f).restype = C.c_int
@@ -247,6 +249,11 @@ class Context:
         c = Columns(*[cols[f] for f in COLUMN_FIELDS])
         check(lib().tpz_decode_blocks(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks")
+
+    def decode_check(self, stream: int = 0) -> None:
+        """tpz_decode_check: synchronizes the stream; raises TpzError if a decode on it did not
+        run to completion (a tail workgroup's bounded wait timed out)."""
+        check(lib().tpz_decode_check(self.handle, C.c_void_p(stream)), "tpz_decode_check")
 
     def entry_first_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
                          d_first: int, stream: int = 0) -> None:

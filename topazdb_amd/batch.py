@@ -96,12 +96,15 @@ class SlottedColumns:
         grows the arena to what the spilled blocks asked for and decodes the batch again."""
         torch.cuda.synchronize(_dev(self.device))
         if self._decoded is not None:
+            ctx, batch, stream = self._decoded
+            sid = _stream_id(ctx, stream)
+            ctx.decode_check(sid)
             used = int(self.spill_used.cpu()[0])
             if used > self.spill_cap:
-                ctx, batch, stream = self._decoded
                 self.set_spill_cap(used)
                 decode_batch(ctx, batch, self, stream)
                 torch.cuda.synchronize(_dev(self.device))
+                ctx.decode_check(sid)
         return self
 
     def meta_host(self):
@@ -220,6 +223,11 @@ class DenseDecode:
             out.append((self.keys[self.kpos[e]:self.kpos[e + 1]].tobytes(),
                         self.vals[self.vpos[e]:self.vpos[e + 1]].tobytes()))
         return out
+
+
+def _stream_id(ctx: Context, stream: torch.cuda.Stream | None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
+    return s.cuda_stream
 
 
 def decode_batch(ctx: Context, batch: DeviceBatch, cols: SlottedColumns | None = None,

@@ -123,7 +123,8 @@ struct tpz_workspace {
                                 // [4, 4 + cap) big or codec list, [4 + cap, 4 + 2 cap) spill list,
                                 // [4 + 2 cap, 4 + 3 cap) bigwave list
   uint32_t defer_cap = 0;
-  uint32_t* d_tail = nullptr;   // the decode's tpz::kTailCounters (zero between decodes)
+  uint32_t* d_tail = nullptr;   // the decode's tpz::kTailCounters (zero between decodes) + the
+                                // sticky tpz::kTailError word
   uint64_t* d_big_scratch = nullptr;
   uint32_t* d_acc = nullptr;    // acc_cap per-range accumulators of tpz_crc32_ranges
   uint32_t acc_cap = 0;
@@ -200,8 +201,8 @@ tpz_err get_workspace(tpz_ctx* c, void* stream, uint32_t max_blocks, tpz_workspa
   if (!w.d_big_scratch)
     TPZ_HIP(hipMalloc(&w.d_big_scratch, (size_t)c->num_cus * 2 * tpz::kBigMaxSlots * sizeof(uint64_t)));
   if (!w.d_tail) {
-    TPZ_HIP(hipMalloc(&w.d_tail, tpz::kTailCounters * sizeof(uint32_t)));
-    TPZ_HIP(hipMemsetAsync(w.d_tail, 0, tpz::kTailCounters * sizeof(uint32_t), (hipStream_t)stream));
+    TPZ_HIP(hipMalloc(&w.d_tail, tpz::kTailWords * sizeof(uint32_t)));
+    TPZ_HIP(hipMemsetAsync(w.d_tail, 0, tpz::kTailWords * sizeof(uint32_t), (hipStream_t)stream));
   }
   if (!w.d_defer || w.defer_cap < max_blocks) {
     uint32_t* d = nullptr;
@@ -234,6 +235,10 @@ void tpz_internal_pipe_release(tpz_ctx* c, void* pipe, bool fresh) {
   c->pipes_free.push_back(pipe);
 }
 tpz_err tpz_internal_hip_fail(hipError_t e, const char* what) { return hip_fail(e, what); }
+tpz_err tpz_internal_fail(tpz_err err, const char* what) {
+  g_last_error = what;
+  return err;
+}
 
 extern "C" {
 
@@ -357,6 +362,26 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   tpz::launch_decode(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
+}
+
+tpz_err tpz_decode_check(tpz_ctx* c, void* stream) {
+  if (!c) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  uint32_t* tail = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->ws.find(stream);
+    if (it != c->ws.end()) tail = it->second.d_tail;
+  }
+  TPZ_HIP(hipStreamSynchronize((hipStream_t)stream));
+  if (!tail) return TPZ_SUCCESS;
+  uint32_t flag = 0;
+  TPZ_HIP(hipMemcpy(&flag, tail + tpz::kTailError, 4, hipMemcpyDeviceToHost));
+  if (!flag) return TPZ_SUCCESS;
+  TPZ_HIP(hipMemset(tail + tpz::kTailError, 0, 4));
+  g_last_error = "tpz_decode_blocks: a tail workgroup's wait for the big path timed out; spill "
+                 "blocks of a batch on this stream may be undecoded";
+  return TPZ_ERR_INTERNAL;
 }
 
 static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint32_t* d_crc,

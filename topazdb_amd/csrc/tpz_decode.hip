@@ -1743,11 +1743,14 @@ __global__ __launch_bounds__(kBigThreads, 1) void decode_tail_kernel(Params p, s
   // both list lengths in one round trip (the bigwave kernel before this one has appended to them);
   // the spill list is read again only after the big phase, which can append to it
   const u32 nb = uni(tail_load(ctr + kTailBig)), nc0 = uni(tail_load(ctr + kTailSpill));
+  bool big_done = true;
   if (nb) {
     if (open(ctr + kTailBigTicket, nb)) big_phase(p, lds, nb, ctr + kTailBigTicket, ctr + kTailBigDone, &bcast);
-    tail_wait(ctr + kTailBigDone, nb);
+    big_done = tail_wait(ctr + kTailBigDone, nb, ctr + kTailError, &bcast);
   }
-  const u32 nc = nb ? uni(tail_load(ctr + kTailSpill)) : nc0;
+  // (a timed-out wait leaves the spill list to the workgroups whose wait ended, and the error
+  // word set: the spill count read here would not be final)
+  const u32 nc = !big_done ? 0u : nb ? uni(tail_load(ctr + kTailSpill)) : nc0;
   if (nc && open(ctr + kTailSpillTicket, nc)) sp::spill_phase(spp, lds, nc, ctr + kTailSpillTicket);
   // the last workgroup out zeroes the counters for the next decode on the stream: no memset
   // launch, and a captured graph replays correctly

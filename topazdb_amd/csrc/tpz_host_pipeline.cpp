@@ -204,10 +204,13 @@ static uint64_t decoded_bound(const uint8_t* b, uint64_t len) {
   if (len == 0) return 0;
   const uint8_t tag = b[len - 1];
   if (tag == 2) {                                 // snappy: the varint preamble (+ tag byte)
+    // snap's header rule, as the device sizes pass and the oracle apply it: up to 10 varint
+    // bytes (redundant continuation bytes allowed), a value past u32 is TooBig, a truncated
+    // varint an Err; an Err block decodes to its 1-byte tag-0 form
     uint64_t v = 0;
-    for (uint32_t i = 0, sh = 0; i < 5 && i + 1 < len; i++, sh += 7) {
-      v |= (uint64_t)(b[i] & 0x7F) << sh;
-      if (!(b[i] & 0x80)) return v + 1;
+    for (uint32_t i = 0; i < 10 && i + 1 < len; i++) {
+      v |= (uint64_t)(b[i] & 0x7F) << (7 * i);
+      if (!(b[i] & 0x80)) return v > 0xFFFFFFFFull ? 1 : v + 1;
     }
     return 1;
   }
@@ -279,7 +282,8 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   if (n == 0) return TPZ_SUCCESS;
   const uint64_t src_bytes = h_ext[n];
   const uint64_t data_cap = o->data_cap ? o->data_cap : tpz_data_capacity(src_bytes, n);
-  if (!codec && data_cap < tpz_data_capacity(src_bytes, n)) return TPZ_ERR_INVALID_ARG;
+  // (a data_cap too small for the batch is TPZ_ERR_NOMEM, as for codec batches: the chunks
+  //  whose slots do not fit are not copied out and the sizes needed are returned)
   PIPE_HIP(hipSetDevice(tpz_internal_device(ctx)));
   const uint32_t cb = chunk_blocks ? chunk_blocks : 8192u;
   const uint32_t n_chunks = (n + cb - 1) / cb;
@@ -300,11 +304,29 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   TpzHostPipe* P = static_cast<TpzHostPipe*>(tpz_internal_pipe_acquire(ctx));
   const bool fresh = P == nullptr;
   if (fresh) P = new TpzHostPipe();
+  // Declared after the Pins, so it runs before they unregister the caller's memory: an early
+  // return (a failed HIP call, a NOMEM) can leave copies and kernels in flight on the pipe's
+  // streams, so they are drained first, and then the pipe goes back to the pool. A fresh pipe
+  // whose streams or events could not all be created is destroyed instead of pooled.
   struct Release {
     tpz_ctx* c;
     TpzHostPipe* p;
     bool fresh;
-    ~Release() { tpz_internal_pipe_release(c, p, fresh); }
+    ~Release() {
+      bool whole = true;
+      for (hipStream_t q : {p->up, p->comp, p->down}) {
+        if (q) (void)hipStreamSynchronize(q);
+        whole &= q != nullptr;
+      }
+      for (const Slot& S : p->slot)
+        for (hipEvent_t e : {S.ev, S.ev_up, S.ev_pack, S.ev_down}) whole &= e != nullptr;
+      (void)hipGetLastError();
+      if (fresh && !whole) {
+        delete p;
+        return;
+      }
+      tpz_internal_pipe_release(c, p, fresh);
+    }
   } release{ctx, P, fresh};
   if (fresh) {
     PIPE_HIP(hipStreamCreateWithFlags(&P->up, hipStreamNonBlocking));
@@ -463,6 +485,13 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       if (r != TPZ_SUCCESS) return r;
       PIPE_HIP(hipEventSynchronize(S.ev));
     }
+    // still short after the tries (each grows the buffers to 1.25x what the chunk reported, so
+    // this takes a device that keeps reporting more): the chunk's emptied extents must not be
+    // copied out as if they were its blocks
+    if ((codec && S.h_meta.as<ChunkMeta>()->overflow) || *S.h_used.as<uint64_t>() > S.d_spill.n) {
+      return tpz_internal_fail(TPZ_ERR_NOMEM,
+                               "tpz_decode_blocks_host: chunk buffers still overflow after 4 decodes");
+    }
     const uint64_t used = *S.h_used.as<uint64_t>();
     const uint64_t* first = S.h_first.as<uint64_t>();
     const uint64_t total = first[m];
@@ -551,5 +580,8 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   PIPE_HIP(hipStreamSynchronize(P->up));
   PIPE_HIP(hipStreamSynchronize(P->comp));
   PIPE_HIP(hipStreamSynchronize(P->down));
+  // every chunk decoded to completion (tpz_decode_check: no timed-out tail wait on comp)
+  const tpz_err chk = tpz_decode_check(ctx, P->comp);
+  if (chk != TPZ_SUCCESS) return chk;
   return (short_ends || short_spill || short_data) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
 }

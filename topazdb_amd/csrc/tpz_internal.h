@@ -9,6 +9,8 @@
 // Context accessors for the host pipeline (tpz_host_pipeline.cpp; defined in tpz_api.cpp).
 int tpz_internal_device(tpz_ctx* c);
 tpz_err tpz_internal_hip_fail(hipError_t e, const char* what);
+// Sets tpz_last_error's text and returns err.
+tpz_err tpz_internal_fail(tpz_err err, const char* what);
 // The context's pool of host pipelines (streams + buffers of tpz_decode_blocks_host, reused
 // across calls; one per concurrent caller): acquire returns a free one or nullptr; release puts
 // one back (fresh = created by this call: the context takes ownership); the context destroys
@@ -116,18 +118,36 @@ enum TailCounter : int {
   kTailSpillTicket,    // spill blocks claimed
   kTailExit,           // tail-kernel workgroups finished
   kTailWave,           // (diagnostic builds) the wave path's global chunk counter
-  kTailCounters
+  kTailCounters,
+  // Sticky, past the counters the tail kernel zeroes: set when a tail workgroup's wait for the
+  // big phase timed out (tpz_decode_check reports it and clears it)
+  kTailError = kTailCounters,
+  kTailWords
 };
 __device__ __forceinline__ uint32_t tail_load(const uint32_t* c) {
   return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Every thread of the workgroup: wait until *done reaches n, then see what the finished blocks
-// wrote. Bounded (about a second), so a counting bug cannot hang the device.
-__device__ __forceinline__ void tail_wait(const uint32_t* done, uint32_t n) {
-  if (threadIdx.x == 0)
-    for (uint32_t i = 0; i < (1u << 22) && tail_load(done) < n; i++) __builtin_amdgcn_s_sleep(2);
+// wrote. Workgroups only wait for blocks that running workgroups hold (tickets), so the wait
+// ends; it is still bounded (about a second), so that a counting bug cannot hang the device.
+// A wait that times out is not passed over: it sets the sticky error word (tpz_decode_check
+// returns TPZ_ERR_INTERNAL) and returns false, and the caller skips what depended on it.
+__device__ __forceinline__ bool tail_wait(const uint32_t* done, uint32_t n, uint32_t* err,
+                                          uint32_t* flag) {
+  if (threadIdx.x == 0) {
+    uint32_t i = 0;
+    for (; i < (1u << 22) && tail_load(done) < n; i++) __builtin_amdgcn_s_sleep(2);
+#ifdef TPZ_ABL_TAILLATE
+    const bool late = true;   // diagnostic build (tests/test_gpu_tail_check.py): every wait times out
+#else
+    const bool late = tail_load(done) < n;
+#endif
+    if (late) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = late ? 0u : 1u;
+  }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return __builtin_amdgcn_readfirstlane(*flag) != 0;
 }
 
 // Long blocks with few entries (tpz_bigwave.hip): one wave per block, straight from HBM.
