@@ -265,6 +265,59 @@ def gpu_local_cpus(device: int) -> list[int]:
         return []
 
 
+def mem_available() -> int:
+    """MemAvailable of this host in bytes (0 if /proc/meminfo cannot be read)."""
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
+
+
+def e2e_host_bytes(ext: np.ndarray, n_ent: np.ndarray, k: int) -> int:
+    """Host bytes e2e_rate pins for the first k blocks of a shard: the input copy, the slotted
+    data capacity, the packed ends, and the per-block outputs (first u64, count u32, status u8,
+    crc u32, spill offset u64)."""
+    src_bytes = int(ext[k] - ext[0])
+    return (src_bytes + _lib.data_capacity(src_bytes, k) + 4 * (2 * int(n_ent[:k].sum()) + 64)
+            + 25 * (k + 1))
+
+
+def e2e_plan(ext: np.ndarray, n_ent: np.ndarray, avail: int, local_ranks: int,
+             frac: float = 0.5, quantum: int = 8192) -> int:
+    """Blocks of the shard the e2e leg runs on (BASELINE.json configs[4] at N GPUs: every rank
+    of the node pins its buffers at once). The whole shard when every local rank's pinned
+    footprint fits `frac` of the host's available memory; otherwise the longest prefix of whole
+    `quantum`-block chunks (the host pipeline's chunk) that fits; 0 (skip) when not even one
+    chunk fits. avail = 0 (unknown) keeps the whole shard."""
+    nb = len(ext) - 1
+    if avail <= 0:
+        return nb
+    budget = frac * avail / max(1, local_ranks)
+    if e2e_host_bytes(ext, n_ent, nb) <= budget:
+        return nb
+    lo, hi = 0, nb // quantum          # largest m with m * quantum blocks inside the budget
+    while lo < hi:
+        m = (lo + hi + 1) // 2
+        if e2e_host_bytes(ext, n_ent, m * quantum) <= budget:
+            lo = m
+        else:
+            hi = m - 1
+    return lo * quantum
+
+
+def agree_min(dist, k: int, device) -> int:
+    """The smallest k over ranks (every rank runs the e2e leg on the same number of blocks)."""
+    if dist is None:
+        return k
+    t = torch.tensor([k], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
 def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps: int = 5,
              chunk_blocks: int = 0) -> dict:
     """Host memory -> HBM -> host memory through the library's own pipeline
@@ -1033,11 +1086,24 @@ def main():
     if not args.no_e2e:
         # every rank (BASELINE.json configs[4]: the H2D/D2H-inclusive rate at N GPUs, all ranks
         # sharing the host's links and memory): per-rank times, max over ranks, all bytes
+        # The pinned footprint is bounded: every local rank pins its buffers at once (~9.2 GB
+        # per rank for the 4k shard), so the leg runs on the longest prefix of the
+        # shard that fits half of the host's available memory, the same on every rank.
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        avail = mem_available()
+        k = agree_min(dist, e2e_plan(ext, n_ent, avail, local_ranks), dev)
         r = None
-        try:
-            r = e2e_rate(ctx, src, ext, n_ent, dev)
-        except Exception as ex:  # reported, never the metric
-            log(rank, f"e2e measurement failed: {ex}")
+        if k > 0:
+            try:
+                r = e2e_rate(ctx, src[:int(ext[k])], ext[:k + 1], n_ent[:k], dev)
+                r["sample_blocks"] = k
+                r["host_pinned_bytes_per_rank"] = e2e_host_bytes(ext, n_ent, k)
+                r["host_mem_available"] = avail
+            except Exception as ex:  # reported, never the metric
+                log(rank, f"e2e measurement failed: {ex}")
+        else:
+            log(rank, f"e2e skipped: {local_ranks} ranks x one chunk exceed half of "
+                      f"{avail / GIB:.1f} GiB available")
         e2e = combine_e2e(dist, r, world, dev)   # every rank joins, failed or not
 
     fcrc = None

@@ -124,3 +124,43 @@ def test_parse_cpulist():
 def test_shard_seeds_distinct():
     seeds = {bench.shard_seed("4k", r) for r in range(8)}
     assert len(seeds) == 8
+
+
+def test_e2e_plan_bounds_pinned_footprint():
+    """The e2e leg's pinned footprint (BASELINE.json configs[4]: every local rank pins at once):
+    the whole shard when it fits half the available memory over the local ranks, otherwise the
+    longest prefix of whole host-pipeline chunks that fits, 0 (skip) when not even one does."""
+    nb = 4 * 256
+    src, ext, gen, n_ent, _, _ = bench.make_shard("4k", nb, 0)
+    whole = bench.e2e_host_bytes(ext, n_ent, nb)
+    assert whole > 2 * int(ext[-1])                       # input + slotted data + ends
+    assert bench.e2e_plan(ext, n_ent, 0, 8, quantum=256) == nb        # unknown: whole shard
+    assert bench.e2e_plan(ext, n_ent, 2 * 8 * whole, 8, quantum=256) == nb
+    for m in (1, 2, 3):
+        budget = bench.e2e_host_bytes(ext, n_ent, m * 256) + 1
+        k = bench.e2e_plan(ext, n_ent, 2 * 8 * budget, 8, quantum=256)
+        assert k == m * 256 and bench.e2e_host_bytes(ext, n_ent, k) <= budget
+    assert bench.e2e_plan(ext, n_ent, 100, 8, quantum=256) == 0
+
+
+def _plan_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nb = 4 * 256
+        src, ext, gen, n_ent, _, _ = bench.make_shard("4k", nb, rank)
+        # rank 1 sees less available memory: both ranks must run the same (smaller) prefix
+        budget = bench.e2e_host_bytes(ext, n_ent, (4 - 2 * rank) * 256) + 1
+        k = bench.e2e_plan(ext, n_ent, 2 * world * budget, world, quantum=256)
+        out[rank] = (k, bench.agree_min(dist, k, torch.device("cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_e2e_plan_agreed_over_ranks():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_plan_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert out[0][0] == 4 * 256 and out[1][0] <= 2 * 256
+    assert out[0][1] == out[1][1] == out[1][0]

@@ -62,6 +62,27 @@ __global__ __launch_bounds__(256) void copy_k(const uint4* __restrict__ s, uint4
   for (; i < n16; i += stride) d[i] = s[i];
 }
 
+// guide-style: one float4 per thread (or K consecutive per thread), a grid covering the buffer
+template <int K, bool NT>
+__global__ __launch_bounds__(256) void copy_flat_k(const uint4* __restrict__ s, uint4* __restrict__ d, u64 n16) {
+  const u64 i0 = ((u64)blockIdx.x * blockDim.x) * K + threadIdx.x;
+  uint4 v[K];
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    if (i0 + k * 256 < n16) v[k] = s[i0 + k * 256];
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    if (i0 + k * 256 < n16) {
+      if (NT) {
+        typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 t = {v[k].x, v[k].y, v[k].z, v[k].w};
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(&d[i0 + k * 256]));
+      } else {
+        d[i0 + k * 256] = v[k];
+      }
+    }
+}
+
 __global__ __launch_bounds__(256) void read_k(const uint4* __restrict__ s, u64 n16, u32* out) {
   const u64 stride = (u64)gridDim.x * blockDim.x;
   u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -140,6 +161,9 @@ int main(int argc, char** argv) {
       else if (v == "copy_g16") copy_k<4, false, false><<<cus * 16, 256>>>(s, d, n16);
       else if (v == "copy_g32") copy_k<4, false, false><<<cus * 32, 256>>>(s, d, n16);
       else if (v == "copy_wave4k") wave4k_k<<<cus, 1024>>>(s, d, N / 4096);
+      else if (v == "copy_flat") copy_flat_k<1, false><<<(u32)((n16 + 255) / 256), 256>>>(s, d, n16);
+      else if (v == "copy_flat4") copy_flat_k<4, false><<<(u32)((n16 + 1023) / 1024), 256>>>(s, d, n16);
+      else if (v == "copy_flat_nt") copy_flat_k<1, true><<<(u32)((n16 + 255) / 256), 256>>>(s, d, n16);
       else if (v == "memcpy") (void)hipMemcpyAsync(b, a, N, hipMemcpyDeviceToDevice, 0);
       else if (v == "copy_small") copy_k<4, false, false><<<cus * 8, 256>>>(s, d, small16);
     };
