@@ -48,8 +48,10 @@ extern "C" {
  *      panic of Block::decode
  *   4  tpz_decode_blocks_host takes snappy / lz4 blocks (tpz_host_columns.h_dext, data_cap);
  *      the exact ends layout (tpz_columns.d_entry_first, tpz_table.d_entry_first)
+ *   5  the flat layout: tpz_flat_layout + tpz_decode_blocks_flat (tpz_flat_columns); no
+ *      existing struct or status changed
  * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
-#define TPZ_ABI_VERSION 4
+#define TPZ_ABI_VERSION 5
 int tpz_abi_version(void);
 
 /* ---- API return codes ------------------------------------------------------------------- */
@@ -285,6 +287,57 @@ tpz_err tpz_entry_first(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_first,
  * spill records; zeros for a block whose status is none of OK, OK_SPILLED, BAD_ENTRY). */
 tpz_err tpz_pack_ends(tpz_ctx* ctx, const tpz_batch* batch, const tpz_columns* cols,
                       const uint64_t* d_first, uint32_t* d_dense, void* stream);
+
+/* ---- the flat layout ---------------------------------------------------------------------
+ * One dense key column and one dense value column for the whole batch: every key of every
+ * block, in SsTableIterator order (blocks in batch order, entries in block order: what
+ * BlockIterator::key() returns for each entry, src/block/iterator.rs:63-83), back to back, and
+ * likewise every value; the {kend, vend} pairs give each entry's end within its block's run.
+ *
+ * tpz_flat_layout sizes the columns on the device (one pass over the batch and three scans, no
+ * host sync): d_first holds 3 * (n_blocks + 1) u64, with st = n_blocks + 1:
+ *   d_first[i]          entries of blocks 0..i-1 (the exact ends layout's d_entry_first)
+ *   d_first[st + i]     key bytes of blocks 0..i-1: block i's keys start at d_keys[d_first[st + i]]
+ *   d_first[2 st + i]   value bytes of blocks 0..i-1, likewise in d_values
+ * and the totals at i = n_blocks (read them back to size the columns). A block's reservation is
+ * what decoding it yields when its CRC matches: its header n entries and the bytes of every key
+ * and value that reads whole (src/block/iterator.rs:74-82: an unreadable key or value reserves
+ * nothing, as in TPZ_BLOCK_BAD_ENTRY), for a block with tag 1 and len >= 7 + 2n; nothing for any
+ * other block (EMPTY, BAD_TAG, UNSUPPORTED_CODEC, MALFORMED). Run the codec step first for
+ * snappy / lz4 batches. Asynchronous on `stream`; uses the stream's workspace. */
+tpz_err tpz_flat_layout(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_first, void* stream);
+
+/* tpz_decode_blocks_flat: tpz_decode_blocks into the flat layout. Per block i (st as above):
+ *   keys:   key_j   = d_keys  [kb + (j ? ends[2(e+j-1)]   : 0) .. kb + ends[2(e+j)]]
+ *   values: value_j = d_values[vb + (j ? ends[2(e+j-1)+1] : 0) .. vb + ends[2(e+j)+1]]
+ *   with e = d_first[i], kb = d_first[st + i], vb = d_first[2 st + i], j < count[i]
+ *   d_count, d_status, d_crc: as tpz_columns. Every decoded block reports TPZ_BLOCK_OK or
+ *   TPZ_BLOCK_BAD_ENTRY (no OK_SPILLED: the spill path writes the columns too); a block that
+ *   fails its CRC keeps its reserved bytes, unspecified.
+ *   d_spill / spill_cap / d_spill_off / d_spill_used: a BAD_ENTRY block's count[i] class bytes
+ *   (tpz_entry_class) at d_spill[d_spill_off[i] ..] (records of n bytes rounded up to 128; the
+ *   entry's unreadable key or value is empty in the columns), SPILL_FULL as in tpz_columns.
+ *   May be NULL / 0 for batches without bad entries.
+ * d_keys and d_values must be 16-byte aligned, with d_first[st + n_blocks] and
+ * d_first[2 st + n_blocks] bytes; d_ends 2 * d_first[n_blocks] u32. Blocks share 16-byte chunks
+ * of the columns at their boundaries: the decode writes those chunks byte-exactly (each block
+ * its own bytes), so blocks still decode independently. Asynchronous on `stream`. */
+typedef struct {
+  uint8_t* d_keys;
+  uint8_t* d_values;
+  uint32_t* d_ends;
+  const uint64_t* d_first;  /* from tpz_flat_layout over the same batch */
+  uint32_t* d_count;
+  uint8_t* d_status;
+  uint32_t* d_crc;
+  uint8_t* d_spill;
+  uint64_t spill_cap;
+  uint64_t* d_spill_off;
+  uint64_t* d_spill_used;
+} tpz_flat_columns;
+
+tpz_err tpz_decode_blocks_flat(tpz_ctx* ctx, const tpz_batch* batch, const tpz_flat_columns* out,
+                               void* stream);
 
 /* ---- the host pipeline -------------------------------------------------------------------
  * SsTable::read_block for a whole run of blocks that sit in HOST memory (src/table.rs:154-164;

@@ -35,7 +35,7 @@ pub const TPZ_ENTRY_OK: u8 = 0;
 pub const TPZ_ENTRY_BAD_VALUE: u8 = 1;
 pub const TPZ_ENTRY_BAD_KEY: u8 = 2;
 
-pub const TPZ_ABI_VERSION: c_int = 4;
+pub const TPZ_ABI_VERSION: c_int = 5;
 pub const TPZ_LDS_BLOCK_BYTES: u32 = 94192;
 pub const TPZ_BIGWAVE_BLOCK_BYTES: u32 = 0x40000000;
 pub const TPZ_PLAN_ASYNC_MAX_BLOCK: u32 = 10242;
@@ -66,6 +66,24 @@ pub struct TpzColumns {
     pub d_spill_off: *mut u64,
     pub d_spill_used: *mut u64,
     pub d_entry_first: *const u64,
+}
+
+/// `tpz_flat_columns`: the flat layout (one dense key column and one dense value column for the
+/// batch, exact `{kend, vend}` pairs); `d_first` from `tpz_flat_layout`.
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct TpzFlatColumns {
+    pub d_keys: *mut u8,
+    pub d_values: *mut u8,
+    pub d_ends: *mut u32,
+    pub d_first: *const u64,
+    pub d_count: *mut u32,
+    pub d_status: *mut u8,
+    pub d_crc: *mut u32,
+    pub d_spill: *mut u8,
+    pub spill_cap: u64,
+    pub d_spill_off: *mut u64,
+    pub d_spill_used: *mut u64,
 }
 
 /// `tpz_host_columns`: `tpz_decode_blocks_host`'s outputs in host memory.
@@ -142,6 +160,10 @@ extern "C" {
                            stream: *mut c_void) -> TpzErr;
     pub fn tpz_pack_ends(ctx: *mut TpzCtx, batch: *const TpzBatch, cols: *const TpzColumns,
                          d_first: *const u64, d_dense: *mut u32, stream: *mut c_void) -> TpzErr;
+    pub fn tpz_flat_layout(ctx: *mut TpzCtx, batch: *const TpzBatch, d_first: *mut u64,
+                           stream: *mut c_void) -> TpzErr;
+    pub fn tpz_decode_blocks_flat(ctx: *mut TpzCtx, batch: *const TpzBatch,
+                                  out: *const TpzFlatColumns, stream: *mut c_void) -> TpzErr;
     pub fn tpz_host_decoded_bound(h_src: *const u8, h_ext: *const u64, n_blocks: u32,
                                   bound: *mut u64) -> TpzErr;
     pub fn tpz_decode_blocks_host(ctx: *mut TpzCtx, h_src: *const u8, h_ext: *const u64,

@@ -21,7 +21,7 @@ RUST = os.path.join(ROOT, "rust", "tpz-gpu-sys", "src", "lib.rs")
 C_SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64",
              "int": "int", "tpz_err": "int", "double": "f64", "size_t": "usize", "char": "c_char",
              "void": "c_void"}
-C_STRUCTS = {"tpz_batch": "TpzBatch", "tpz_columns": "TpzColumns",
+C_STRUCTS = {"tpz_batch": "TpzBatch", "tpz_columns": "TpzColumns", "tpz_flat_columns": "TpzFlatColumns",
              "tpz_host_columns": "TpzHostColumns", "tpz_table": "TpzTable",
              "tpz_entries": "TpzEntries", "tpz_ctx": "TpzCtx"}
 R_ALIASES = {"c_int": "int", "TpzErr": "int", "i32": "int"}
@@ -127,7 +127,8 @@ RFNS, RSTRUCTS, RCONSTS = parse_rust()
 
 def test_parsers_found_the_abi():
     assert len(HFNS) >= 36 and "tpz_decode_blocks" in HFNS and "tpz_decode_check" in HFNS
-    assert set(HSTRUCTS) == {"TpzBatch", "TpzColumns", "TpzHostColumns", "TpzTable", "TpzEntries"}
+    assert set(HSTRUCTS) == {"TpzBatch", "TpzColumns", "TpzFlatColumns", "TpzHostColumns", "TpzTable",
+                             "TpzEntries"}
     assert HCONSTS["TPZ_ABI_VERSION"] >= 4 and HCONSTS["TPZ_BLOCK_BAD_ENTRY"] == 9
 
 

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4: flat-layout parity tests and the decode/spill/exact parity tests on the GPU box, then
+# the r4b diagnostics (copy ceiling, CRC-lookup variants A/B against the round-3 HEAD build).
+set -o pipefail
+OUT=gpurun_out/r4c
+mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_flat.py tests/test_gpu_decode.py tests/test_gpu_exact.py tests/test_gpu_spill.py tests/test_gpu_bad_entry.py -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
+tail -3 $OUT/tests.log
+VARIANTS="${VARIANTS:-full head nocf lutvalu nocrc onchip onchip_nocf onchip_lutvalu onchip_nocrc}" bash tools/gpu_r4b.sh

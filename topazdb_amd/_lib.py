@@ -22,7 +22,7 @@ SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM, ERR_INTERNAL = 0, -
  BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR, BLOCK_BAD_ENTRY) = range(10)
 # tpz_entry_class (BAD_ENTRY blocks)
 ENTRY_OK, ENTRY_BAD_VALUE, ENTRY_BAD_KEY = 0, 1, 2
-ABI_VERSION = 4           # TPZ_ABI_VERSION this binding was written against
+ABI_VERSION = 5           # TPZ_ABI_VERSION this binding was written against
 LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks with 64+ entries take the spill path
 BIGWAVE_BLOCK_BYTES = 0x40000000   # TPZ_BIGWAVE_BLOCK_BYTES
 
@@ -44,6 +44,17 @@ class Columns(C.Structure):
 
 COLUMN_FIELDS = ("data", "ends", "count", "status", "crc", "spill", "spill_cap", "spill_off",
                  "spill_used", "entry_first")
+
+
+class FlatColumns(C.Structure):
+    """tpz_flat_columns: the flat layout (one key column, one value column, exact ends)."""
+    _fields_ = [("d_keys", C.c_void_p), ("d_values", C.c_void_p), ("d_ends", C.c_void_p),
+                ("d_first", C.c_void_p), ("d_count", C.c_void_p), ("d_status", C.c_void_p),
+                ("d_crc", C.c_void_p), ("d_spill", C.c_void_p), ("spill_cap", C.c_uint64),
+                ("d_spill_off", C.c_void_p), ("d_spill_used", C.c_void_p)]
+
+FLAT_FIELDS = ("keys", "values", "ends", "first", "count", "status", "crc", "spill", "spill_cap",
+               "spill_off", "spill_used")
 
 
 class Table(C.Structure):
@@ -125,6 +136,11 @@ def lib() -> C.CDLL:
         L.tpz_pack_ends.restype = C.c_int
         L.tpz_entry_first.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
         L.tpz_entry_first.restype = C.c_int
+        L.tpz_flat_layout.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
+        L.tpz_flat_layout.restype = C.c_int
+        L.tpz_decode_blocks_flat.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(FlatColumns),
+                                             C.c_void_p]
+        L.tpz_decode_blocks_flat.restype = C.c_int
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
@@ -261,6 +277,22 @@ class Context:
         b = Batch(d_src, d_ext, n_blocks, src_bytes)
         check(lib().tpz_entry_first(self.handle, C.byref(b), C.c_void_p(d_first),
                                     C.c_void_p(stream)), "tpz_entry_first")
+
+    def flat_layout_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
+                         d_first: int, stream: int = 0) -> None:
+        """tpz_flat_layout: 3 x (n_blocks + 1) u64 of per-block entry / key-byte / value-byte
+        prefixes (the flat layout's sizes)."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        check(lib().tpz_flat_layout(self.handle, C.byref(b), C.c_void_p(d_first),
+                                    C.c_void_p(stream)), "tpz_flat_layout")
+
+    def decode_flat_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int, cols: dict,
+                         stream: int = 0) -> None:
+        """tpz_decode_blocks_flat on raw device pointers; cols maps FLAT_FIELDS -> pointer."""
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        c = FlatColumns(*[cols[f] for f in FLAT_FIELDS])
+        check(lib().tpz_decode_blocks_flat(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
+              "tpz_decode_blocks_flat")
 
     def decode_host_ptrs(self, h_src: int, h_ext: int, n_blocks: int, cols: HostColumns,
                          chunk_blocks: int = 0) -> int:

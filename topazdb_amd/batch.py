@@ -264,6 +264,121 @@ def exact_columns(ctx: Context, batch: DeviceBatch, spill_cap: int = 0,
     return SlottedColumns(batch.n_blocks, batch.src_bytes, ctx.device, spill_cap, first, n_pairs)
 
 
+def flat_layout(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None
+                ) -> torch.Tensor:
+    """tpz_flat_layout (asynchronous): int64 [3, n_blocks + 1] exclusive prefixes of every
+    block's entries, key bytes and value bytes (totals in the last column)."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(s):
+        first = torch.empty(3 * (batch.n_blocks + 1), dtype=torch.int64, device=dev)
+    ctx.flat_layout_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
+                         batch.src_bytes, first.data_ptr(), s.cuda_stream)
+    return first.view(3, batch.n_blocks + 1)
+
+
+class FlatColumns:
+    """The flat layout (tpz_flat_columns): one dense key column and one dense value column for
+    the whole batch, in SsTableIterator order, plus exact {kend, vend} pairs per block."""
+
+    def __init__(self, ctx: Context, batch: DeviceBatch, spill_cap: int = 0,
+                 stream: torch.cuda.Stream | None = None):
+        dev = _dev(ctx.device)
+        self.device = ctx.device
+        self.first = flat_layout(ctx, batch, stream)
+        tot = self.first[:, batch.n_blocks].cpu().numpy()      # one sync: the column sizes
+        self.n_pairs, self.key_bytes, self.value_bytes = (int(x) for x in tot)
+        nb = max(batch.n_blocks, 1)
+        self.keys = torch.empty(max(self.key_bytes, 16), dtype=torch.uint8, device=dev)
+        self.values = torch.empty(max(self.value_bytes, 16), dtype=torch.uint8, device=dev)
+        self.ends = torch.empty(2 * max(self.n_pairs, 1), dtype=torch.int32, device=dev)
+        self.count = torch.empty(nb, dtype=torch.int32, device=dev)
+        self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
+        self.crc = torch.empty(nb, dtype=torch.int32, device=dev)
+        self.spill_off = torch.empty(nb, dtype=torch.int64, device=dev)
+        self.spill_used = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.set_spill_cap(spill_cap)
+        self.n_blocks = batch.n_blocks
+        self._decoded = None
+
+    def set_spill_cap(self, spill_cap: int) -> None:
+        self.spill_cap = int(spill_cap)
+        self.spill = (torch.empty(self.spill_cap, dtype=torch.uint8, device=_dev(self.device))
+                      if self.spill_cap else None)
+
+    def ptrs(self) -> dict:
+        p = {k: getattr(self, k).data_ptr() for k in ("keys", "values", "ends", "first", "count",
+                                                     "status", "crc", "spill_off", "spill_used")}
+        p["spill"] = self.spill.data_ptr() if self.spill is not None else None
+        p["spill_cap"] = self.spill_cap
+        return p
+
+    def complete(self) -> "FlatColumns":
+        """Waits for the decode; grows the class-byte arena and decodes again when a
+        BAD_ENTRY block did not fit it (SPILL_FULL)."""
+        torch.cuda.synchronize(_dev(self.device))
+        if self._decoded is not None:
+            ctx, batch, stream = self._decoded
+            sid = _stream_id(ctx, stream)
+            ctx.decode_check(sid)
+            used = int(self.spill_used.cpu()[0])
+            if used > self.spill_cap:
+                self.set_spill_cap(used)
+                decode_flat(ctx, batch, self, stream)
+                torch.cuda.synchronize(_dev(self.device))
+                ctx.decode_check(sid)
+        return self
+
+    def dense(self) -> "DenseDecode":
+        """The decoded entries as the oracle's dense decode (block order), read straight from
+        the columns: block b's keys are keys[first[1, b] ..], its values values[first[2, b] ..]."""
+        self.complete()
+        nb = self.n_blocks
+        status = self.status[:nb].cpu().numpy()
+        crc = self.crc[:nb].cpu().numpy().view(np.uint32)
+        count = self.count[:nb].cpu().numpy().view(np.uint32)
+        first = self.first.cpu().numpy()
+        okm = np.isin(status, (BLOCK_OK, _lib.BLOCK_OK_SPILLED, _lib.BLOCK_BAD_ENTRY))
+        n_ok = np.where(okm, count, 0).astype(np.int64)
+        ebase = np.zeros(nb + 1, np.int64)
+        np.cumsum(n_ok, out=ebase[1:])
+        total = int(ebase[-1])
+        bid = np.arange(nb, dtype=np.int64)
+        eblk = np.repeat(bid, n_ok)
+        j = np.arange(total, dtype=np.int64) - ebase[eblk]
+        pair = first[0][eblk] + j
+        ends = self.ends.cpu().numpy().view(np.uint32).astype(np.int64)
+        ke = ends[2 * pair] if total else np.zeros(0, np.int64)
+        ve = ends[2 * pair + 1] if total else np.zeros(0, np.int64)
+        ks = np.where(j == 0, 0, ends[np.maximum(2 * pair - 2, 0)]) if total else ke
+        vs = np.where(j == 0, 0, ends[np.maximum(2 * pair - 1, 1)]) if total else ve
+        keys = _gather(self.keys.cpu().numpy(), first[1][eblk] + ks, ke - ks)
+        vals = _gather(self.values.cpu().numpy(), first[2][eblk] + vs, ve - vs)
+        d = DenseDecode(status.astype(np.uint8), crc, n_ok.astype(np.uint32), count,
+                        (ke - ks).astype(np.uint32), (ve - vs).astype(np.uint32), keys, vals)
+        d.raw_status = status
+        bad = np.nonzero(status == _lib.BLOCK_BAD_ENTRY)[0]
+        if len(bad):
+            sp = self.spill.cpu().numpy()
+            offs = self.spill_off[:nb].cpu().numpy()
+            for b in bad:
+                n = int(count[b])
+                d.cls[int(ebase[b]):int(ebase[b]) + n] = sp[int(offs[b]):int(offs[b]) + n]
+        return d
+
+
+def decode_flat(ctx: Context, batch: DeviceBatch, cols: FlatColumns | None = None,
+                stream: torch.cuda.Stream | None = None, spill_cap: int = 0) -> FlatColumns:
+    """tpz_flat_layout (with one sync for the column sizes) + tpz_decode_blocks_flat."""
+    if cols is None:
+        cols = FlatColumns(ctx, batch, spill_cap, stream)
+    s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
+    ctx.decode_flat_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
+                         batch.src_bytes, cols.ptrs(), s.cuda_stream)
+    cols._decoded = (ctx, batch, stream)
+    return cols
+
+
 def pack_ends(ctx: Context, batch: DeviceBatch, cols: SlottedColumns,
               stream: torch.cuda.Stream | None = None):
     """tpz_pack_ends: the used {kend, vend} pairs of every block, dense in block order (for a

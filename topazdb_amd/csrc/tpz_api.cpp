@@ -113,6 +113,24 @@ std::vector<uint32_t> build_rep_tables(const std::vector<uint32_t>& range) {
   return out;
 }
 
+// The wave path's LDS table image (tpz_decode.hip, decode_wave_kernel): T_0 replicated 32
+// times (word b*32 + r = T_0[b]: lane l reads replica l mod 32, so a byte-indexed lookup is
+// bank-conflict-free), then the decode tables' ids 16..40 (the combine's shift operators and
+// the inverse table), then ids 41..44 = T_39..T_36 (the shift by 40 bytes that joins a lane's
+// two byte chains).
+std::vector<uint32_t> build_wave_tables(const std::vector<uint32_t>& dec) {
+  std::vector<uint32_t> out((size_t)tpz::kWaveTableWords);
+  for (int b = 0; b < 256; b++)
+    for (int r = 0; r < 32; r++) out[(size_t)b * 32 + r] = dec[(size_t)b];
+  std::memcpy(&out[8192], &dec[16 * 256], (size_t)(tpz::kNumCrcTables - 16) * 256 * 4);
+  const size_t sh = 8192 + (size_t)(tpz::kNumCrcTables - 16) * 256;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t z = x8n((uint64_t)(tpz::kCrcChainBytes - 1 - i));
+    for (int b = 0; b < 256; b++) out[sh + (size_t)i * 256 + b] = dec[b] ? multmodp(z, dec[b]) : 0u;
+  }
+  return out;
+}
+
 }  // namespace
 
 // Device workspace of one stream: the big-path and spill-path worklists, the big path's
@@ -141,6 +159,7 @@ struct tpz_ctx {
   int device = 0;
   uint32_t num_cus = 0;
   uint32_t* d_tables = nullptr;        // block-decode CRC tables
+  uint32_t* d_wave_tables = nullptr;   // the wave path's LDS table image
   uint32_t* d_range_tables = nullptr;  // range-CRC tables
   uint32_t* d_rep_tables = nullptr;    // replicated slice-by-4 tables
   std::mutex mu;  // guards the workspace map and the host pipelines
@@ -276,9 +295,10 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
   const std::vector<uint32_t> t = build_crc_tables();
   const std::vector<uint32_t> rt = build_range_tables();
   const std::vector<uint32_t> rep = build_rep_tables(rt);
+  const std::vector<uint32_t> wt = build_wave_tables(t);
   hipError_t e = hipSuccess;
   for (auto [dst, v] : {std::make_pair(&c->d_tables, &t), std::make_pair(&c->d_range_tables, &rt),
-                        std::make_pair(&c->d_rep_tables, &rep)}) {
+                        std::make_pair(&c->d_rep_tables, &rep), std::make_pair(&c->d_wave_tables, &wt)}) {
     if (e == hipSuccess) e = hipMalloc(dst, v->size() * 4);
     if (e == hipSuccess) e = hipMemcpy(*dst, v->data(), v->size() * 4, hipMemcpyHostToDevice);
   }
@@ -297,6 +317,7 @@ void tpz_ctx_destroy(tpz_ctx* c) {
   if (c->d_tables) (void)hipFree(c->d_tables);
   if (c->d_range_tables) (void)hipFree(c->d_range_tables);
   if (c->d_rep_tables) (void)hipFree(c->d_rep_tables);
+  if (c->d_wave_tables) (void)hipFree(c->d_wave_tables);
   for (auto& kv : c->ws) free_workspace(kv.second);
   for (void* p : c->pipes) tpz_internal_pipe_destroy(p);
   delete c;
@@ -338,6 +359,7 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.src_bytes = b->src_bytes;
   a.n_blocks = b->n_blocks;
   a.crc_tables = c->d_tables;
+  a.wave_tables = c->d_wave_tables;
   a.data = o->d_data;
   a.ends = o->d_ends;
   a.count = o->d_count;
@@ -475,6 +497,83 @@ tpz_err tpz_entry_first(tpz_ctx* c, const tpz_batch* b, uint64_t* d_first, void*
   }
   tpz::launch_entry_first(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, d_first,
                           reinterpret_cast<uint64_t*>(part), (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_flat_layout(tpz_ctx* c, const tpz_batch* b, uint64_t* d_first, void* stream) {
+  if (!c || !b || !d_first) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks && (!b->d_src || !b->d_ext)) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  uint32_t* part = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err e = get_acc(c, stream, 2 * (uint32_t)tpz::flat_scan_parts_words(b->n_blocks), &part);
+    if (e != TPZ_SUCCESS) return e;
+  }
+  tpz::launch_flat_layout(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, d_first,
+                          reinterpret_cast<uint64_t*>(part), c->num_cus, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+tpz_err tpz_decode_blocks_flat(tpz_ctx* c, const tpz_batch* b, const tpz_flat_columns* o,
+                               void* stream) {
+  if (!c || !b || !o) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks == 0) {
+    if (o->d_spill_used) {
+      TPZ_HIP(hipSetDevice(c->device));
+      TPZ_HIP(hipMemsetAsync(o->d_spill_used, 0, 8, (hipStream_t)stream));
+    }
+    return TPZ_SUCCESS;
+  }
+  if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_values || !o->d_ends || !o->d_first ||
+      !o->d_count || !o->d_status || !o->d_crc || !o->d_spill_off || !o->d_spill_used ||
+      (o->spill_cap && !o->d_spill) || (reinterpret_cast<uintptr_t>(b->d_src) & 15u) ||
+      (reinterpret_cast<uintptr_t>(o->d_keys) & 15u) || (reinterpret_cast<uintptr_t>(o->d_values) & 15u))
+    return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  tpz_workspace* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err r = get_workspace(c, stream, b->n_blocks, &w);
+    if (r != TPZ_SUCCESS) return r;
+  }
+  uint32_t* tail = w->d_tail;
+  const uint64_t st = (uint64_t)b->n_blocks + 1;
+  tpz::LaunchArgs a{};
+  a.src = b->d_src;
+  a.ext = b->d_ext;
+  a.src_bytes = b->src_bytes;
+  a.n_blocks = b->n_blocks;
+  a.crc_tables = c->d_tables;
+  a.wave_tables = c->d_wave_tables;
+  a.data = nullptr;                 // no slots: every path writes the columns
+  a.ends = o->d_ends;
+  a.count = o->d_count;
+  a.status = o->d_status;
+  a.crc = o->d_crc;
+  a.tail = tail;
+  a.defer_count = tail + tpz::kTailBig;
+  a.defer_list = w->d_defer + 4;
+  a.spill_count = tail + tpz::kTailSpill;
+  a.spill_list = w->d_defer + 4 + w->defer_cap;
+  a.bw_count = tail + tpz::kTailBw;
+  a.bw_list = nullptr;              // long blocks go to the spill path, which writes the columns
+  a.rep = c->d_rep_tables;
+  a.spill = o->d_spill;
+  a.spill_cap = o->d_spill ? o->spill_cap : 0;
+  a.spill_off = o->d_spill_off;
+  a.spill_used = o->d_spill_used;
+  a.num_cus = c->num_cus;
+  a.big_scratch = w->d_big_scratch;
+  a.big_grid = c->num_cus;
+  a.efirst = o->d_first;
+  a.keys = o->d_keys;
+  a.vals = o->d_values;
+  a.kfirst = o->d_first + st;
+  a.vfirst = o->d_first + 2 * st;
+  tpz::launch_decode(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
 }

@@ -36,6 +36,9 @@
 #include <stdint.h>
 
 #include "tpz_internal.h"
+#if defined(TPZ_ABL_SARW) && !defined(TPZ_CRC_SARW)
+#define TPZ_CRC_SARW   // variant builds: make variants (libtpz_gpu_sarw.so, onchip_sarw, ...)
+#endif
 // the tail kernel's spill phase (namespace tpz::sp), compiled into this unit
 #include "tpz_spill.hip"
 
@@ -67,11 +70,22 @@ constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B 
 constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads, the 5th partial
 constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
+#ifdef TPZ_CRC_SARW
+// byte-serial CRC over a 32-fold replicated T_0 (bank-conflict-free lookups): the table image
+// takes 61 KiB, so the entry table holds 2n + 1 <= 255 segments
+constexpr u32 kWaveMaxN = 127;
+constexpr int kWaveTabSlots = 256;
+constexpr int kWaveTabBytes = kWaveTableWords * 4;
+#else
 constexpr u32 kWaveMaxN = 255;                      // the table holds 2n + 1 <= 511 entries
+constexpr int kWaveTabSlots = 512;
+constexpr int kWaveTabBytes = kTableBytes;
+#endif
 constexpr int kWaveMapLen = 288;                    // >= (kWaveMaxLen + 2) / 16 + 3 map slots
-constexpr int kSlotBytes = kGuard + kWinBytes + 32 + 512 * 4 + 2 * kWaveMapLen;
+constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveTabSlots * 4 + 2 * kWaveMapLen;
 static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 8 == 0, "slot alignment");
-constexpr int kWaveLds = kTableBytes + kWavesPerWG * kSlotBytes;
+static_assert(2 * kWaveMaxN + 1 <= (u32)kWaveTabSlots, "entry table");
+constexpr int kWaveLds = kWaveTabBytes + kWavesPerWG * kSlotBytes;
 static_assert(kWaveLds <= 163840, "wave path LDS");
 
 // big path (one 16-wave workgroup per block): [tables][guard 96][window 92 KiB][pad 32]
@@ -349,6 +363,49 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
   return crc_combine(tab, A);
 }
 
+#ifdef TPZ_CRC_SARW
+// Wave path, byte-serial CRC (Sarwate) over T_0 replicated 32 times: word b * 32 + r = T_0[b],
+// lane l reads replica l mod 32, so a lookup with any byte per lane hits 32 distinct banks
+// (ds_read_b32 serves lanes 0-31 and 32-63 in one LDS cycle each) instead of the slice tables'
+// ~3x replays. tab (ids >= 16, as everywhere) sits right after the replicas.
+__device__ __forceinline__ const u32* crc_rep(const u32* tab) { return tab + 16 * 256 - 8192; }
+// c = T_0[(c ^ b) & 0xFF] ^ (c >> 8) for the four bytes of w
+__device__ __forceinline__ u32 sarw4(const u32* rep, u32 lr, u32 c, u32 w) {
+  c ^= w;
+#pragma unroll
+  for (int i = 0; i < 4; i++) c = rep[((c & 0xFFu) << 5) | lr] ^ (c >> 8);
+  return c;
+}
+// shift_k (k zero bytes) and its inverse, for a wave-uniform k < 16
+__device__ __forceinline__ u32 crc_shift_small_w(const u32* tab, u32 a, u32 k) {
+  const u32* rep = crc_rep(tab);
+  const u32 lr = lane_id() & 31u;
+  for (u32 i = 0; i < k; i++) a = rep[((a & 0xFFu) << 5) | lr] ^ (a >> 8);
+  return a;
+}
+__device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k) {
+  const u32* rep = crc_rep(tab);
+  const u32 lr = lane_id() & 31u;
+  for (u32 i = 0; i < k; i++) {
+    const u32 b = tlook(tab, kCrcInvTable, r >> 24);
+    r = ((r ^ rep[(b << 5) | lr]) << 8) | b;
+  }
+  return r;
+}
+// shift by kCrcChainBytes (ids 41..44: T_39..T_36)
+__device__ __forceinline__ u32 crc_shift_chain(const u32* tab, u32 a) {
+  return xor3(tlook(tab, 41, a & 0xFF), tlook(tab, 42, (a >> 8) & 0xFF),
+              tlook(tab, 43, (a >> 16) & 0xFF)) ^ tlook(tab, 44, a >> 24);
+}
+#else
+__device__ __forceinline__ u32 crc_shift_small_w(const u32* tab, u32 a, u32 k) {
+  return crc_shift_small(tab, a, k);
+}
+__device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k) {
+  return crc_unshift_small(tab, r, k);
+}
+#endif
+
 // ------------------------------------------------------------------ entry tables
 // The NON-EMPTY keys in order, then the non-empty values in order (one table for the block's
 // output stream): end = exclusive end offset of the segment's bytes in the stream, delta = (LDS
@@ -489,6 +546,12 @@ struct Out {
   u32* bw_list;        // long blocks with n < 64: decode_bigwave_kernel (tpz_bigwave.hip)
   u32* bw_count;
   const u64* efirst;   // exact ends layout (tpz_columns.d_entry_first), or null: slotted
+  // flat layout (tpz_decode_blocks_flat), or null: slotted. Block b's keys go to
+  // keys[kfirst[b] ..], its values to vals[vfirst[b] ..] (tpz_flat_layout's prefixes).
+  uint8_t* keys;
+  uint8_t* vals;
+  const u64* kfirst;
+  const u64* vfirst;
 };
 
 // Lane 0 appends block b to a worklist (the big path's or the spill path's).
@@ -569,6 +632,98 @@ struct Src16 {
   __device__ __forceinline__ uint4 operator()(int x) const { return lds_window16(win, x); }
 };
 
+// ------------------------------------------------------------------ copy destinations
+// Slotted layout: chunk c of the block's stream goes to slot + 16 c; chunks up to npad (the
+// 128-byte line) are written, bytes past the stream (tot) zeroed.
+struct SlotDst {
+  uint8_t* p;
+  u32 npad, tot;
+  __device__ __forceinline__ void put(u32 c, uint4 acc, bool act) const {
+    const u32 x0 = 16 * c;
+    if (act && x0 + 16 > tot) acc = keep_head(acc, tot - x0);
+    const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
+#ifdef TPZ_ABL_NOSTORE
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+#else
+    if (c < npad) *reinterpret_cast<uint4*>(p + x0) = v;
+#endif
+  }
+};
+
+// Bytes [lo, hi) of the 16-byte chunk v to p[lo .. hi) (p 16-aligned), in naturally aligned
+// pieces: the bytes around them belong to the neighbouring block's keys or values, which
+// another wave writes.
+__device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, u32 lo, u32 hi) {
+  const u64 q0 = (u64)v.y << 32 | v.x, q1 = (u64)v.w << 32 | v.z;
+  auto bytes = [&](u32 a) -> u64 {   // the 8 bytes from a (a < 16)
+    return a == 0 ? q0 : a >= 8 ? (q1 >> (8 * (a - 8))) : ((q0 >> (8 * a)) | (q1 << (64 - 8 * a)));
+  };
+  u32 a = lo;
+  if ((a & 1u) && a + 1 <= hi) { p[a] = (uint8_t)bytes(a); a += 1; }
+  if ((a & 2u) && a + 2 <= hi) { *reinterpret_cast<uint16_t*>(p + a) = (uint16_t)bytes(a); a += 2; }
+  if ((a & 4u) && a + 4 <= hi) { *reinterpret_cast<u32*>(p + a) = (u32)bytes(a); a += 4; }
+  if ((a & 8u) && a + 8 <= hi) { *reinterpret_cast<u64*>(p + a) = bytes(a); a += 8; }
+  if (a + 8 <= hi) { *reinterpret_cast<u64*>(p + a) = bytes(a); a += 8; }
+  if (a + 4 <= hi) { *reinterpret_cast<u32*>(p + a) = (u32)bytes(a); a += 4; }
+  if (a + 2 <= hi) { *reinterpret_cast<uint16_t*>(p + a) = (uint16_t)bytes(a); a += 2; }
+  if (a + 1 <= hi) p[a] = (uint8_t)bytes(a);
+}
+
+// Flat layout: the block's keys go to keys[kf ..] and its values to vals[vf ..], back to back
+// with the neighbouring blocks'. The copy runs over a virtual stream whose chunks line up with
+// the columns' 16-byte chunks: key byte x at 16-aligned position dk + x (dk = kf mod 16), value
+// byte y at 16 kch + dv + y (kch = the key chunks, dv = vf mod 16). Whole chunks are stored
+// with one 16-byte store; a column's first and last chunk hold the neighbours' bytes too and
+// are stored piecewise (store_partial). The stores go through two descriptors that end at the
+// block's last key / value chunk.
+struct FlatOut {
+  __amdgpu_buffer_rsrc_t rk, rv;   // from the key / value chunk base, 16 kch / 16 vch bytes
+  uint8_t* kb;                     // the 16-aligned key / value chunk bases
+  uint8_t* vb;
+  u32 kch, vch;                    // chunks of each column
+  u32 klo, khi, vlo, vhi;          // valid bytes [lo, hi) of the first / last chunk
+  __device__ __forceinline__ void put(u32 c, uint4 acc, bool skip) const {
+    const bool isk = c < kch;
+    const u32 jv = c - kch;
+    const bool isv = !isk && jv < vch;
+    const u32 lo = isk ? (c == 0 ? klo : 0u) : (jv == 0 ? vlo : 0u);
+    const u32 hi = isk ? (c + 1 == kch ? khi : 16u) : (jv + 1 == vch ? vhi : 16u);
+    const bool full = lo == 0 && hi == 16;
+    const auto v4 = __builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc);
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (!skip && isk && full) ? 16 * c : kOob, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (!skip && isv && full) ? 16 * jv : kOob, 0, 0);
+    const bool part = !skip && (isk || isv) && !full;
+    if (__ballot(part) && part) store_partial(isk ? kb + 16 * c : vb + 16 * jv, acc, lo, hi);
+  }
+};
+// The flat destination of block b with K key and V value bytes (dk / dv: its column starts mod 16).
+__device__ __forceinline__ FlatOut flat_out(const Out& o, u64 kf, u64 vf, u32 K, u32 V) {
+  FlatOut D;
+  const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
+  D.kch = K ? (dk + K + 15) >> 4 : 0u;
+  D.vch = V ? (dv + V + 15) >> 4 : 0u;
+  D.kb = o.keys + (kf & ~15ull);
+  D.vb = o.vals + (vf & ~15ull);
+  D.rk = __builtin_amdgcn_make_buffer_rsrc(D.kb, (short)0, (int)(16 * D.kch), 0x00020000);
+  D.rv = __builtin_amdgcn_make_buffer_rsrc(D.vb, (short)0, (int)(16 * D.vch), 0x00020000);
+  D.klo = dk;
+  D.khi = dk + K - 16 * (D.kch ? D.kch - 1 : 0u);
+  D.vlo = dv;
+  D.vhi = dv + V - 16 * (D.vch ? D.vch - 1 : 0u);
+  return D;
+}
+// Where the virtual stream's values start: the key chunks, then dv (flat); value_start(K)
+// (slotted).
+template <bool FLAT>
+__device__ __forceinline__ u32 stream_vstart(u32 K, u32 dk, u32 dv) {
+  return FLAT ? (K ? (dk + K + 15) & ~15u : 0u) + dv : (K + 15) & ~15u;
+}
+// The flat destination's put as a copy_window destination (every active chunk stored).
+struct FlatDst {
+  const FlatOut* d;
+  __device__ __forceinline__ void put(u32 c, uint4 acc, bool act) const { d->put(c, acc, !act); }
+};
+
 // Output-driven copy of a block's stream (tot bytes: the keys, a gap to the next 16-byte
 // boundary, the values): the wave takes 64 output chunks of 16 B per window (lane l: chunk
 // c = 64 w + l), so every store is a coalesced 1 KiB.
@@ -584,10 +739,9 @@ struct Src16 {
 //      its bytes are unspecified.
 //   4. store; pad chunks up to the 128-byte line are zeroed.
 // One window of the copy (chunks 64 w .. 64 w + 63); returns the carry for the next window.
-template <class Col, class MapT, class S>
+template <class Col, class MapT, class S, class D>
 __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const MapT* map, u32 nk,
-                                           u32 tot, u32 npad, uint8_t* dst, u32 map_len, u32 w,
-                                           u32 carry) {
+                                           u32 tot, const D& dst, u32 map_len, u32 w, u32 carry) {
   const u32 nch = (tot + 15) >> 4;
   const u32 lane = lane_id();
   const u32 last = nk ? nk - 1 : 0u;
@@ -635,30 +789,24 @@ __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const M
       acc.w = (acc.w & ~byte_mask(lo, hi, 3)) | (v.w & byte_mask(lo, hi, 3));
     }
   }
-  // 4. store (bytes past the stream and pad chunks up to the 128-byte line are zeroed)
-  if (act && x0 + 16 > tot) acc = keep_head(acc, tot - x0);
-  const uint4 v = make_uint4(act ? acc.x : 0u, act ? acc.y : 0u, act ? acc.z : 0u, act ? acc.w : 0u);
-#ifdef TPZ_ABL_NOSTORE
-  asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-#else
-  if (c < npad) *reinterpret_cast<uint4*>(dst + x0) = v;
-#endif
+  // 4. store (slotted: bytes past the stream and pad chunks up to the 128-byte line are zeroed)
+  dst.put(c, acc, act);
   return carry_out;
 }
 
-template <class Col, class MapT, class S>
+template <class Col, class MapT, class S, class D>
 __device__ __forceinline__ void copy_stream(const S& src, const Col& col, const MapT* map, u32 nk,
-                                            u32 tot, uint8_t* dst, u32 map_len) {
+                                            u32 tot, const D& dst, u32 map_len) {
   const u32 lane = lane_id();
   const u32 nch = (tot + 15) >> 4;
   const u32 npad = (nch + 7) & ~7u;                   // whole 128-byte lines
   const u32 nw = (npad + 63) >> 6;
 #ifdef TPZ_ABL_MEMONLY
-  for (u32 c = lane; c < npad; c += 64) *reinterpret_cast<uint4*>(dst + c * 16) = make_uint4(c, 0, 0, 0);
+  for (u32 c = lane; c < npad; c += 64) dst.put(c, make_uint4(c, 0, 0, 0), c < nch);
   return;
 #endif
   u32 carry = 0;
-  for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, tot, npad, dst, map_len, w, carry);
+  for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, tot, dst, map_len, w, carry);
 }
 
 // ------------------------------------------------------------------ fused copy + CRC (wave path)
@@ -674,8 +822,32 @@ struct CrcLane {
   int seg;      // the lane's run [seg, seg + 80) relative to the payload start (end-aligned)
   bool act;     // the run overlaps the payload
   u32 c;        // the run's raw CRC so far
+#ifdef TPZ_CRC_SARW
+  u32 c2;       // the second byte chain: the run's last 40 bytes
+  u32 lr;       // the lane's table replica
+#endif
 };
 
+#ifdef TPZ_CRC_SARW
+// Step t: bytes [8t, 8t + 8) of each of the run's two 40-byte halves, one byte chain per half.
+__device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
+                                         int t) {
+  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+  const u32* rep = crc_rep(tab);
+  const int a = L.act ? pb + L.seg + 8 * t : -kGuard;  // 8-byte aligned either way
+  const int a2 = L.act ? a + kCrcChainBytes : -kGuard;
+  const u32x2 w = *reinterpret_cast<const u32x2*>(win + a);
+  const u32x2 w2 = *reinterpret_cast<const u32x2*>(win + a2);
+  L.c = sarw4(rep, L.lr, L.c, w.x);
+  L.c2 = sarw4(rep, L.lr, L.c2, w2.x);
+  L.c = sarw4(rep, L.lr, L.c, w.y);
+  L.c2 = sarw4(rep, L.lr, L.c2, w2.y);
+}
+// The run's raw CRC: the first half's chain shifted past the second half, XOR the second's.
+__device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) {
+  return crc_shift_chain(tab, L.c) ^ L.c2;
+}
+#else
 __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
                                          int t) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
@@ -683,6 +855,8 @@ __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int
   const u32x4 w = *reinterpret_cast<const u32x4*>(win + a);
   L.c = slice16(tab, w.x ^ L.c, w.y, w.z, w.w);
 }
+__device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) { return L.c; }
+#endif
 
 struct FastWin {
   u32 nk, tot, nch, npad, last;
@@ -691,9 +865,10 @@ struct FastWin {
 
 // The common path of copy_window, branch-free; returns the carry, sets bit w of `rare` when any
 // lane of the window needs copy_window's rare path.
-template <class S>
+template <bool FLAT, class S>
 __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, const uint16_t* map,
-                                         const FastWin& F, u32 w, u32 carry, u32& rare) {
+                                         const FastWin& F, const FlatOut& D, u32 w, u32 carry,
+                                         u32& rare) {
   const u32 lane = lane_id();
   const u32 c = 64 * w + lane;
   const u32 x0 = 16 * c;
@@ -712,9 +887,13 @@ __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, cons
   const bool rw = __ballot(act && (e0 <= x0 || (cross && e1 < x0 + 16 && j + 2 < F.nk))) != 0;
   if (rw) rare |= 1u << w;
   if (cross) acc = merge_at(acc, nx, (int)(e0 - x0));
-  // an idle lane read the zeroed guard: its pad chunk stores zeros without a select
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
-                                         F.out, rw ? kOob : x0, 0, 0);
+  if (FLAT) {
+    D.put(c, acc, rw);
+  } else {
+    // an idle lane read the zeroed guard: its pad chunk stores zeros without a select
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
+                                           F.out, rw ? kOob : x0, 0, 0);
+  }
   return carry_out;
 }
 
@@ -723,9 +902,10 @@ __device__ __forceinline__ u32 copy_fast(const S& src, const ColSmall& col, cons
 // then names the earlier one). Entries j .. j+3 come from two ds_read2_b32; the chunk starts in
 // j or j + 1 and takes up to three segments' bytes. Anything longer (segments under 8 bytes)
 // is left to copy_window.
-template <class S>
+template <bool FLAT, class S>
 __device__ __forceinline__ u32 copy_fast3(const S& src, const ColSmall& col, const uint16_t* map,
-                                          const FastWin& F, u32 w, u32 carry, u32& rare) {
+                                          const FastWin& F, const FlatOut& D, u32 w, u32 carry,
+                                          u32& rare) {
   const u32 lane = lane_id();
   const u32 c = 64 * w + lane;
   const u32 x0 = 16 * c;
@@ -750,8 +930,11 @@ __device__ __forceinline__ u32 copy_fast3(const S& src, const ColSmall& col, con
   if (rw) rare |= 1u << w;
   if (b1) acc = merge_at(acc, n1, (int)(e0 - x0));
   if (b2) acc = merge_at(acc, n2, (int)(e1 - x0));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
-                                         F.out, rw ? kOob : x0, 0, 0);
+  if (FLAT)
+    D.put(c, acc, rw);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc),
+                                           F.out, rw ? kOob : x0, 0, 0);
   return carry_out;
 }
 
@@ -762,48 +945,72 @@ __device__ __forceinline__ u32 copy_fast3(const S& src, const ColSmall& col, con
 // windows with the CRC steps (3 % slower on the 4k config, profiles/r3/bisect_4k.jsonl).
 // The stream's last chunk carries no bytes of other blocks or of earlier ones: every byte a
 // chunk reads past its last segment lies in the block or in the 16 zeroed bytes after the payload.
-template <bool SHORT, class S>
+template <bool SHORT, bool FLAT, class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
-                                              const uint8_t* win, int pb, u32 Pa, u32 kshift,
-                                              Stamps& St) {
+                                              const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
+                                              u32 kshift, Stamps& St) {
   constexpr bool short_segs = SHORT;
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
   F.tot = tot;
   F.nch = (tot + 15) >> 4;
-  F.npad = (F.nch + 7) & ~7u;
+  F.npad = FLAT ? F.nch : (F.nch + 7) & ~7u;   // flat: no line padding (the neighbours' bytes)
   F.last = nk ? nk - 1 : 0u;
-  F.out = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)(F.npad * 16), 0x00020000);
+  F.out = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, FLAT ? 0 : (int)(F.npad * 16), 0x00020000);
   const u32 nw = (F.npad + 63) >> 6;
   CrcLane L;
   L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
   L.act = L.seg + kCrcLaneBytes > 0;
   L.c = 0;
+#ifdef TPZ_CRC_SARW
+  L.c2 = 0;
+  L.lr = lane & 31u;
+#endif
   u32 carry = 0, rare = 0, cw[5];
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     cw[t] = carry;
     crc_step(tab, win, pb, L, t);
-    carry = short_segs ? copy_fast3(src, col, map, F, (u32)t, carry, rare)
-                       : copy_fast(src, col, map, F, (u32)t, carry, rare);
+    carry = short_segs ? copy_fast3<FLAT>(src, col, map, F, D, (u32)t, carry, rare)
+                       : copy_fast<FLAT>(src, col, map, F, D, (u32)t, carry, rare);
   }
   cw[4] = carry;
   crc_step(tab, win, pb, L, 4);
   if (nw > 4)
-    carry = short_segs ? copy_fast3(src, col, map, F, 4u, carry, rare)
-                       : copy_fast(src, col, map, F, 4u, carry, rare);
+    carry = short_segs ? copy_fast3<FLAT>(src, col, map, F, D, 4u, carry, rare)
+                       : copy_fast<FLAT>(src, col, map, F, D, 4u, carry, rare);
   TPZ_STAMP(St, 4);
 #ifdef TPZ_ABL_STAMPS
   St.rare += __builtin_popcount(rare);
 #endif
   if (rare) {
     for (u32 w = 0; w < nw; w++)
-      if (rare & (1u << w)) copy_window(src, col, map, nk, F.tot, F.npad, dst, (u32)kWaveMapLen, w, cw[w]);
+      if (rare & (1u << w)) {
+        if (FLAT)
+          copy_window(src, col, map, nk, F.tot, FlatDst{&D}, (u32)kWaveMapLen, w, cw[w]);
+        else
+          copy_window(src, col, map, nk, F.tot, SlotDst{dst, F.npad, F.tot}, (u32)kWaveMapLen, w, cw[w]);
+      }
   }
-  return L.c;   // the lane's raw run CRC: crc_combine gives R0 of the whole range
+  return crc_lane_value(tab, L);   // the lane's raw run CRC: crc_combine gives R0 of the range
 }
+
+#ifdef TPZ_CRC_SARW
+// wave_crc for a wave-path block (Pa <= 5120) with the byte chains of crc_step.
+__device__ __forceinline__ u32 wave_crc_w(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
+  const u32 lane = lane_id();
+  CrcLane L;
+  L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
+  L.act = L.seg + kCrcLaneBytes > 0;
+  L.c = L.c2 = 0;
+  L.lr = lane & 31u;
+#pragma unroll
+  for (int t = 0; t < kCrcLaneBytes / 16; t++) crc_step(tab, win, pb, L, t);
+  return crc_combine(tab, crc_lane_value(tab, L));
+}
+#endif
 
 // The wave path defers a block's CRC combine and status write into the next block's decode
 // (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
@@ -817,8 +1024,8 @@ struct PendingCrc {
 __device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
   if (!pd.live) return;
   const u32 R = crc_combine(tab, pd.lc);
-  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
-                                                                 : ~crc_unshift_small(tab, R, pd.k);
+  const u32 crc = (R == crc_shift_small_w(tab, ~pd.stored, pd.k)) ? pd.stored
+                                                                   : ~crc_unshift_small_w(tab, R, pd.k);
   const bool ok = crc == pd.stored;                                            // checksum.rs:17
   put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
   pd.live = 0;
@@ -826,7 +1033,7 @@ __device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, Pen
 
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. `map` is the
 // stream's chunk map (kMapLen slots, LDS), `col` its entry table.
-template <class Col, class MapT, int kMapLen, bool BIG>
+template <class Col, class MapT, int kMapLen, bool BIG, bool FLAT = false>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
                                              const Out& o, u32 kshift, Stamps& S, PendingCrc& pd) {
@@ -840,6 +1047,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   const u32 tag = win[(int)(a0 + len) - 1];                                    // compress.rs:99
   const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));      // block.rs:51
   const u32 n = lds_be16(win, a0);                                             // block.rs:54
+  // flat layout: the block's first key / value byte in the columns (tpz_flat_layout)
+  const u64 kf = FLAT ? o.kfirst[b] : 0ull, vf = FLAT ? o.vfirst[b] : 0ull;
+  const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
 #ifndef TPZ_ABL_NODEFER
   finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
 #endif
@@ -858,17 +1068,21 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   bool f_short = false;        // segments under 16 bytes (copy_fast3)
   u32 f_nk = 0, f_tot = 0;
   uint8_t* f_dst = nullptr;
+  FlatOut fo;                  // flat: the block's destination in the key / value columns
   if (P < 2 || P < 2 + 2 * n) {                                                // block.rs:54-59
     st = TPZ_BLOCK_MALFORMED;
     cnt = 0;
   } else if (!BIG && n > kWaveMaxN) {
-    defer_to(o.defer_list, o.defer_count, b);
+    // the LDS big path (slotted); the spill path writes the flat columns directly
+    if (FLAT) defer_to(o.spill_list, o.spill_count, b);
+    else defer_to(o.defer_list, o.defer_count, b);
     return;
   } else {
 #ifndef TPZ_ABL_NOPARSE
     const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
     const u32 dl = P - 2 - 2 * n;
-    const bool slots_fit = 6u * n <= len;
+    // (flat: the exact ends, n pairs reserved for every block by tpz_flat_layout)
+    const bool slots_fit = FLAT || 6u * n <= len;
     uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
     // whole 128-byte lines of {kend, vend} in the slotted layout; exactly n in the exact one
     const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
@@ -936,7 +1150,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         ktot = readlane(ki, 63);
         knz_all = __builtin_popcountll(kmask);
       }
-      const u32 vs = (ktot + 15) & ~15u;  // value stream start (tpz_value_start)
+      const u32 vs = stream_vstart<FLAT>(ktot, dk, dv);  // value stream start (tpz_value_start)
 #ifndef TPZ_ABL_NOENDS
       __builtin_amdgcn_raw_buffer_store_b64(
           __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
@@ -948,8 +1162,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         // after the segment's end (ends beyond the map only occur in blocks that spill)
         if (kl) {
           const u32 m = knz + lanes_below(kmask);
-          col.put(m, ki, (int)(db + off + 2) - (int)(ki - kl));
-          if (((ki + 15) >> 4) < (u32)kMapLen) map[(ki + 15) >> 4] = (MapT)(m + 1);
+          const u32 ke = ki + dk;   // the key's end in the stream (flat: shifted by dk)
+          col.put(m, ke, (int)(db + off + 2) - (int)(ke - kl));
+          if (((ke + 15) >> 4) < (u32)kMapLen) map[(ke + 15) >> 4] = (MapT)(m + 1);
         }
         if (vl) {
           const u32 m = knz_all + vnz + lanes_below(vmask);
@@ -964,9 +1179,11 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       vc = readlane(vi, 63);
     }
 
-    const u32 vs = (kc + 15) & ~15u;
+    const u32 vs = stream_vstart<FLAT>(kc, dk, dv);
     TPZ_STAMP(S, 2);
-    if (bad || !slots_fit || vs + vc > len + 2) {   // the slot holds len + 129 bytes
+    // the slot holds len + 129 bytes; the flat stream has at most len + 2 + 45 bytes for
+    // entries that neither overlap nor repeat (the map's length)
+    if (bad || !slots_fit || vs + vc > len + (FLAT ? 47u : 2u)) {
       // entries out of range (Ok(Block) with per-entry classes: TPZ_BLOCK_BAD_ENTRY), or
       // entries that overlap or repeat: the spill path decodes the block (CRC included)
       defer_to(o.spill_list, o.spill_count, b);
@@ -984,11 +1201,18 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         f_short = short_segs;
         f_nk = knz + vnz;
         f_tot = vs + vc;
-        f_dst = o.data + slot_base(ext_b, b);
+        f_dst = FLAT ? nullptr : o.data + slot_base(ext_b, b);
+        if (FLAT) fo = flat_out(o, kf, vf, kc, vc);
       } else
 #endif
-      copy_stream(Src16{win}, col, map, knz + vnz, vs + vc, o.data + slot_base(ext_b, b),
-                  (u32)kMapLen);
+      if (FLAT) {
+        fo = flat_out(o, kf, vf, kc, vc);
+        copy_stream(Src16{win}, col, map, knz + vnz, vs + vc, FlatDst{&fo}, (u32)kMapLen);
+      } else {
+        const u32 nch = (vs + vc + 15) >> 4;
+        copy_stream(Src16{win}, col, map, knz + vnz, vs + vc,
+                    SlotDst{o.data + slot_base(ext_b, b), (nch + 7) & ~7u, vs + vc}, (u32)kMapLen);
+      }
 #endif
     }
     TPZ_STAMP(S, 3);
@@ -1013,12 +1237,12 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     u32 R;
     if (!BIG && fuse) {
       const u32 lc = f_short
-          ? copy_crc_fused<true>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                                 reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
-                                 P + k, kshift, S)
-          : copy_crc_fused<false>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
-                                  reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, win, pb,
-                                  P + k, kshift, S);
+          ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                                       reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
+                                       fo, win, pb, P + k, kshift, S)
+          : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
+                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
+                                        fo, win, pb, P + k, kshift, S);
 #ifndef TPZ_ABL_NODEFER
       pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
       return;
@@ -1026,9 +1250,17 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       R = crc_combine(tab, lc);
 #endif
     } else {
-      R = wave_crc(tab, win, pb, P + k);
+#ifdef TPZ_CRC_SARW
+      if constexpr (!BIG) {
+        R = wave_crc_w(tab, win, pb, P + k);
+      } else
+#endif
+        R = wave_crc(tab, win, pb, P + k);
     }
-    crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+    if constexpr (BIG)
+      crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
+    else
+      crc = (R == crc_shift_small_w(tab, ~stored, k)) ? stored : ~crc_unshift_small_w(tab, R, k);
 #if defined(TPZ_ABL_NOCF) || defined(TPZ_ABL_LUTVALU)
     asm volatile("" ::"v"(R));   // keep the CRC work, report a match (timing builds only)
     crc = stored;
@@ -1092,6 +1324,7 @@ struct Params {
   u64 src_bytes;
   u32 n_blocks;
   const u32* crc_tables;
+  const u32* wave_tables;  // the wave path's table image (TPZ_CRC_SARW builds)
   Out out;
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
@@ -1109,9 +1342,15 @@ constexpr u32 kOnchipMask = 4095;
 // diagnostic: each wave's start and end time (s_memrealtime, 100 MHz) and block count
 __device__ unsigned long long g_wave_ends[3 * 8192];
 #endif
+template <bool FLAT>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
+#ifdef TPZ_CRC_SARW
+  // [T_0 x 32 replicas][ids 16..44]: tab[id * 256 + b] reaches ids >= 16 (crc_rep gives T_0)
+  u32* tab = reinterpret_cast<u32*>(lds) + 8192 - 16 * 256;
+#else
   u32* tab = reinterpret_cast<u32*>(lds);
+#endif
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
 #ifdef TPZ_ABL_XGLOBAL
@@ -1128,7 +1367,16 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef TPZ_CRC_SARW
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(p.wave_tables);
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < kWaveTabBytes / 16; i += blockDim.x) d[i] = s[i];
+    __syncthreads();
+  }
+#else
   load_tables(tab, p.crc_tables);
+#endif
 
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
@@ -1136,11 +1384,11 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #ifdef TPZ_ABL_PRIO
   if (wid & 1u) __builtin_amdgcn_s_setprio(1);   // diagnostic: static priority for half the waves
 #endif
-  uint8_t* slot = lds + kTableBytes + wid * kSlotBytes;
+  uint8_t* slot = lds + kWaveTabBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
   const ColSmall col{reinterpret_cast<u32*>(etab)};
-  uint16_t* map = reinterpret_cast<uint16_t*>(etab + 512 * 4);
+  uint16_t* map = reinterpret_cast<uint16_t*>(etab + kWaveTabSlots * 4);
 
   if (lane < kGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   const u32 nw = gridDim.x * kWavesPerWG;
@@ -1224,7 +1472,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     u32 nent = 0xFFFFu;
     if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
     const bool to_bw = lng && nent < 64 && p.out.bw_list && ge - gs <= TPZ_BIGWAVE_BLOCK_BYTES;
-    const bool to_spill = lng && !to_bw && ge - gs > kBigMaxLen;
+    // (flat: every long block to the spill path, which writes the columns directly)
+    const bool to_spill = lng && !to_bw && (FLAT || ge - gs > kBigMaxLen);
     if (p.out.bw_list) defer_lanes(p.out.bw_list, p.out.bw_count, to_bw, (u32)bb);
     defer_lanes(p.out.spill_list, p.out.spill_count, to_spill, (u32)bb);
     defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
@@ -1329,7 +1578,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #else
       const u32 bdec = bcur;
 #endif
-      decode_block<ColSmall, uint16_t, kWaveMapLen, false>(tab, win, col, map, (u32)(s & 15u),
+      decode_block<ColSmall, uint16_t, kWaveMapLen, false, FLAT>(tab, win, col, map, (u32)(s & 15u),
                                                            len64, bdec, s, p.out, kshift, S, pd);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
@@ -1571,7 +1820,7 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     for (u32 j = wid; j < nw; j += kBigWaves) {
       u32 m = lane < j ? wmax[lane] : 0u;
       if (lane + 64 < j) m = max(m, wmax[lane + 64]);
-      copy_window(Src16{win}, col, map, nk, tot, npad, dst, (u32)kBigMapLen, j, wave_max(m));
+      copy_window(Src16{win}, col, map, nk, tot, SlotDst{dst, npad, tot}, (u32)kBigMapLen, j, wave_max(m));
     }
     TPZ_STAMP(S, 3);
   }
@@ -1796,10 +2045,12 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.src_bytes = a.src_bytes;
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
+  p.wave_tables = a.wave_tables;
   p.big_scratch = a.big_scratch;
   p.spill_used = a.spill_used;
   p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count,
-              a.spill_list, a.spill_count, a.bw_list, a.bw_count, a.efirst};
+              a.spill_list, a.spill_count, a.bw_list, a.bw_count, a.efirst,
+              a.keys, a.vals, a.kfirst, a.vfirst};
   const u32* xp = big_super_shifts();
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   const u32* ls = lane_run_shifts();
@@ -1816,7 +2067,10 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
-  hipLaunchKernelGGL(decode_wave_kernel, dim3(grid), dim3(kWGThreads), 0, stream, p);
+  if (a.keys)
+    hipLaunchKernelGGL(decode_wave_kernel<true>, dim3(grid), dim3(kWGThreads), 0, stream, p);
+  else
+    hipLaunchKernelGGL(decode_wave_kernel<false>, dim3(grid), dim3(kWGThreads), 0, stream, p);
   if (a.bw_list)
     launch_bigwave(BigWaveLaunch{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.data, a.ends,
                                  a.count, a.status, a.crc, a.spill_list, a.spill_count, a.defer_list,
@@ -1825,7 +2079,8 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   const sp::SpillParams spp = sp::spill_params(SpillLaunch{a.src, a.ext, a.src_bytes, a.crc_tables,
                                                            a.spill_list, a.spill, a.spill_cap,
                                                            a.spill_off, a.spill_used, a.count,
-                                                           a.status, a.crc});
+                                                           a.status, a.crc, a.ends, a.efirst,
+                                                           a.keys, a.vals, a.kfirst, a.vfirst});
   hipLaunchKernelGGL(decode_tail_kernel, dim3(a.big_grid), dim3(kBigThreads), 0, stream, p, spp, a.tail);
 }
 

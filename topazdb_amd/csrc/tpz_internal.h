@@ -30,6 +30,10 @@ constexpr int kNumCrcTables = 41;
 constexpr int kCrcInvTable = 40;
 constexpr int kCrcLaneBytes = 80;
 constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
+// The wave path's table image (tpz_api.cpp build_wave_tables): T_0 replicated 32 times (8192
+// words), the decode tables' ids 16..40, then the shift by kCrcChainBytes (ids 41..44).
+constexpr int kCrcChainBytes = 40;
+constexpr int kWaveTableWords = 8192 + (kNumCrcTables - 16 + 4) * 256;
 // Big path entry-table capacity per block and column: slots are only written when 6n <= len
 // (the unified key+value table holds 2 x this).
 constexpr uint32_t kBigMaxSlots = TPZ_LDS_BLOCK_BYTES / 6 + 16;
@@ -76,6 +80,7 @@ struct LaunchArgs {
   uint64_t src_bytes;
   uint32_t n_blocks;
   const uint32_t* crc_tables;
+  const uint32_t* wave_tables;   // the wave path's LDS table image (kWaveTableWords)
   uint8_t* data;
   uint32_t* ends;
   uint32_t* count;
@@ -96,6 +101,12 @@ struct LaunchArgs {
   uint32_t* bw_count;     // tail + kTailBw
   const uint32_t* rep;    // replicated slice-by-4 tables (the bigwave phase's CRC)
   const uint64_t* efirst; // exact ends layout (tpz_columns.d_entry_first) or null
+  // flat layout (tpz_decode_blocks_flat): key / value columns and the blocks' first key / value
+  // byte in them; null: slotted (data)
+  uint8_t* keys;
+  uint8_t* vals;
+  const uint64_t* kfirst;
+  const uint64_t* vfirst;
   uint32_t* tail;         // workspace: kTailCounters, zero at the launch (the tail kernel
                           // leaves them zero)
 };
@@ -187,6 +198,15 @@ struct SpillLaunch {
   uint32_t* count;
   uint8_t* status;
   uint32_t* crc;
+  // flat layout (keys non-null): the spill path writes the block's ends to
+  // ends[2 * efirst[b] ..], its keys to keys[kfirst[b] ..] and its values to vals[vfirst[b] ..];
+  // its arena record holds only a BAD_ENTRY block's class bytes
+  uint32_t* ends;
+  const uint64_t* efirst;
+  uint8_t* keys;
+  uint8_t* vals;
+  const uint64_t* kfirst;
+  const uint64_t* vfirst;
 };
 
 struct CrcLaunch {
@@ -267,6 +287,12 @@ void launch_pack_ends(const PackLaunch& a, hipStream_t stream);
 // d_first[i] = sum of the header n of blocks < i (tpz_entry_first); `part` = workspace of
 // entry_first_parts(n_blocks) u64.
 uint64_t entry_first_parts(uint32_t n_blocks);
+// tpz_flat_layout (tpz_flat.hip): first = 3 x (n_blocks + 1) u64 (entries, key bytes, value
+// bytes: exclusive prefixes, totals at [n_blocks]); `part` = flat_scan_parts_words(n_blocks) u64.
+uint64_t flat_scan_parts_words(uint32_t n_blocks);
+void launch_flat_layout(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
+                        uint32_t n_blocks, uint64_t* first, uint64_t* part, uint32_t num_cus,
+                        hipStream_t stream);
 void launch_entry_first(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
                         uint32_t n_blocks, uint64_t* first, uint64_t* part, hipStream_t stream);
 // first[i] = exclusive prefix of count over decoded (OK / OK_SPILLED) blocks, first[n] = total.

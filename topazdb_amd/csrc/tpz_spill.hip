@@ -74,6 +74,14 @@ struct SpillParams {
   u32* count;
   uint8_t* status;
   u32* crc;
+  // flat layout (keys non-null, tpz_decode_blocks_flat): ends, keys and values straight into the
+  // caller's columns; the arena record holds only a BAD_ENTRY block's class bytes
+  u32* ends;
+  const u64* efirst;
+  uint8_t* keys;
+  uint8_t* vals;
+  const u64* kfirst;
+  const u64* vfirst;
   u32 xp[64];            // x^(8 * 2^j) mod P
 };
 
@@ -293,13 +301,19 @@ __device__ __forceinline__ void spill_block(const SpillParams& p, SpillLds& L, u
   const u64 K = wg_sum64(kt, red), V = wg_sum64(vt, red), B = wg_sum64(bad, red);
   // ---- the record: ends, then the stream (keys | values from value_start(K)), then for a
   // block with bad entries their classes (Ok(Block) either way: block.rs:46-65)
-  const u64 need = spill_record_bytes(n, K, V) + (B ? (((u64)n + 127u) & ~127ull) : 0u);
+  // (flat: the columns hold the entries; a record only for the class bytes of a bad block)
+  const bool flat = p.keys != nullptr;
+  const u64 ncls = B ? (((u64)n + 127u) & ~127ull) : 0u;
+  const u64 need = flat ? ncls : spill_record_bytes(n, K, V) + ncls;
   if (tid == 0) {
-    const u64 off = atomicAdd(reinterpret_cast<unsigned long long*>(p.spill_used),
-                              (unsigned long long)need);
-    const bool fits = off + need <= p.spill_cap;
-    L.shared_off = fits ? off : ~0ull;
-    p.spill_off[b] = fits ? off : need;
+    u64 off = 0;
+    if (need) {
+      off = atomicAdd(reinterpret_cast<unsigned long long*>(p.spill_used), (unsigned long long)need);
+      const bool fits = off + need <= p.spill_cap;
+      p.spill_off[b] = fits ? off : need;
+      off = fits ? off : ~0ull;
+    }
+    L.shared_off = off;
   }
   __syncthreads();
   const u64 roff = L.shared_off;
@@ -307,10 +321,11 @@ __device__ __forceinline__ void spill_block(const SpillParams& p, SpillLds& L, u
     put_meta(p, b, TPZ_BLOCK_SPILL_FULL, n, crc);
     return;
   }
-  u32* ends = reinterpret_cast<u32*>(p.spill + roff);
+  u32* ends = flat ? p.ends + 2 * p.efirst[b] : reinterpret_cast<u32*>(p.spill + roff);
   uint8_t* stream = p.spill + roff + spill_stream(n);
-  uint8_t* classes = p.spill + roff + spill_record_bytes(n, K, V);
-  const u64 vs = value_start(K);
+  uint8_t* classes = flat ? p.spill + roff : p.spill + roff + spill_record_bytes(n, K, V);
+  uint8_t* kdst = flat ? p.keys + p.kfirst[b] : stream;
+  uint8_t* vdst = flat ? p.vals + p.vfirst[b] : stream + value_start(K);
   u32 kc = 0, vc = 0;
   for (u32 r0 = 0; r0 < n; r0 += kThreads) {
     const u32 i = r0 + tid;
@@ -329,14 +344,14 @@ __device__ __forceinline__ void spill_block(const SpillParams& p, SpillLds& L, u
     const u32 m = n - r0 < (u32)kThreads ? n - r0 : (u32)kThreads;
     for (u32 j = wid; j < m; j += kWaves) {
       const Entry ej = parse(blk, db, dl, r0 + j);
-      wave_copy(stream + e_kst[j], blk + db + ej.off + 2, ej.kl);
-      wave_copy(stream + vs + e_vst[j], blk + db + ej.off + 4 + ej.kl, ej.vl);
+      wave_copy(kdst + e_kst[j], blk + db + ej.off + 2, ej.kl);
+      wave_copy(vdst + e_vst[j], blk + db + ej.off + 4 + ej.kl, ej.vl);
     }
     kc += ktot;
     vc += vtot;
     __syncthreads();
   }
-  put_meta(p, b, B ? TPZ_BLOCK_BAD_ENTRY : TPZ_BLOCK_OK_SPILLED, n, crc);
+  put_meta(p, b, B ? TPZ_BLOCK_BAD_ENTRY : flat ? TPZ_BLOCK_OK : TPZ_BLOCK_OK_SPILLED, n, crc);
 }
 
 // Phase C of decode_tail_kernel (tpz_decode.hip): the cnt blocks of the spill list, one per
@@ -375,6 +390,12 @@ SpillParams spill_params(const SpillLaunch& a) {
   p.count = a.count;
   p.status = a.status;
   p.crc = a.crc;
+  p.ends = a.ends;
+  p.efirst = a.efirst;
+  p.keys = a.keys;
+  p.vals = a.vals;
+  p.kfirst = a.kfirst;
+  p.vfirst = a.vfirst;
   // x^(8 * 2^j) mod P by repeated squaring, from x^8
   u32 x = 0x80000000u >> 8;
   for (int j = 0; j < 64; j++) {
