@@ -41,7 +41,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from topazdb_amd import _lib, synth  # noqa: E402
-from topazdb_amd.batch import DeviceBatch, SlottedColumns, decode_batch, entry_first  # noqa: E402
+from topazdb_amd.batch import (DeviceBatch, FlatColumns, SlottedColumns, decode_batch,  # noqa: E402
+                               entry_first)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
 GIB = float(1 << 30)
@@ -936,6 +937,72 @@ def exact_ends_rate(ctx, batch: DeviceBatch, ext, n_ent, gen, alg: int, dev, ste
     return out
 
 
+def validate_flat(cols: FlatColumns, n_ent: np.ndarray, gen, dev) -> None:
+    """The flat columns against the generator: every block OK with its count, the key column
+    and the value column equal to the generator's keys and values back to back, every
+    {kend, vend} pair at its block's exact offset."""
+    keys, kpos, vals, vpos = gen
+    nb = len(n_ent)
+    assert int((cols.status[:nb] != 0).sum()) == 0, "flat: blocks not OK"
+    assert (cols.count[:nb].cpu().numpy().astype(np.int64) == n_ent).all(), "flat: entry counts"
+    ne = int(n_ent.sum())
+    kb, vb = int(kpos[ne]), int(vpos[ne])
+    assert cols.key_bytes == kb and cols.value_bytes == vb and cols.n_pairs == ne
+    assert torch.equal(cols.keys[:kb], torch.from_numpy(keys[:kb]).to(dev)), "flat: key column"
+    assert torch.equal(cols.values[:vb], torch.from_numpy(vals[:vb]).to(dev)), "flat: value column"
+    e0 = np.zeros(nb + 1, np.int64)
+    np.cumsum(n_ent, out=e0[1:])
+    t_ne = torch.from_numpy(n_ent.astype(np.int64)).to(dev)
+    blk_first = torch.repeat_interleave(torch.from_numpy(e0[:-1]).to(dev), t_ne)
+    ends = cols.ends[:2 * ne].view(-1, 2).to(torch.int64)
+    for col, pos in ((0, kpos), (1, vpos)):
+        tpos = torch.from_numpy(pos[:ne + 1].astype(np.int64)).to(dev)
+        exp = tpos[1:] - tpos[blk_first]
+        assert torch.equal(ends[:, col], exp), "flat: end offsets"
+
+
+def flat_rate(ctx, batch: DeviceBatch, n_ent, gen, alg: int, dev, steps: int, warmup: int) -> dict:
+    """The metric's batch decoded into the flat layout (one dense key column, one dense value
+    column): tpz_flat_layout and tpz_decode_blocks_flat each timed with HIP events on the decode
+    stream, the columns validated against the generator. roofline_frac is the decode's alone
+    (its algorithmic bytes are the slotted decode's: the same key, value and ends bytes);
+    layout_decode_frac counts the sizing pass too."""
+    stream = torch.cuda.current_stream(dev)
+    cols = FlatColumns(ctx, batch, 0, stream)
+    args = (batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(steps):
+            fn()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        return ev0.elapsed_time(ev1) / steps
+    layout_ms = timed(lambda: ctx.flat_layout_ptrs(*args, cols.first.data_ptr(), stream.cuda_stream))
+    ptrs = cols.ptrs()
+    kernel_ms = timed(lambda: ctx.decode_flat_ptrs(*args, ptrs, stream.cuda_stream))
+    ctx.decode_check(stream.cuda_stream)
+    validate_flat(cols, n_ent, gen, dev)
+    src_b = float(batch.src_bytes)
+    out = {"layout_ms": round(layout_ms, 4), "kernel_ms": round(kernel_ms, 4),
+           "gib_s": round(src_b / (kernel_ms * 1e-3) / GIB, 1),
+           "roofline_frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "layout_decode_gib_s": round(src_b / ((layout_ms + kernel_ms) * 1e-3) / GIB, 1),
+           "layout_decode_frac": round(alg / ((layout_ms + kernel_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "layout_read_gb_s": round(src_b / (layout_ms * 1e-3) / 1e9, 1),
+           "key_bytes": cols.key_bytes, "value_bytes": cols.value_bytes, "n_pairs": cols.n_pairs,
+           "device_bytes_per_input_byte": round((cols.key_bytes + cols.value_bytes + 8 * cols.n_pairs
+                                                 + 24 * (batch.n_blocks + 1)) / src_b, 4),
+           "validated": "key and value columns equal the generator's keys and values back to back; "
+                        "every block's status, count and end offsets"}
+    del cols
+    torch.cuda.empty_cache()
+    return out
+
+
 def side_config_rate(ctx, config: str, dev, steps: int, warmup: int) -> dict:
     """BASELINE.json configs[2] (64k) / configs[3] (zipf) at full size on one GPU: the metric's
     decode timing and roofline over that config's generated blocks, every block checked against
@@ -1001,6 +1068,7 @@ def main():
     ap.add_argument("--no-seek", action="store_true")
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-exact", action="store_true")
+    ap.add_argument("--no-flat", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -1074,6 +1142,14 @@ def main():
 
     e2e = None
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
+    flat = None
+    if side and not args.no_flat and full == 1 and part == 0:
+        try:
+            flat = flat_rate(ctx, batch, n_ent, gen, alg, dev, args.steps, args.warmup)
+            log(rank, f"flat: decode {flat['kernel_ms']} ms (frac {flat['roofline_frac']}), "
+                      f"layout {flat['layout_ms']} ms")
+        except Exception as ex:  # reported, never the metric
+            log(rank, f"flat measurement failed: {ex}")
     exact = None
     if side and not args.no_exact and full == 1 and part == 0:
         try:
@@ -1208,6 +1284,7 @@ def main():
             "encode": encode,
             "config5": config5,
             "exact_ends": exact,
+            "flat": flat,
             "zipf": sides.get("zipf"),
             "64k": sides.get("64k"),
         }

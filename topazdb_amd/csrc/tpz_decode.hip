@@ -49,13 +49,7 @@ typedef uint64_t u64;
 
 // ------------------------------------------------------------------ LDS geometry
 constexpr int kWave = 64;
-#ifdef TPZ_ABL_W8
-constexpr int kWavesPerWG = 8;
-#elif defined(TPZ_ABL_W12)
-constexpr int kWavesPerWG = 12;
-#else
 constexpr int kWavesPerWG = 16;
-#endif
 constexpr int kWGThreads = kWave * kWavesPerWG;
 // Blocks a wave of the wave path claims at a time (decode_wave_kernel): 2^chunk_shift, chosen
 // per launch (launch_decode); TPZ_WAVE_CHUNK forces one (diagnostic builds).
@@ -134,12 +128,8 @@ __device__ __forceinline__ u32 lds_u32(const uint8_t* base, u32 a) {
 }
 // Big-endian u16 at byte offset a (bytes::Buf::get_u16).
 __device__ __forceinline__ u32 lds_be16(const uint8_t* base, u32 a) {
-#ifdef TPZ_ABL_BE16U8
-  return ((u32)base[a] << 8) | base[a + 1];   // two ds_read_u8 + v_lshl_or
-#else
   u32 w = lds_u32(base, a);
   return ((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu);
-#endif
 }
 __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 
@@ -148,30 +138,6 @@ __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 // one ds_read_b128 at the byte address (TPZ_ABL_U128; gfx950 replays it: 64 LDS cycles), two
 // aligned ds_read_b128 + a two-bit select (TPZ_ABL_FUNNEL, 16 VALU).
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
-#if defined(TPZ_ABL_U128) || defined(TPZ_ABL_FUNNEL)
-  typedef u32 u32x4 __attribute__((ext_vector_type(4)));
-#endif
-#if defined(TPZ_ABL_U128)
-  typedef u32x4 u32x4_u __attribute__((aligned(1)));
-  const u32x4 v = *reinterpret_cast<const u32x4_u*>(base + x);
-  return make_uint4(v.x, v.y, v.z, v.w);
-#elif defined(TPZ_ABL_FUNNEL)
-  // two aligned ds_read_b128 + a two-bit dword select. The empty asm hides the loads from the
-  // selects: otherwise hipcc turns "select of loaded dwords" into branches around dword reads.
-  const u32x4* p = reinterpret_cast<const u32x4*>(base + (x & ~15));
-  u32x4 va = p[0], vb = p[1];
-  asm volatile("" : "+v"(va), "+v"(vb));
-  const uint4 a = make_uint4(va.x, va.y, va.z, va.w);
-  const uint4 b = make_uint4(vb.x, vb.y, vb.z, vb.w);
-  const u32 sh = (u32)x & 15u, s = sh & 3u, q = sh >> 2;
-  const u32 w0 = q < 2 ? (q == 0 ? a.x : a.y) : (q == 2 ? a.z : a.w);
-  const u32 w1 = q < 2 ? (q == 0 ? a.y : a.z) : (q == 2 ? a.w : b.x);
-  const u32 w2 = q < 2 ? (q == 0 ? a.z : a.w) : (q == 2 ? b.x : b.y);
-  const u32 w3 = q < 2 ? (q == 0 ? a.w : b.x) : (q == 2 ? b.y : b.z);
-  const u32 w4 = q < 2 ? (q == 0 ? b.x : b.y) : (q == 2 ? b.z : b.w);
-  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
-                    __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
-#else  // default: three 8-byte-aligned ds_read_b64 (2 LDS cycles each instead of a 64-cycle
        // unaligned ds_read_b128 replay) + a one-bit dword select + alignbyte
   typedef u32 u32x2 __attribute__((ext_vector_type(2)));
   const u32x2* p = reinterpret_cast<const u32x2*>(base + (x & ~7));
@@ -183,7 +149,6 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
             s4 = h ? c.y : c.x;
   return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, s), __builtin_amdgcn_alignbyte(s2, s1, s),
                     __builtin_amdgcn_alignbyte(s3, s2, s), __builtin_amdgcn_alignbyte(s4, s3, s));
-#endif
 }
 
 // ------------------------------------------------------------------ CRC-32 (table driven)
@@ -305,20 +270,6 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
 // in lanes 0, 16, 32, 48; those are shifted by 1280 / 2560 B and read out.
 __device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
   const u32 lane = lane_id();
-#ifdef TPZ_ABL_FLATCOMB
-  // diagnostic: every lane looks up at every level (no exec branches, more LDS lookups)
-  { const u32 t = crc_shift<0>(tab, A); A = (lane & 1u) ? t : A; }
-  A ^= dpp<kRowShl + 1>(A);
-  { const u32 t = crc_shift<1>(tab, A); A = (lane & 3u) == 2u ? t : A; }
-  A ^= dpp<kRowShl + 2>(A);
-  { const u32 t = crc_shift<2>(tab, A); A = (lane & 7u) == 4u ? t : A; }
-  A ^= dpp<kRowShl + 4>(A);
-  { const u32 t = crc_shift<3>(tab, A); A = (lane & 15u) == 8u ? t : A; }
-  A ^= dpp<kRowShl + 8>(A);
-  { const u32 t = crc_shift<4>(tab, A); A = (lane & 31u) == 16u ? t : A; }
-  { const u32 t = crc_shift<5>(tab, A); A = (lane & 47u) == 32u ? t : A; }
-  return readlane(A, 0) ^ readlane(A, 16) ^ readlane(A, 32) ^ readlane(A, 48);
-#endif
   if ((lane & 1u) == 1u) A = crc_shift<0>(tab, A);
   A ^= dpp<kRowShl + 1>(A);
   if ((lane & 3u) == 2u) A = crc_shift<1>(tab, A);
@@ -581,10 +532,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)0x7FFFFFF0, 0x00020000);
 }
 __device__ __forceinline__ void put_meta(const Out& o, u32 b, u32 st, u32 n, u32 crc) {
-#ifdef TPZ_ABL_NOMETA
-  asm volatile("" ::"v"(st), "v"(n), "v"(crc));   // timing build only: no per-block meta stores
-  return;
-#endif
   const bool l0 = lane_id() == 0;
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)st, whole_rsrc(o.status), l0 ? b : kOob, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32(n, whole_rsrc(o.count), l0 ? 4 * b : kOob, 0, 0);
@@ -1038,10 +985,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
                                              const Out& o, u32 kshift, Stamps& S, PendingCrc& pd) {
   const u32 lane = lane_id();
-#ifdef TPZ_ABL_LOADONLY
-  put_meta(o, b, TPZ_BLOCK_OK, win[a0], 0);
-  return;
-#endif
   // the header reads are issued together (one LDS round trip); the checks keep the reference's
   // order
   const u32 tag = win[(int)(a0 + len) - 1];                                    // compress.rs:99
@@ -1050,9 +993,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   // flat layout: the block's first key / value byte in the columns (tpz_flat_layout)
   const u64 kf = FLAT ? o.kfirst[b] : 0ull, vf = FLAT ? o.vfirst[b] : 0ull;
   const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
-#ifndef TPZ_ABL_NODEFER
   finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
-#endif
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
   if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
@@ -1078,7 +1019,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     else defer_to(o.defer_list, o.defer_count, b);
     return;
   } else {
-#ifndef TPZ_ABL_NOPARSE
     const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
     const u32 dl = P - 2 - 2 * n;
     // (flat: the exact ends, n pairs reserved for every block by tpz_flat_layout)
@@ -1120,19 +1060,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       const bool act = i < n;
       u32 off = 0, kl = 0, vl = 0;
       bool ok = true;
-#ifdef TPZ_ABL_BFPARSE
-      // diagnostic: branch-free reads (an out-of-range read goes to the block start instead)
-      {
-        off = lds_be16(win, act ? a0 + 2 + 2 * i : a0);
-        const bool ok1 = act && off + 2 <= dl;
-        kl = lds_be16(win, ok1 ? db + off : a0);
-        const bool ok2 = ok1 && off + 4 + kl <= dl;
-        vl = lds_be16(win, ok2 ? db + off + 2 + kl : a0);
-        ok = !act || (ok2 && off + 4 + kl + vl <= dl);
-        if (!(act && ok)) kl = vl = 0;
-        if (!act) off = 0;
-      }
-#else
       if (act) {
         off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
         ok = off + 2 <= dl;
@@ -1140,7 +1067,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
         if (!ok) kl = vl = 0;
       }
-#endif
       bad |= __ballot(act && !ok) != 0;
       short_segs |= __ballot((kl != 0 && kl < 16) || (vl != 0 && vl < 16)) != 0;
       const u32 ki = wave_scan_incl(kl) + kc;
@@ -1151,12 +1077,10 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         knz_all = __builtin_popcountll(kmask);
       }
       const u32 vs = stream_vstart<FLAT>(ktot, dk, dv);  // value stream start (tpz_value_start)
-#ifndef TPZ_ABL_NOENDS
       __builtin_amdgcn_raw_buffer_store_b64(
           __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32,
                              act ? make_uint2(ki, vi) : make_uint2(0, 0)),
           whole_rsrc(ends_g), (slots_fit && i < n_pad) ? 8 * i : kOob, 0, 0);
-#endif
       if (act && slots_fit) {
         // entry table + chunk map: the chunk t = ceil(end / 16) is the first one starting at or
         // after the segment's end (ends beyond the map only occur in blocks that spill)
@@ -1195,7 +1119,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       }
       __builtin_amdgcn_wave_barrier();
 #ifndef TPZ_ABL_NOCOPY
-#if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY) && !defined(TPZ_ABL_NOFUSE)
+#if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY)
       if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
         fuse = true;
         f_short = short_segs;
@@ -1216,7 +1140,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 #endif
     }
     TPZ_STAMP(S, 3);
-#endif
   }
   __builtin_amdgcn_wave_barrier();
   u32 crc;
@@ -1243,12 +1166,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
           : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                         fo, win, pb, P + k, kshift, S);
-#ifndef TPZ_ABL_NODEFER
       pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
       return;
-#else
-      R = crc_combine(tab, lc);
-#endif
     } else {
 #ifdef TPZ_CRC_SARW
       if constexpr (!BIG) {
@@ -1329,7 +1248,6 @@ struct Params {
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
   u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
-  u32* wave_ctr;      // (diagnostic XGLOBAL builds) the global chunk counter, a tail counter
 };
 
 // ------------------------------------------------------------------ wave path kernel
@@ -1353,16 +1271,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #endif
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
-#ifdef TPZ_ABL_XGLOBAL
-  __shared__ u32 gchunk[8], gready[8];
-  if (threadIdx.x < 8) gready[threadIdx.x] = 0;
-  if (threadIdx.x == 0) {
-    gchunk[0] = atomicAdd(p.wave_ctr, 1u);
-    gready[0] = 1;
-    gchunk[1] = atomicAdd(p.wave_ctr, 1u);
-    gready[1] = 2;
-  }
-#endif
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1381,9 +1289,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
   const u32 kshift = p.lane_shift[lane];
-#ifdef TPZ_ABL_PRIO
-  if (wid & 1u) __builtin_amdgcn_s_setprio(1);   // diagnostic: static priority for half the waves
-#endif
   uint8_t* slot = lds + kWaveTabBytes + wid * kSlotBytes;
   uint8_t* win = slot + kGuard;
   uint8_t* etab = win + kWinBytes + 32;
@@ -1412,33 +1317,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   const u32 kChunk = 1u << cshift, rshift = kRowShift - cshift;   // chunks per row: 2^rshift
   // (saturated at n_blocks: a chunk past the batch is empty)
   const u32 row0 = blockIdx.x * kWavesPerWG;
-#ifdef TPZ_ABL_XGLOBAL
-  // diagnostic: single blocks from global 64-block chunks (claimed by the workgroups in turn,
-  // each published two chunks ahead), so the balance is across CUs too
-  (void)rshift;
-  (void)row0;
-  auto chunk_first = [&](u32 q) -> u32 { return q < p.n_blocks ? q : p.n_blocks; };
-  auto claim_chunk = [&]() -> u32 {
-    u32 t = 0;
-    if (lane == 0) t = atomicAdd(&chunk_next, 1u);
-    t = uni(t);
-    const u32 k = t >> 6, j = t & 63u;
-    if (j == 32u) {
-      u32 g = 0;
-      if (lane == 0) g = atomicAdd(p.wave_ctr, 1u);
-      g = uni(g);
-      if (lane == 0) {
-        __hip_atomic_store(&gchunk[(k + 2) & 7u], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&gready[(k + 2) & 7u], k + 3, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    for (u32 i = 0; i < (1u << 24); i++)
-      if (uni(__hip_atomic_load(&gready[k & 7u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == k + 1) break;
-    const u32 g = uni(__hip_atomic_load(&gchunk[k & 7u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    const u64 bb = (u64)g * 64 + j;
-    return bb < p.n_blocks ? (u32)bb : p.n_blocks;
-  };
-#else
   auto chunk_first = [&](u32 q) -> u32 {
     const u64 f = (u64)(q >> rshift) * nw + row0 + ((q & ((1u << rshift) - 1u)) << cshift);
     return f < p.n_blocks ? (u32)f : p.n_blocks;
@@ -1448,7 +1326,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     return uni(q);
   };
-#endif
   u64 gs_cur, ge_cur, gs_nxt, ge_nxt;
   auto load_group = [&](u32 q, u64& gs, u64& ge) {
     // lanes past the chunk or the batch re-read an extent (unconditional: the loads write their
@@ -1479,9 +1356,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
   u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
-#ifdef TPZ_ABL_CLAIM2
-  u32 q_nxt2 = claim_chunk();   // diagnostic: the claim one chunk further ahead
-#endif
   load_group(q_cur, gs_cur, ge_cur);
   load_group(q_nxt, gs_nxt, ge_nxt);
   triage_group(q_cur, gs_cur, ge_cur);
@@ -1524,18 +1398,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   issue(b, 0, s_cur, e_cur);
   vm_pad<kVmAfter>(p.out);
 
-#ifdef TPZ_ABL_ROTPRIO   // diagnostic: rotate the wave's issue priority every block
-  u32 rot = blockIdx.x * kWavesPerWG + wid;
-#endif
   while (b < p.n_blocks) {
-#ifdef TPZ_ABL_ROTPRIO
-    switch (uni(rot++) & 3u) {
-      case 0: __builtin_amdgcn_s_setprio(0); break;
-      case 1: __builtin_amdgcn_s_setprio(1); break;
-      case 2: __builtin_amdgcn_s_setprio(2); break;
-      default: __builtin_amdgcn_s_setprio(3); break;
-    }
-#endif
     const u64 s = s_cur, e = e_cur;
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
     const bool fits = (e - s) <= kWaveMaxLen;
@@ -1557,12 +1420,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       q_cur = q_nxt;
       gs_cur = gs_nxt;
       ge_cur = ge_nxt;
-#ifdef TPZ_ABL_CLAIM2
-      q_nxt = q_nxt2;
-      q_nxt2 = claim_chunk();
-#else
       q_nxt = claim_chunk();
-#endif
       load_group(q_nxt, gs_nxt, ge_nxt);
       triage_group(q_cur, gs_cur, ge_cur);
     }
@@ -1723,7 +1581,6 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
     bcnt = 0;
     __syncthreads();
   } else {
-#ifndef TPZ_ABL_NOPARSE
     const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
     const bool slots_fit = 6u * n <= len;
     uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
@@ -1797,9 +1654,6 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
       nk = T.kn + T.vn;
       tot = vs + T.vb;
     }
-#else
-    __syncthreads();
-#endif
   }
   TPZ_STAMP(S, 1);
 #ifdef TPZ_ABL_NOCOPY
@@ -1931,10 +1785,6 @@ __device__ __forceinline__ void big_phase(const Params& p, uint8_t* lds, u32 cnt
     if (more) issue(nxt);
     [&]() {
       const u32 a0 = (u32)(s & 15u);
-#ifdef TPZ_ABL_LOADONLY
-      if (wid == 0) put_meta(p.out, b, TPZ_BLOCK_OK, win[a0], 0);
-      return;
-#endif
       const u32 tag = win[(int)(a0 + len) - 1];                                  // compress.rs:99
       const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));    // block.rs:51
       const u32 n = lds_be16(win, a0);                                           // block.rs:54
@@ -2063,7 +1913,6 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // 2.20 with 4, 2.78 with 1; profiles/r3/wave_chunks.jsonl).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
   p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
-  p.wave_ctr = a.tail + kTailWave;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;

@@ -128,7 +128,6 @@ enum TailCounter : int {
   kTailBigDone,        // big blocks finished
   kTailSpillTicket,    // spill blocks claimed
   kTailExit,           // tail-kernel workgroups finished
-  kTailWave,           // (diagnostic builds) the wave path's global chunk counter
   kTailCounters,
   // Sticky, past the counters the tail kernel zeroes: set when a tail workgroup's wait for the
   // big phase timed out (tpz_decode_check reports it and clears it)
