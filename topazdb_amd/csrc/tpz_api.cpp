@@ -122,8 +122,14 @@ std::vector<uint32_t> build_wave_tables(const std::vector<uint32_t>& dec) {
   std::vector<uint32_t> out((size_t)tpz::kWaveTableWords);
   for (int b = 0; b < 256; b++)
     for (int r = 0; r < 32; r++) out[(size_t)b * 32 + r] = dec[(size_t)b];
-  std::memcpy(&out[8192], &dec[16 * 256], (size_t)(tpz::kNumCrcTables - 16) * 256 * 4);
-  const size_t sh = 8192 + (size_t)(tpz::kNumCrcTables - 16) * 256;
+  for (int l = 0; l < 64; l++) {     // the combine matrix: columns of Z_{80 l}
+    const uint32_t z = x8n((uint64_t)tpz::kCrcLaneBytes * (uint64_t)l);
+    for (int j = 0; j < 32; j++)
+      out[tpz::kWaveRepWords + ((size_t)(j >> 2) * 64 + l) * 4 + (j & 3)] = multmodp(z, 1u << j);
+  }
+  const size_t ids = tpz::kWaveRepWords + tpz::kWaveMatWords;
+  std::memcpy(&out[ids], &dec[16 * 256], (size_t)(tpz::kNumCrcTables - 16) * 256 * 4);
+  const size_t sh = ids + (size_t)(tpz::kNumCrcTables - 16) * 256;
   for (int i = 0; i < 4; i++) {
     const uint32_t z = x8n((uint64_t)(tpz::kCrcChainBytes - 1 - i));
     for (int b = 0; b < 256; b++) out[sh + (size_t)i * 256 + b] = dec[b] ? multmodp(z, dec[b]) : 0u;

@@ -39,6 +39,9 @@
 #if defined(TPZ_ABL_SARW) && !defined(TPZ_CRC_SARW)
 #define TPZ_CRC_SARW   // variant builds: make variants (libtpz_gpu_sarw.so, onchip_sarw, ...)
 #endif
+#if defined(TPZ_ABL_MCOMB) && !defined(TPZ_CRC_MCOMB)
+#define TPZ_CRC_MCOMB
+#endif
 // the tail kernel's spill phase (namespace tpz::sp), compiled into this unit
 #include "tpz_spill.hip"
 
@@ -64,16 +67,33 @@ constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B 
 constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads, the 5th partial
 constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
-#ifdef TPZ_CRC_SARW
-// byte-serial CRC over a 32-fold replicated T_0 (bank-conflict-free lookups): the table image
-// takes 61 KiB, so the entry table holds 2n + 1 <= 255 segments
+// The wave path's CRC tables in LDS, words (tab = the pointer the CRC helpers take; ids as in
+// tpz_internal.h; the image parts come from tpz_api.cpp build_wave_tables):
+//   default       [ids 0..40]                                     tab = base
+//   MCOMB         [ids 0..15][id 40 (inv)][matrix 2048]           tab = base
+//   SARW          [T_0 x 32][ids 16..44]                          tab = base + 8192 - 16 * 256
+//   SARW + MCOMB  [T_0 x 32][matrix 2048][ids 40..44]             tab = base + 10240 - 40 * 256
+#if defined(TPZ_CRC_SARW) && defined(TPZ_CRC_MCOMB)
+constexpr int kWaveTabWords = kWaveRepWords + kWaveMatWords + 5 * 256;
+constexpr int kTabOff = kWaveRepWords + kWaveMatWords - 40 * 256;
+#elif defined(TPZ_CRC_SARW)
+constexpr int kWaveTabWords = kWaveRepWords + kWaveIdsWords;
+constexpr int kTabOff = kWaveRepWords - 16 * 256;
+#elif defined(TPZ_CRC_MCOMB)
+constexpr int kWaveTabWords = 17 * 256 + kWaveMatWords;
+constexpr int kTabOff = 0;
+#else
+constexpr int kWaveTabWords = kNumCrcTables * 256;
+constexpr int kTabOff = 0;
+#endif
+constexpr int kWaveTabBytes = kWaveTabWords * 4;
+#if defined(TPZ_CRC_SARW) && !defined(TPZ_CRC_MCOMB)
+// the SARW image takes 61 KiB: the entry table holds 2n + 1 <= 255 segments
 constexpr u32 kWaveMaxN = 127;
 constexpr int kWaveTabSlots = 256;
-constexpr int kWaveTabBytes = kWaveTableWords * 4;
 #else
 constexpr u32 kWaveMaxN = 255;                      // the table holds 2n + 1 <= 511 entries
 constexpr int kWaveTabSlots = 512;
-constexpr int kWaveTabBytes = kTableBytes;
 #endif
 constexpr int kWaveMapLen = 288;                    // >= (kWaveMaxLen + 2) / 16 + 3 map slots
 constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveTabSlots * 4 + 2 * kWaveMapLen;
@@ -319,7 +339,8 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
 // lane l reads replica l mod 32, so a lookup with any byte per lane hits 32 distinct banks
 // (ds_read_b32 serves lanes 0-31 and 32-63 in one LDS cycle each) instead of the slice tables'
 // ~3x replays. tab (ids >= 16, as everywhere) sits right after the replicas.
-__device__ __forceinline__ const u32* crc_rep(const u32* tab) { return tab + 16 * 256 - 8192; }
+__device__ __forceinline__ const u32* crc_rep(const u32* tab) { return tab - kTabOff; }
+__device__ __forceinline__ const u32* crc_inv(const u32* tab) { return tab + kCrcInvTable * 256; }
 // c = T_0[(c ^ b) & 0xFF] ^ (c >> 8) for the four bytes of w
 __device__ __forceinline__ u32 sarw4(const u32* rep, u32 lr, u32 c, u32 w) {
   c ^= w;
@@ -338,7 +359,7 @@ __device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k)
   const u32* rep = crc_rep(tab);
   const u32 lr = lane_id() & 31u;
   for (u32 i = 0; i < k; i++) {
-    const u32 b = tlook(tab, kCrcInvTable, r >> 24);
+    const u32 b = crc_inv(tab)[r >> 24];
     r = ((r ^ rep[(b << 5) | lr]) << 8) | b;
   }
   return r;
@@ -353,8 +374,46 @@ __device__ __forceinline__ u32 crc_shift_small_w(const u32* tab, u32 a, u32 k) {
   return crc_shift_small(tab, a, k);
 }
 __device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k) {
+#ifdef TPZ_CRC_MCOMB
+  for (u32 i = 0; i < k; i++) {            // the inverse table sits at id 16 in this layout
+    const u32 b = tlook(tab, 16, r >> 24);
+    r = ((r ^ tlook(tab, 0, b)) << 8) | b;
+  }
+  return r;
+#else
   return crc_unshift_small(tab, r, k);
+#endif
 }
+#endif
+
+// The wave path's combine of the lanes' run values (lane l's run ends 80 l bytes before the
+// range end) into R0 of the range.
+#ifdef TPZ_CRC_MCOMB
+// One short chain instead of the tree's six dependent LDS round trips: lane l applies
+// Z_{80 l} (a GF(2) matrix, its columns from LDS in 8 ds_read_b128) to its value, XORing the
+// column of every set bit, and the wave XORs the results.
+__device__ __forceinline__ const u32* crc_mat(const u32* tab) {
+#ifdef TPZ_CRC_SARW
+  return tab - kTabOff + kWaveRepWords;
+#else
+  return tab + 17 * 256;
+#endif
+}
+__device__ __forceinline__ u32 crc_combine_w(const u32* tab, u32 A) {
+  const uint4* M = reinterpret_cast<const uint4*>(crc_mat(tab)) + lane_id();
+  u32 R = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 c = M[64 * q];
+    R ^= c.x & (u32)((int)(A << (31 - 4 * q)) >> 31);
+    R ^= c.y & (u32)((int)(A << (30 - 4 * q)) >> 31);
+    R ^= c.z & (u32)((int)(A << (29 - 4 * q)) >> 31);
+    R ^= c.w & (u32)((int)(A << (28 - 4 * q)) >> 31);
+  }
+  return wave_xor(R);
+}
+#else
+__device__ __forceinline__ u32 crc_combine_w(const u32* tab, u32 A) { return crc_combine(tab, A); }
 #endif
 
 // ------------------------------------------------------------------ entry tables
@@ -944,18 +1003,21 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   return crc_lane_value(tab, L);   // the lane's raw run CRC: crc_combine gives R0 of the range
 }
 
-#ifdef TPZ_CRC_SARW
-// wave_crc for a wave-path block (Pa <= 5120) with the byte chains of crc_step.
+#if defined(TPZ_CRC_SARW) || defined(TPZ_CRC_MCOMB)
+// wave_crc for a wave-path block (Pa <= 5120): its steps and combine (crc_step, crc_combine_w).
 __device__ __forceinline__ u32 wave_crc_w(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
   const u32 lane = lane_id();
   CrcLane L;
   L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
   L.act = L.seg + kCrcLaneBytes > 0;
-  L.c = L.c2 = 0;
+  L.c = 0;
+#ifdef TPZ_CRC_SARW
+  L.c2 = 0;
   L.lr = lane & 31u;
+#endif
 #pragma unroll
   for (int t = 0; t < kCrcLaneBytes / 16; t++) crc_step(tab, win, pb, L, t);
-  return crc_combine(tab, crc_lane_value(tab, L));
+  return crc_combine_w(tab, crc_lane_value(tab, L));
 }
 #endif
 
@@ -970,7 +1032,7 @@ struct PendingCrc {
 
 __device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
   if (!pd.live) return;
-  const u32 R = crc_combine(tab, pd.lc);
+  const u32 R = crc_combine_w(tab, pd.lc);
   const u32 crc = (R == crc_shift_small_w(tab, ~pd.stored, pd.k)) ? pd.stored
                                                                    : ~crc_unshift_small_w(tab, R, pd.k);
   const bool ok = crc == pd.stored;                                            // checksum.rs:17
@@ -1169,7 +1231,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
       return;
     } else {
-#ifdef TPZ_CRC_SARW
+#if defined(TPZ_CRC_SARW) || defined(TPZ_CRC_MCOMB)
       if constexpr (!BIG) {
         R = wave_crc_w(tab, win, pb, P + k);
       } else
@@ -1263,28 +1325,37 @@ __device__ unsigned long long g_wave_ends[3 * 8192];
 template <bool FLAT>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
-#ifdef TPZ_CRC_SARW
-  // [T_0 x 32 replicas][ids 16..44]: tab[id * 256 + b] reaches ids >= 16 (crc_rep gives T_0)
-  u32* tab = reinterpret_cast<u32*>(lds) + 8192 - 16 * 256;
-#else
-  u32* tab = reinterpret_cast<u32*>(lds);
-#endif
+  u32* tab = reinterpret_cast<u32*>(lds) + kTabOff;   // (the layouts: kWaveTabWords)
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifdef TPZ_CRC_SARW
   {
-    const uint4* s = reinterpret_cast<const uint4*>(p.wave_tables);
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    for (int i = threadIdx.x; i < kWaveTabBytes / 16; i += blockDim.x) d[i] = s[i];
+    // the build's table layout from the decode tables (ids) and the wave image (kWaveTableWords)
+    u32* base = reinterpret_cast<u32*>(lds);
+    auto put = [&](const u32* src, int dst_word, int words) {
+      const uint4* s = reinterpret_cast<const uint4*>(src);
+      uint4* d = reinterpret_cast<uint4*>(base + dst_word);
+      for (int i = threadIdx.x; i < words / 4; i += blockDim.x) d[i] = s[i];
+    };
+    const int ids = kWaveRepWords + kWaveMatWords;     // id 16 in the image
+#if defined(TPZ_CRC_SARW) && defined(TPZ_CRC_MCOMB)
+    put(p.wave_tables, 0, kWaveRepWords + kWaveMatWords);
+    put(p.wave_tables + ids + (40 - 16) * 256, kWaveRepWords + kWaveMatWords, 5 * 256);
+#elif defined(TPZ_CRC_SARW)
+    put(p.wave_tables, 0, kWaveRepWords);
+    put(p.wave_tables + ids, kWaveRepWords, kWaveIdsWords);
+#elif defined(TPZ_CRC_MCOMB)
+    put(p.crc_tables, 0, 16 * 256);
+    put(p.crc_tables + kCrcInvTable * 256, 16 * 256, 256);
+    put(p.wave_tables + kWaveRepWords, 17 * 256, kWaveMatWords);
+#else
+    put(p.crc_tables, 0, kNumCrcTables * 256);
+#endif
     __syncthreads();
   }
-#else
-  load_tables(tab, p.crc_tables);
-#endif
 
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
