@@ -160,6 +160,9 @@ extern "C" {
                            stream: *mut c_void) -> TpzErr;
     pub fn tpz_pack_ends(ctx: *mut TpzCtx, batch: *const TpzBatch, cols: *const TpzColumns,
                          d_first: *const u64, d_dense: *mut u32, stream: *mut c_void) -> TpzErr;
+    pub fn tpz_layout_compress_bound(src_bytes: u64, n_blocks: u64) -> u64;
+    pub fn tpz_compress_blocks(ctx: *mut TpzCtx, batch: *const TpzBatch, codec: u32, d_dst: *mut u8,
+                               d_dst_ext: *mut u64, stream: *mut c_void) -> TpzErr;
     pub fn tpz_flat_layout(ctx: *mut TpzCtx, batch: *const TpzBatch, d_first: *mut u64,
                            stream: *mut c_void) -> TpzErr;
     pub fn tpz_decode_blocks_flat(ctx: *mut TpzCtx, batch: *const TpzBatch,

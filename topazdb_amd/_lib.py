@@ -136,6 +136,11 @@ def lib() -> C.CDLL:
         L.tpz_pack_ends.restype = C.c_int
         L.tpz_entry_first.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
         L.tpz_entry_first.restype = C.c_int
+        L.tpz_compress_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_uint32, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]
+        L.tpz_compress_blocks.restype = C.c_int
+        L.tpz_layout_compress_bound.argtypes = [C.c_uint64, C.c_uint64]
+        L.tpz_layout_compress_bound.restype = C.c_uint64
         L.tpz_flat_layout.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
         L.tpz_flat_layout.restype = C.c_int
         L.tpz_decode_blocks_flat.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(FlatColumns),

@@ -158,6 +158,8 @@ struct tpz_workspace {
   size_t plan1_cap = 0;
   void* d_bloom = nullptr;      // tpz_bloom_build: probe buckets + slice histograms
   size_t bloom_cap = 0;
+  void* d_comp = nullptr;       // tpz_compress_blocks: the per-block scratch slots + scan parts
+  size_t comp_cap = 0;
   uint32_t* h_info = nullptr;   // pinned: tpz_plan_blocks' read-back of its 16-byte info
 };
 
@@ -184,6 +186,7 @@ void free_workspace(tpz_workspace& w) {
   if (w.d_plan0) (void)hipFree(w.d_plan0);
   if (w.d_plan1) (void)hipFree(w.d_plan1);
   if (w.d_bloom) (void)hipFree(w.d_bloom);
+  if (w.d_comp) (void)hipFree(w.d_comp);
   if (w.h_info) (void)hipHostFree(w.h_info);
   w = tpz_workspace{};
 }
@@ -580,6 +583,32 @@ tpz_err tpz_decode_blocks_flat(tpz_ctx* c, const tpz_batch* b, const tpz_flat_co
   a.kfirst = o->d_first + st;
   a.vfirst = o->d_first + 2 * st;
   tpz::launch_decode(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
+}
+
+uint64_t tpz_layout_compress_bound(uint64_t src_bytes, uint64_t n_blocks) {
+  return src_bytes + src_bytes / 6 + 40 * n_blocks + 64;
+}
+
+tpz_err tpz_compress_blocks(tpz_ctx* c, const tpz_batch* b, uint32_t codec, uint8_t* d_dst,
+                            uint64_t* d_dst_ext, void* stream) {
+  if (!c || !b || !d_dst_ext || codec != 2) return TPZ_ERR_INVALID_ARG;
+  if (b->n_blocks && (!b->d_src || !b->d_ext || !d_dst)) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  const uint64_t scratch = tpz::compress_scratch_bytes(b->src_bytes, b->n_blocks);
+  const uint64_t parts = (uint64_t)tpz::flat_scan_parts_words(b->n_blocks);
+  tpz_workspace* w = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    w = &c->ws[stream];
+    tpz_err r = grow(stream, &w->d_comp, &w->comp_cap, ((scratch + 15) & ~15ull) + 8 * parts);
+    if (r != TPZ_SUCCESS) return r;
+  }
+  uint8_t* sc = static_cast<uint8_t*>(w->d_comp);
+  tpz::launch_compress(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, sc, d_dst_ext,
+                       reinterpret_cast<uint64_t*>(sc + ((scratch + 15) & ~15ull)), d_dst,
+                       c->num_cus, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
 }

@@ -222,6 +222,17 @@ uint64_t flat_scan_parts_words(uint32_t n_blocks) {
   return 3 * ((uint64_t)(n_blocks + kScWg - 1) / kScWg + 1);
 }
 
+void launch_scan_u64(u64* a, u32 n, u64* part, hipStream_t stream) {
+  if (n == 0) {
+    (void)hipMemsetAsync(a, 0, 8, stream);
+    return;
+  }
+  const u32 np = (n + kScWg - 1) / kScWg;
+  hipLaunchKernelGGL(flat_scan_parts, dim3(np, 1), dim3(256), 0, stream, a, n, part, np);
+  hipLaunchKernelGGL(flat_scan_totals, dim3(1), dim3(1024), 0, stream, part, np);
+  hipLaunchKernelGGL(flat_scan_write, dim3(np, 1), dim3(256), 0, stream, a, n, part, np);
+}
+
 void launch_flat_layout(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n_blocks,
                         u64* first, u64* part, u32 num_cus, hipStream_t stream) {
   if (n_blocks == 0) {

@@ -297,6 +297,15 @@ uint64_t entry_first_parts(uint32_t n_blocks);
 // tpz_flat_layout (tpz_flat.hip): first = 3 x (n_blocks + 1) u64 (entries, key bytes, value
 // bytes: exclusive prefixes, totals at [n_blocks]); `part` = flat_scan_parts_words(n_blocks) u64.
 uint64_t flat_scan_parts_words(uint32_t n_blocks);
+// In place: a[i] = sum of a[j < i], a[n] = the total (n + 1 u64; part = flat_scan_parts_words(n)
+// / 3 u64 suffices).
+void launch_scan_u64(uint64_t* a, uint32_t n, uint64_t* part, hipStream_t stream);
+// tpz_compress_blocks (tpz_compress.hip): scratch bytes for the per-block slots; the snappy
+// encode, the scan of the sizes into dst_ext and the packing into dst.
+uint64_t compress_scratch_bytes(uint64_t src_bytes, uint32_t n_blocks);
+void launch_compress(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes, uint32_t n_blocks,
+                     uint8_t* scratch, uint64_t* dst_ext, uint64_t* part, uint8_t* dst,
+                     uint32_t num_cus, hipStream_t stream);
 void launch_flat_layout(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
                         uint32_t n_blocks, uint64_t* first, uint64_t* part, uint32_t num_cus,
                         hipStream_t stream);

@@ -130,6 +130,30 @@ def encode_blocks_async(ctx: Context, ent: DeviceEntries, first: torch.Tensor, e
     return out
 
 
+def compress_bound(src_bytes: int, n_blocks: int) -> int:
+    """tpz_layout_compress_bound: bytes that hold any batch's snappy-encoded blocks."""
+    return int(_lib.lib().tpz_layout_compress_bound(src_bytes, n_blocks))
+
+
+def compress_blocks(ctx: Context, src: torch.Tensor, ext: torch.Tensor, n_blocks: int,
+                    src_bytes: int, codec: int = 2, out: torch.Tensor | None = None,
+                    stream: torch.cuda.Stream | None = None):
+    """tpz_compress_blocks: compress::encode with CompressOptions::Snappy (compress.rs:66-71)
+    for every Uncompress block of a device batch (the write side's output, compaction with the
+    default codec, src/opt.rs:48). Returns (out, out_ext): the encoded blocks back to back and
+    their n_blocks + 1 extents (int64, device)."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    if out is None:
+        out = torch.empty(max(compress_bound(src_bytes, n_blocks), 16), dtype=torch.uint8, device=dev)
+    out_ext = torch.empty(n_blocks + 1, dtype=torch.int64, device=dev)
+    b = _lib.Batch(src.data_ptr(), ext.data_ptr(), n_blocks, src_bytes)
+    _lib.check(_lib.lib().tpz_compress_blocks(ctx.handle, C.byref(b), codec, C.c_void_p(out.data_ptr()),
+                                              C.c_void_p(out_ext.data_ptr()), C.c_void_p(s.cuda_stream)),
+               "tpz_compress_blocks")
+    return out, out_ext
+
+
 def build_region(ctx: Context, keys, kpos, vals, vpos, block_size: int):
     """The whole write side for host entries: (data-region bytes, block extents, first entry of
     every block), as numpy arrays (the device counterpart of synth.build_blocks)."""
