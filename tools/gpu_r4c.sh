@@ -4,6 +4,6 @@
 set -o pipefail
 OUT=gpurun_out/r4c
 mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 900 python3 -u -m pytest tests/test_gpu_flat.py tests/test_gpu_compress.py tests/test_gpu_decode.py tests/test_gpu_exact.py tests/test_gpu_spill.py tests/test_gpu_bad_entry.py -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
 VARIANTS="${VARIANTS:-full head sarw mcomb sarw_mcomb nocf lutvalu nocrc stamps onchip onchip_sarw onchip_mcomb onchip_sarw_mcomb onchip_nocf onchip_lutvalu onchip_nocrc}" PMCV="full sarw mcomb sarw_mcomb onchip" bash tools/gpu_r4b.sh
