@@ -73,9 +73,6 @@ struct Stamps {
 #define STAMPS_PASS
 #endif
 
-#ifdef TPZ_CODEC_SALU
-#define CODEC_HDR(x) uni(x)      // diagnostic: snappy element headers on the scalar unit
-#else
 // an opaque VGPR copy: the compiler cannot prove the value wave-uniform, so the header decode and
 // the positions derived from it stay on the VALU (branches on them become exec-masked regions
 // that skip when empty)
@@ -85,7 +82,6 @@ __device__ __forceinline__ u32 vgpr_opaque(u32 x) {
   return y;
 }
 #define CODEC_HDR(x) vgpr_opaque(x)
-#endif
 
 __device__ __forceinline__ u32 lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -137,7 +133,7 @@ struct CodecParams {
   uint8_t* status;
   u32* defer_list;
   u32* defer_count;
-  u32 group_pass;    // snappy_group_kernel ran first (status 0xFF = left for the wave kernel)
+  u32 group_pass;    // the lane kernels ran first (status 0xFF = left for the wave kernel)
 };
 
 // ------------------------------------------------------------------ per-block work
@@ -574,12 +570,8 @@ struct Lz4GlobalOut {            // wave-wide copies into global memory
 __device__ __forceinline__ int64_t lz4_block_length(const uint8_t* src, u64 src_bytes, u64 s, u64 len) {
   const int64_t size = lz4_prefix(src + s, len - 1);
   if (size < 0) return -1;
-#ifdef TPZ_CODEC_SIZES_BYTES
-  return lz4_walk(Lz4GlobalSrc{src + s + 4}, (int64_t)len - 5, Lz4NoOut{}, size);
-#else
   return lz4_walk(Lz4WideSrc{src, src_bytes, s + 4, (s + 4 - (1ull << 62)) & ~15ull, 0, 0, 0, 0},
                   (int64_t)len - 5, Lz4NoOut{}, size);
-#endif
 }
 
 __device__ __forceinline__ int64_t lz4_block_length_bytes(const uint8_t* blk, u64 len) {
@@ -801,151 +793,6 @@ __global__ __launch_bounds__(kWave * kSmallWaves) void codec_wave_kernel(CodecPa
 #endif
 }
 
-// ------------------------------------------------------------------ snappy, G blocks per wave
-// The one-block-per-wave element loop is bound by instruction issue (its wave-uniform work runs
-// once per element per block). Here a wave decodes G snappy blocks at once, one per group of
-// W = 64 / G lanes: every group walks its own element chain with per-lane (group-uniform)
-// state, so each header decode, check and copy instruction serves G blocks; the groups diverge
-// only in which copy path a round takes and for how many iterations. Blocks it does not take
-// (other tags, blocks past the windows, an invalid or mismatching preamble) get status 0xFF and
-// are left to codec_wave_kernel, which runs next and skips every other block.
-#ifndef TPZ_CODEC_G
-#define TPZ_CODEC_G 2
-#endif
-constexpr int kGroupBlocks = TPZ_CODEC_G;
-constexpr int kGroupWaves = 16 / TPZ_CODEC_G;
-constexpr u32 kGroupSlot = kGuard + kSmallIn + kSmallOut;
-static_assert(kGroupWaves * kGroupBlocks * kGroupSlot <= 163840, "group LDS");
-
-template <int G>
-__global__ __launch_bounds__(kWave * kGroupWaves) void snappy_group_kernel(CodecParams p) {
-  constexpr u32 W = kWave / G;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kGroupWaves * G * kGroupSlot];
-  const u32 lane = lane_id();
-  const u32 gi = lane / W, sl = lane % W;
-  const u32 wid = uni(threadIdx.x >> 6);
-  uint8_t* in_win = lds + (wid * G + gi) * kGroupSlot + kGuard;
-  uint8_t* out_win = in_win + kSmallIn;
-  const u32 nw = gridDim.x * kGroupWaves, gw = blockIdx.x * kGroupWaves + wid;
-  for (u32 r = 0;; r++) {
-    const u64 b64 = ((u64)r * nw + gw) * G + gi;
-    if (uni((u32)(((u64)r * nw + gw) * G >= p.n_blocks))) break;  // no group has a block
-    const bool valid = b64 < p.n_blocks;
-    const u32 b = valid ? (u32)b64 : 0u;
-    u64 s = 0, e = 0, D0 = 0, D1 = 0;
-    u32 tag = 0;
-    if (valid) {
-      s = p.ext[b];
-      e = p.ext[b + 1];
-      D0 = p.dst_ext[b];
-      D1 = p.dst_ext[b + 1];
-      tag = e > s ? p.src[e - 1] : 0u;
-    }
-    const u64 len = e - s, dn = D1 - D0;
-    bool mine = valid && len > 1 && tag == 2 && len - 1 + kInSlack <= kSmallIn &&
-                dn + 16 <= kSmallOut && dn >= 2;
-    const u32 n = (u32)(len - 1);
-    // stage the compressed bytes at in_win[(s & 15) ..] (16-byte pieces; the piece that
-    // straddles the end of the source buffer is read byte by byte)
-    if (mine) {
-      const u64 ws = s & ~15ull;
-      const u32 nb = (u32)(s + n - ws);
-      for (u32 off = 16 * sl; off < nb; off += 16 * W) {
-        uint4 v;
-        if (ws + off + 16 <= p.src_bytes) {
-          v = *reinterpret_cast<const uint4*>(p.src + ws + off);
-        } else {
-          uint8_t t[16];
-          for (int i = 0; i < 16; i++) t[i] = ws + off + i < p.src_bytes ? p.src[ws + off + i] : 0;
-          v = *reinterpret_cast<const uint4*>(t);
-        }
-        *reinterpret_cast<uint4*>(in_win + off) = v;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint8_t* in = in_win + (u32)(s & 15);
-    const u32 a_out = (u32)(reinterpret_cast<uintptr_t>(p.dst + D0) & 15);
-    uint8_t* out = out_win + a_out;
-    // the varint preamble (at most 10 bytes); a mismatch with the sizes pass leaves the block
-    u32 ip = 0, want = 0;
-    if (mine) {
-      u64 v = 0;
-      u32 h = 0;
-      for (u32 i = 0; i < 10 && i < n; i++) {
-        const u32 c = in[i];
-        v |= (u64)(c & 0x7F) << (7 * i);
-        if (!(c & 0x80)) {
-          if (v <= 0xFFFFFFFFull) h = i + 1;
-          break;
-        }
-      }
-      mine = h != 0 && v + 1 == dn;
-      ip = h;
-      want = (u32)v;
-    }
-    if (valid && !mine && sl == 0) p.status[b] = kLeftForWaveKernel;
-    // the element loop: one element per group per round
-    bool ok = mine, run = mine && ip < n;
-    u32 d = 0;
-    while (__ballot(run)) {
-      if (run) {
-        const u32 w0 = lds_u32_lane(in + ip), w1 = lds_u32_lane(in + ip + 4);
-        const u32 tg = w0 & 0xFF, kind = tg & 3, t6 = tg >> 2;
-        const u32 x = (w0 >> 8) | (w1 << 24);
-        const u32 nb = t6 >= 60 ? t6 - 59 : 0u;
-        u32 lx = nb == 0 ? t6 : (nb == 4 ? x : x & ((1u << (8 * nb)) - 1));
-        lx = lx < 0x7FFFFFFFu ? lx : 0x7FFFFFFFu;
-        const u32 ln = kind == 0 ? lx + 1 : (kind == 1 ? 4 + (t6 & 7) : t6 + 1);
-        const u32 hl = kind == 0 ? 1 + nb : (0x5320u >> (4 * kind)) & 15;
-        const u32 off = kind == 1 ? ((tg >> 5) << 8) | (x & 0xFF) : (kind == 2 ? x & 0xFFFF : x);
-        const u32 next = ip + hl + (kind == 0 ? ln : 0u);
-        if (d + ln > want || next > n || (kind != 0 && off - 1 >= d)) {
-          ok = false;                                   // snap's Err
-        } else if (kind == 0) {
-          // literal: head bytes to the next 4-byte boundary, then whole aligned dwords (the last
-          // may write up to 3 bytes past the literal, which later elements overwrite)
-          const u32 pad0 = (0u - (u32)reinterpret_cast<uintptr_t>(out + d)) & 3u;
-          const u32 pad = pad0 < ln ? pad0 : ln;
-          if (sl < pad) out[d + sl] = in[ip + hl + sl];
-          const u32 nd = (ln - pad + 3) >> 2;
-          u32* o = reinterpret_cast<u32*>(out + d + pad);
-          const uint8_t* i8 = in + ip + hl + pad;
-          for (u32 t = sl; t < nd; t += W) o[t] = lds_u32_lane(i8 + 4 * t);
-        } else {
-          // copy (<= 64 bytes): period `off` when it overlaps
-          for (u32 k = sl; k < ln; k += W) {
-            const u32 q = (u32)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-            out[d + k] = out[d - off + (off >= ln ? k : k - q * off)];
-          }
-        }
-        ip = next;
-        d += ln;
-        run = ok && ip < n;
-      }
-    }
-    ok = ok && d == want;
-    __builtin_amdgcn_wave_barrier();
-    if (mine) {
-      uint8_t* dst = p.dst + D0;
-      if (ok) {
-        if (sl == 0) out[want] = 1;                     // re-tagged Uncompress
-        __builtin_amdgcn_wave_barrier();
-        // store [0, dn): head bytes to the 16-byte boundary, whole pieces, tail bytes
-        const u32 head = (16 - a_out) & 15, h = head < dn ? head : (u32)dn;
-        const u32 body = ((u32)dn - h) & ~15u;
-        for (u32 k = sl; k < h; k += W) dst[k] = out_win[a_out + k];
-        for (u32 k = 16 * sl; k < body; k += 16 * W)
-          *reinterpret_cast<uint4*>(dst + h + k) = *reinterpret_cast<const uint4*>(out_win + a_out + h + k);
-        for (u32 k = h + body + sl; k < dn; k += W) dst[k] = out_win[a_out + k];
-        if (sl == 0) p.status[b] = TPZ_BLOCK_OK;
-      } else if (sl == 0) {
-        dst[dn - 1] = 0;                                // decodes as BAD_TAG
-        p.status[b] = TPZ_BLOCK_CODEC_ERROR;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
 
 // ------------------------------------------------------------------ snappy, one block per lane
 // The wave-per-block element loop runs its ~70 wave-uniform instructions once per element per
@@ -1142,20 +989,14 @@ __global__ __launch_bounds__(256) void codec_lane_kernel(CodecParams p) {
 
 __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u32& elems) {
   if (b >= p.n_blocks) return;
-#ifndef TPZ_CODEC_LANE_SNAPPY
   if (p.status[b] != kLeftForWaveKernel) return;              // decoded by a ring kernel
-#endif
   const u64 s = p.ext[b], e = p.ext[b + 1], len = e - s;
   const u64 D0 = p.dst_ext[b], dn = p.dst_ext[b + 1] - D0;
   const u32 tag = len ? p.src[e - 1] : 0u;
   const u64 dst_bytes = p.dst_ext[p.n_blocks];
   // (tiny batches, errors, empty outputs and other tags: the wave kernel)
-#ifdef TPZ_CODEC_LANE_SNAPPY
-  bool ok = len > 1 && (tag == 2 || tag == 3) && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16;
-#else
   bool ok = len > 1 && tag == 3 && dn >= 2 && p.src_bytes >= 16 && dst_bytes >= 16;
   if (!ok) return;                                            // status stays 0xFF
-#endif
   if (ok && tag == 2) {
     u64 want = 0;
     const u32 h = snappy_header(p.src + s, len - 1, want);
@@ -1194,16 +1035,8 @@ __device__ __forceinline__ void codec_lane_block(const CodecParams& p, u32 b, u3
 // L1 holds no stale copy. A step issues one set of four 16-byte loads for every lane: a literal's
 // source bytes or a far copy's stored lines (one set instead of one per descriptor: 1.351 ->
 // 1.314 ms per 2^18 4kc blocks).
-#ifdef TPZ_CODEC_WG64
-constexpr u32 kRingWG = 64;
-#else
 constexpr u32 kRingWG = 256;                                 // blocks (threads) per workgroup
-#endif
-#ifdef TPZ_CODEC_RING256
-constexpr u32 kRing = 256;                                   // 2 workgroups (8 waves) per CU
-#else
 constexpr u32 kRing = 128;                                   // 4 workgroups (16 waves) per CU
-#endif
 constexpr u32 kRingLine = 64, kRingStep = 64;
 // 16-byte pieces a step can take. A literal's steps are 64 bytes, but its final step may take up
 // to 16 kPieces bytes as long as it ends by Pl + 128 (every line it completes is then still
@@ -1248,37 +1081,21 @@ __device__ __forceinline__ u128 ring_read(const uint8_t* R, u32 a) {
 // 16)) into the ring's aligned slots. acc holds the slot containing P (its bytes below P are the
 // output); on return it holds the slot containing P + c.
 __device__ __forceinline__ void ring_emit(uint8_t* R, u32 P, u32 c, const u128 (&v)[kPieces], u128& acc) {
-#ifdef TPZ_CODEC_CHEAPEMIT
-  {                                          // timing build only: no funnel (wrong bytes)
-    const u32 A = P & ~15u, K = (c + 15) >> 4;
-#pragma unroll
-    for (int k = 0; k < (int)kPieces; k++)
-      if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), v[k]);
-    acc = v[0];
-    return;
-  }
-#endif
   const u32 m = P & 15, K = (m + c + 15) >> 4, Kn = (m + c) >> 4;
   const u32 A = P & ~15u;
-#ifndef TPZ_CODEC_SLOT16
   // the new frontier's slot keeps its upper half when the frontier is in its lower half: the
   // ring then holds [roundup8(P) - kRing, P) intact (a copy 120 bytes back always from LDS)
   const bool half = ((P + c) & 15u) != 0 && ((P + c) & 15u) <= 8;
-#endif
   u128 carry = m ? lowbytes(acc, m) : (u128)0, nacc = acc;
 #pragma unroll
   for (int k = 0; k <= (int)kPieces; k++) {
     const u128 cur = k < (int)kPieces ? v[k < (int)kPieces ? k : 0] : (u128)0;
     const u128 slot = m ? carry | (cur << (8 * m)) : cur;
-#ifndef TPZ_CODEC_SLOT16
     if ((u32)k < K) {
       uint8_t* q = R + ((A + 16 * k) & (kRing - 1));
       if ((u32)k == Kn && half) *reinterpret_cast<u64*>(q) = (u64)slot;
       else lds16w(q, slot);
     }
-#else
-    if ((u32)k < K) lds16w(R + ((A + 16 * k) & (kRing - 1)), slot);
-#endif
     if ((u32)k == Kn) nacc = slot;
     carry = m ? cur >> (8 * (16 - m)) : (u128)0;
   }
@@ -1299,10 +1116,8 @@ __device__ __forceinline__ void ring_store_exact(const uint8_t* R, uint8_t* dst,
 template <int kCodec>
 __device__ __forceinline__ void ring_body(CodecParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t rings[kRingWG * kRing];
-#ifndef TPZ_CODEC_PERMUTE
   __shared__ u32 fl_addr[kRingWG / kWave][kWave];
   __shared__ u32 fl_lane[kRingWG / kWave][kWave];
-#endif
   const u32 lane = lane_id(), wid = threadIdx.x >> 6;
   uint8_t* R = rings + threadIdx.x * kRing;
   const u32 b = blockIdx.x * kRingWG + threadIdx.x;
@@ -1378,11 +1193,7 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
   // per 2^18 4kc blocks (profiles/r3/wave_chunks.jsonl).
   u32 rot = blockIdx.x * 4u + (threadIdx.x >> 6);
   while (__ballot(live)) {
-#ifdef TPZ_CODEC_ROT2   // diagnostic: rotate every second trip
-    switch ((uni(rot++) >> 1) & 3u) {
-#else
     switch (uni(rot++) & 3u) {
-#endif
       case 0: __builtin_amdgcn_s_setprio(0); break;
       case 1: __builtin_amdgcn_s_setprio(1); break;
       case 2: __builtin_amdgcn_s_setprio(2); break;
@@ -1523,16 +1334,8 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     // half-slot, so the bytes past it still hold the bytes kRing before (a far copy of an
     // entry 120 bytes back is served from the ring; with whole 16-byte slots only about half
     // of them were). Everything below Pl is stored (the lines completed before this step).
-#ifdef TPZ_CODEC_RINGLO_LINE
-    const u32 ring_lo = Pl >= kRing - kRingLine ? Pl - (kRing - kRingLine) : 0u;
-#else
-#ifdef TPZ_CODEC_SLOT16
-    const u32 Pr = (P + 15) & ~15u;
-#else
     const u32 Pr = (P + 7) & ~7u;
-#endif
     const u32 ring_lo = Pr >= kRing ? Pr - kRing : 0u;
-#endif
     const u32 q0 = P - eoff;                                          // a copy's first source byte
     const bool gcopy = prod && far && q0 < ring_lo;
     // the 16-byte pieces this step loads from memory (a prefix of the step's four): a literal's,
@@ -1620,25 +1423,6 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
       const u64 mk = __ballot(has);
       if (mk == 0) break;
       const u32 cnt = __builtin_popcountll(mk);
-#ifdef TPZ_CODEC_PERMUTE
-      // the k-th completed line goes to lanes 4k .. 4k + 3 (mod 64): its owner pushes fl | lane
-      // (fl is 64-aligned) to lane 4k with ds_permute, the quad broadcasts it with DPP
-      const u32 kr = __builtin_amdgcn_mbcnt_hi((u32)(mk >> 32), __builtin_amdgcn_mbcnt_lo((u32)mk, 0u));
-      for (u32 q = 0; q < cnt; q += kWave / 4) {
-        const bool send = has && kr >= q && kr < q + kWave / 4;
-        const u32 tgt = send ? 4u * (kr - q) : ((lane & ~3u) | 1u);   // others: never a quad's lane 0
-        const u32 x0 = (u32)__builtin_amdgcn_ds_permute((int)(4 * tgt), (int)(fl | lane));
-        const u32 x = (u32)__builtin_amdgcn_mov_dpp((int)x0, 0x00, 0xF, 0xF, false);
-        const u32 k = q + (lane >> 2);
-        if (k < cnt) {
-          const u32 a = x & ~63u;
-          const uint8_t* Rs = rings + (wid * kWave + (x & 63u)) * kRing;
-          const u32 o = (a & (kRing - 1)) + 16 * (lane & 3);
-          st16u(p.dst + a + 16 * (lane & 3), lds16(Rs + o));
-        }
-      }
-      if (has) fl += kRingLine;
-#else
       if (has) {
         const u32 k = __builtin_amdgcn_mbcnt_hi((u32)(mk >> 32), __builtin_amdgcn_mbcnt_lo((u32)mk, 0u));
         fl_addr[wid][k] = fl;
@@ -1660,7 +1444,6 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
       }
       __builtin_amdgcn_wave_barrier();
       if (has) fl += kRingLine;
-#endif
     }
   }
 #ifdef TPZ_CODEC_STAMPS
@@ -1741,29 +1524,14 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
   p.status = a.status;
   p.defer_list = a.defer_list;
   p.defer_count = a.defer_count;
-#if defined(TPZ_CODEC_GROUPS)
-  {
-    u32 gg = (a.n_blocks + kGroupBlocks * kGroupWaves - 1) / (kGroupBlocks * kGroupWaves);
-    if (gg > a.num_cus) gg = a.num_cus;
-    if (gg == 0) gg = 1;
-    p.group_pass = 1;
-    hipLaunchKernelGGL(snappy_group_kernel<kGroupBlocks>, dim3(gg), dim3(kWave * kGroupWaves), 0,
-                       stream, p);
-  }
-#elif !defined(TPZ_CODEC_NO_LANES)
   if (a.n_blocks) {
     p.group_pass = 1;
-#ifndef TPZ_CODEC_LANE_SNAPPY
     hipLaunchKernelGGL(snappy_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),
                        0, stream, p);
-#ifndef TPZ_CODEC_NO_LZ4_RING
     hipLaunchKernelGGL(lz4_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),
                        0, stream, p);
-#endif
-#endif
     hipLaunchKernelGGL(codec_lane_kernel, dim3((a.n_blocks + 255) / 256), dim3(256), 0, stream, p);
   }
-#endif
   u32 grid = (a.n_blocks + kSmallWaves - 1) / kSmallWaves;
   if (grid > a.num_cus) grid = a.num_cus;
   if (grid == 0) grid = 1;
