@@ -579,17 +579,20 @@ int tpz_snappy_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64
 int tpz_lz4_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64_t n_blocks,
                           uint8_t* h_out, uint64_t out_cap, uint64_t* h_out_ext,
                           uint64_t* out_len);
-/* ---- compaction output with the default codec, on the device ------------------------------
- * compress::encode(data, CompressOptions::Snappy) (src/block/compress.rs:66-71, :82-93; the
- * default compress_option, src/opt.rs:48) for every block of a batch of Uncompress blocks in HBM
- * (tpz_encode_blocks' output): block i = payload | crc | 1 becomes snappy_raw(payload | crc) | 2,
+/* ---- compaction output with a codec, on the device ---------------------------------------
+ * compress::encode(data, opt) (src/block/compress.rs:66-77, :82-93) for every block of a batch
+ * of Uncompress blocks in HBM (tpz_encode_blocks' output), opt = the SST's compress_option
+ * (src/table/builder.rs:74; Snappy by default, src/opt.rs:48):
+ *   codec 2 (Snappy): block i = payload | crc | 1 becomes snappy_raw(payload | crc) | 2
+ *   codec 3 (Lz4):    u32 LE size | lz4_block(payload | crc) | 3 (lz4::block::compress with
+ *                     prepend_size; every match ends 5 bytes and starts 12 bytes before the
+ *                     end, as LZ4_decompress_safe requires)
  * written back to back into d_dst; d_dst_ext gets n_blocks + 1 extents (its last entry = the
  * bytes written), so BlockMeta::offset of block i is d_dst_ext[i] (src/table/builder.rs:74-84).
- * Blocks with another tag are copied unchanged. codec must be 2 (snappy); any other value is
- * TPZ_ERR_INVALID_ARG. The stream is a valid snappy raw stream of the same bytes (snap decodes
- * it); it is not byte-identical to snap::raw::Encoder's output. d_dst needs
- * tpz_layout_compress_bound(src_bytes, n_blocks) bytes. Asynchronous on `stream`; uses the
- * stream's workspace (scratch of that bound). */
+ * Blocks with another tag are copied unchanged; any other codec is TPZ_ERR_INVALID_ARG. The
+ * streams decode with snap / liblz4 to exactly payload | crc; they are not byte-identical to
+ * those libraries' encoders. d_dst needs tpz_layout_compress_bound(src_bytes, n_blocks) bytes.
+ * Asynchronous on `stream`; uses the stream's workspace (scratch of that bound). */
 uint64_t tpz_layout_compress_bound(uint64_t src_bytes, uint64_t n_blocks);
 tpz_err tpz_compress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint32_t codec, uint8_t* d_dst,
                             uint64_t* d_dst_ext, void* stream);

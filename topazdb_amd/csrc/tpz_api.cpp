@@ -593,7 +593,7 @@ uint64_t tpz_layout_compress_bound(uint64_t src_bytes, uint64_t n_blocks) {
 
 tpz_err tpz_compress_blocks(tpz_ctx* c, const tpz_batch* b, uint32_t codec, uint8_t* d_dst,
                             uint64_t* d_dst_ext, void* stream) {
-  if (!c || !b || !d_dst_ext || codec != 2) return TPZ_ERR_INVALID_ARG;
+  if (!c || !b || !d_dst_ext || (codec != 2 && codec != 3)) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks && (!b->d_src || !b->d_ext || !d_dst)) return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   const uint64_t scratch = tpz::compress_scratch_bytes(b->src_bytes, b->n_blocks);
@@ -606,7 +606,7 @@ tpz_err tpz_compress_blocks(tpz_ctx* c, const tpz_batch* b, uint32_t codec, uint
     if (r != TPZ_SUCCESS) return r;
   }
   uint8_t* sc = static_cast<uint8_t*>(w->d_comp);
-  tpz::launch_compress(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, sc, d_dst_ext,
+  tpz::launch_compress(b->d_src, b->d_ext, b->src_bytes, b->n_blocks, codec, sc, d_dst_ext,
                        reinterpret_cast<uint64_t*>(sc + ((scratch + 15) & ~15ull)), d_dst,
                        c->num_cus, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());

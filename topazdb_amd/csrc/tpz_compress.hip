@@ -1,4 +1,4 @@
-// tpz_compress.hip — compaction output with topazdb's default codec on the device:
+// tpz_compress.hip — compaction output with a codec on the device (Snappy, the default, or Lz4):
 // compress::encode(data, CompressOptions::Snappy) (src/block/compress.rs:66-71, 82-93) for every
 // Uncompress block of a batch the write side produced (tpz_encode_blocks): the payload and CRC
 // (block.rs:31-44) become a snappy raw stream (snap::raw::Encoder::compress_vec's format: varint
@@ -46,34 +46,41 @@ __device__ __forceinline__ u32 ld4(const uint8_t* base, u32 a) {
   return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
 }
 
-struct Emit {
+// Snappy elements (snap::raw's format): a varint preamble, literals (tag 00, the length - 1
+// inline below 60, else in 1..4 bytes), copy-1 for 4..11 bytes within 2 KiB, else copy-2
+// (1..64 bytes, a 2-byte offset); a long match is cut into pieces of at most 64 (never leaving
+// a piece under 4).
+struct SnappyEmit {
+  static constexpr u32 kTag = 2;           // CompressOptions::Snappy
   uint8_t* out;   // the block's scratch slot
   u64 op;         // bytes written (wave-uniform)
-  const uint8_t* lit_src;   // the staged payload (LDS)
 
   __device__ __forceinline__ void byte(u64 at, u32 v) const {
     if (lane_id() == 0) out[at] = (uint8_t)v;
   }
-  // snappy literal element: tag (len-1 < 60: inline; else 60..63 + 1..4 length bytes), bytes
-  __device__ __forceinline__ void literal(u32 lo, u32 hi) {
+  __device__ __forceinline__ void begin(u64 m) {
+    for (u64 v = m;; v >>= 7) {
+      byte(op++, (u32)((v & 0x7F) | (v > 0x7F ? 0x80 : 0)));
+      if (v <= 0x7F) break;
+    }
+  }
+  // literal bytes src[lo .. hi) (LDS or global), at most 2^32 per element
+  __device__ __forceinline__ void literal(const uint8_t* src, u64 lo, u64 hi) {
     if (hi <= lo) return;
-    const u32 v = hi - lo - 1;
+    const u64 v = hi - lo - 1;
     u32 hl = 1;
     if (v < 60) {
-      byte(op, v << 2);
+      byte(op, (u32)v << 2);
     } else {
       const u32 nb = v < (1u << 8) ? 1u : v < (1u << 16) ? 2u : v < (1u << 24) ? 3u : 4u;
       byte(op, (59u + nb) << 2);
-      for (u32 k = 0; k < nb; k++) byte(op + 1 + k, v >> (8 * k));
+      for (u32 k = 0; k < nb; k++) byte(op + 1 + k, (u32)(v >> (8 * k)));
       hl = 1 + nb;
     }
-    const u32 n = hi - lo;
-    for (u32 i = lane_id(); i < n; i += 64) out[op + hl + i] = lit_src[lo + i];
+    const u64 n = hi - lo;
+    for (u64 i = lane_id(); i < n; i += 64) out[op + hl + i] = src[lo + i];
     op += hl + n;
   }
-  // copy elements for a match of len bytes at distance off (< 65536): copy-1 for 4..11 bytes
-  // within 2 KiB, else copy-2 (1..64 bytes); a long match is cut into pieces of at most 64
-  // (never leaving a piece under 4 where copy-1 would be wanted)
   __device__ __forceinline__ void copy(u32 off, u32 len) {
     while (len) {
       const u32 l = len > 64 ? (len - 64 < 4 ? 60u : 64u) : len;
@@ -90,6 +97,63 @@ struct Emit {
       len -= l;
     }
   }
+  __device__ __forceinline__ void seq(const uint8_t* src, u32 lo, u32 hi, u32 off, u32 len) {
+    literal(src, lo, hi);
+    copy(off, len);
+  }
+  __device__ __forceinline__ void last(const uint8_t* src, u64 lo, u64 hi) {
+    for (; hi - lo > (1ull << 32); lo += 1ull << 32) literal(src, lo, lo + (1ull << 32));
+    literal(src, lo, hi);
+  }
+  // matches start at q + 4 <= n and may run to the end
+  static __device__ __forceinline__ u32 last_start(u32 n) { return n - 4; }
+  static __device__ __forceinline__ u32 match_end(u32 n) { return n; }
+};
+
+// LZ4 block format as lz4::block::compress(data, None, true) writes it (compress.rs:73-77): the
+// i32 LE size, then sequences: token (literal length | match length - 4, 15 = continued in
+// 255-bytes), literals, a 2-byte LE offset, the match length continuation; the last sequence is
+// literals only. The end rules LZ4_decompress_safe enforces (liblz4 1.9.3, oracle/tpz_lz4.c): a
+// match starts at least 12 bytes before the end and ends at least 5 before it.
+struct Lz4Emit {
+  static constexpr u32 kTag = 3;           // CompressOptions::Lz4
+  uint8_t* out;
+  u64 op;
+
+  __device__ __forceinline__ void byte(u64 at, u32 v) const {
+    if (lane_id() == 0) out[at] = (uint8_t)v;
+  }
+  __device__ __forceinline__ void begin(u64 m) {
+    for (int k = 0; k < 4; k++) byte(op + k, (u32)(m >> (8 * k)));
+    op += 4;
+  }
+  __device__ __forceinline__ void length(u64 v) {      // a 15-continued length: 255s, remainder
+    for (; v >= 255; v -= 255) byte(op++, 255);
+    byte(op++, (u32)v);
+  }
+  __device__ __forceinline__ void literals(const uint8_t* src, u64 lo, u64 n) {
+    for (u64 i = lane_id(); i < n; i += 64) out[op + i] = src[lo + i];
+    op += n;
+  }
+  __device__ __forceinline__ void seq(const uint8_t* src, u32 lo, u32 hi, u32 off, u32 len) {
+    const u32 ll = hi - lo, ml = len - 4;
+    byte(op++, ((ll < 15 ? ll : 15u) << 4) | (ml < 15 ? ml : 15u));
+    if (ll >= 15) length(ll - 15);
+    literals(src, lo, ll);
+    byte(op, off & 0xFFu);
+    byte(op + 1, off >> 8);
+    op += 2;
+    if (ml >= 15) length(ml - 15);
+  }
+  __device__ __forceinline__ void last(const uint8_t* src, u64 lo, u64 hi) {
+    const u64 ll = hi - lo;
+    byte(op++, (ll < 15 ? (u32)ll : 15u) << 4);
+    if (ll >= 15) length(ll - 15);
+    literals(src, lo, ll);
+  }
+  // MFLIMIT (12) and LASTLITERALS (5)
+  static __device__ __forceinline__ u32 last_start(u32 n) { return n >= 12 ? n - 12 : 0u; }
+  static __device__ __forceinline__ u32 match_end(u32 n) { return n >= 5 ? n - 5 : 0u; }
 };
 
 struct CompressParams {
@@ -106,7 +170,8 @@ struct CompressParams {
 // L + L / 6 + 40 apart.
 __device__ __host__ __forceinline__ u64 cslot(u64 ext_i, u64 i) { return ext_i + ext_i / 6 + 40 * i; }
 
-__global__ __launch_bounds__(1024) void snappy_compress_kernel(CompressParams p) {
+template <class Emit>
+__global__ __launch_bounds__(1024) void compress_kernel(CompressParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kCWaves * kCSlot];
   const u32 lane = lane_id(), wid = uni(threadIdx.x >> 6);
   uint8_t* win = lds + wid * kCSlot;
@@ -121,30 +186,13 @@ __global__ __launch_bounds__(1024) void snappy_compress_kernel(CompressParams p)
       if (lane == 0) p.size[b] = L;
       continue;
     }
-    const u64 m = L - 1;                              // payload | crc: the bytes compress_vec sees
-    Emit E{out, 0, nullptr};
-    for (u64 v = m;; v >>= 7) {                       // the varint preamble
-      E.byte(E.op++, (u32)((v & 0x7F) | (v > 0x7F ? 0x80 : 0)));
-      if (v <= 0x7F) break;
-    }
+    const u64 m = L - 1;                              // payload | crc: the bytes the codec sees
+    Emit E{out, 0};
+    E.begin(m);
     if (m > kCMaxStaged) {
-      // past the LDS window: literal elements of at most 65536 bytes, straight from HBM
-      for (u64 lo = 0; lo < m; lo += 65536) {
-        const u32 n = (u32)(m - lo < 65536 ? m - lo : 65536);
-        const u32 v = n - 1;
-        u32 hl = 1;
-        if (v < 60) {
-          E.byte(E.op, v << 2);
-        } else {
-          const u32 nb = v < 256 ? 1u : 2u;
-          E.byte(E.op, (59u + nb) << 2);
-          for (u32 k = 0; k < nb; k++) E.byte(E.op + 1 + k, v >> (8 * k));
-          hl = 1 + nb;
-        }
-        for (u32 i = lane; i < n; i += 64) out[E.op + hl + i] = p.src[s + lo + i];
-        E.op += hl + n;
-      }
-      E.byte(E.op, 2);
+      // past the LDS window: one literal run straight from HBM (a valid stream, uncompressed)
+      E.last(p.src + s, 0, m);
+      E.byte(E.op, Emit::kTag);
       if (lane == 0) p.size[b] = E.op + 1;
       continue;
     }
@@ -168,18 +216,18 @@ __global__ __launch_bounds__(1024) void snappy_compress_kernel(CompressParams p)
       __builtin_amdgcn_wave_barrier();
     }
     const uint8_t* d = win + a0;
-    E.lit_src = d;
     const u32 n = (u32)m;
+    const u32 qlast = Emit::last_start(n), mend = Emit::match_end(n);
     u32 pos = 0, lit = 0;
-    while (pos + 4 <= n) {
+    while (n >= 4 && pos <= qlast) {
       const u32 q = pos + lane;
-      const bool ok = q + 4 <= n;
+      const bool ok = q <= qlast;
       const u32 w = ok ? ld4(win, a0 + q) : 0u;
       const u32 h = (w * 0x1E35A7BDu) >> (32 - kHashBits);
       // a bucket holds a position of an earlier window of this block, or another block's: only a
       // verified candidate before q counts
       const u32 c = ok ? tab[h] : 0u;
-      const bool hit = ok && c < pos && q - c < 65536 && ld4(win, a0 + c) == w;
+      const bool hit = ok && c < pos && q - c < 65536 && q + 4 <= mend && ld4(win, a0 + c) == w;
       const u64 hm = __ballot(hit);
       if (!hm) {
         if (ok) tab[h] = q;
@@ -189,11 +237,11 @@ __global__ __launch_bounds__(1024) void snappy_compress_kernel(CompressParams p)
       const u32 f = (u32)__builtin_ctzll(hm);
       const u32 qf = pos + f, cf = __builtin_amdgcn_readlane(c, f);
       if (ok && lane <= f) tab[h] = q;
-      // extend the match past its first 4 bytes, 64 bytes per round
+      // extend the match past its first 4 bytes, 64 bytes per round, up to mend
       u32 len = 4;
       for (;;) {
         const u32 k = qf + len + lane;
-        const bool same = k < n && d[k] == d[cf + len + lane];
+        const bool same = k < mend && d[k] == d[cf + len + lane];
         const u64 mm = ~__ballot(same);
         if (mm) {
           len += (u32)__builtin_ctzll(mm);
@@ -201,13 +249,12 @@ __global__ __launch_bounds__(1024) void snappy_compress_kernel(CompressParams p)
         }
         len += 64;
       }
-      E.literal(lit, qf);
-      E.copy(qf - cf, len);
+      E.seq(d, lit, qf, qf - cf, len);
       pos = qf + len;
       lit = pos;
     }
-    E.literal(lit, n);
-    E.byte(E.op, 2);                                  // CompressOptions::Snappy
+    E.last(d, lit, n);
+    E.byte(E.op, Emit::kTag);
     if (lane == 0) p.size[b] = E.op + 1;
   }
 }
@@ -244,7 +291,7 @@ uint64_t compress_scratch_bytes(uint64_t src_bytes, uint32_t n_blocks) {
   return cslot(src_bytes, n_blocks) + 64;
 }
 
-void launch_compress(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n_blocks,
+void launch_compress(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n_blocks, u32 codec,
                      uint8_t* scratch, u64* sizes, u64* part, uint8_t* dst, u32 num_cus,
                      hipStream_t stream) {
   if (n_blocks == 0) {
@@ -253,8 +300,11 @@ void launch_compress(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n_bl
   }
   CompressParams p{src, ext, src_bytes, n_blocks, scratch, sizes};
   u32 grid = (n_blocks + kCWaves - 1) / kCWaves;
-  if (grid > num_cus) grid = num_cus;      // 16 waves (~147 KiB of LDS) per CU, persistent
-  hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(1024), 0, stream, p);
+  if (grid > num_cus) grid = num_cus;      // 16 waves (132 KiB of LDS) per CU, persistent
+  if (codec == 3)
+    hipLaunchKernelGGL(compress_kernel<Lz4Emit>, dim3(grid), dim3(1024), 0, stream, p);
+  else
+    hipLaunchKernelGGL(compress_kernel<SnappyEmit>, dim3(grid), dim3(1024), 0, stream, p);
   launch_scan_u64(sizes, n_blocks, part, stream);
   u32 g2 = (n_blocks + 3) / 4;
   if (g2 > 8 * num_cus) g2 = 8 * num_cus;

@@ -304,7 +304,7 @@ void launch_scan_u64(uint64_t* a, uint32_t n, uint64_t* part, hipStream_t stream
 // encode, the scan of the sizes into dst_ext and the packing into dst.
 uint64_t compress_scratch_bytes(uint64_t src_bytes, uint32_t n_blocks);
 void launch_compress(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes, uint32_t n_blocks,
-                     uint8_t* scratch, uint64_t* dst_ext, uint64_t* part, uint8_t* dst,
+                     uint32_t codec, uint8_t* scratch, uint64_t* dst_ext, uint64_t* part, uint8_t* dst,
                      uint32_t num_cus, hipStream_t stream);
 void launch_flat_layout(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
                         uint32_t n_blocks, uint64_t* first, uint64_t* part, uint32_t num_cus,

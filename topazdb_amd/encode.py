@@ -138,10 +138,10 @@ def compress_bound(src_bytes: int, n_blocks: int) -> int:
 def compress_blocks(ctx: Context, src: torch.Tensor, ext: torch.Tensor, n_blocks: int,
                     src_bytes: int, codec: int = 2, out: torch.Tensor | None = None,
                     stream: torch.cuda.Stream | None = None):
-    """tpz_compress_blocks: compress::encode with CompressOptions::Snappy (compress.rs:66-71)
-    for every Uncompress block of a device batch (the write side's output, compaction with the
-    default codec, src/opt.rs:48). Returns (out, out_ext): the encoded blocks back to back and
-    their n_blocks + 1 extents (int64, device)."""
+    """tpz_compress_blocks: compress::encode with CompressOptions::Snappy (codec 2, the default,
+    src/opt.rs:48; compress.rs:66-71) or Lz4 (codec 3, :73-77) for every Uncompress block of a
+    device batch (the write side's output: compaction output with the SST's codec). Returns
+    (out, out_ext): the encoded blocks back to back and their n_blocks + 1 extents (int64)."""
     dev = _dev(ctx.device)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     if out is None:
