@@ -482,15 +482,11 @@ __device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams&
     x = slice4(rep, r, x ^ v[t].z);
     x = slice4(rep, r, x ^ v[t].w);
   }
-#ifdef TPZ_BW_GFSTEP
-  return i == 0 ? x : (gf_mul(p.step_shift, acc) ^ x);
-#else
   // acc shifted by one step: four byte-table lookups instead of a 32-step GF(2) multiply
   const u32* sh = rep + kCrcRepWords + kWaves * kWaveLds / 4;
   const u32 t = xor3(sh[acc & 0xFF], sh[256 + ((acc >> 8) & 0xFF)], sh[512 + ((acc >> 16) & 0xFF)]) ^
                 sh[768 + (acc >> 24)];
   return i == 0 ? x : (t ^ x);
-#endif
 }
 
 // The list entries [lo, hi) (this workgroup's share of the bigwave list), one block per wave:
