@@ -6,4 +6,4 @@ OUT=gpurun_out/r4c
 mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -60 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
-VARIANTS="${VARIANTS:-full head sarw mcomb sarw_mcomb nocf lutvalu nocrc stamps onchip onchip_sarw onchip_mcomb onchip_sarw_mcomb onchip_nocf onchip_lutvalu onchip_nocrc}" PMCV="full sarw mcomb sarw_mcomb onchip" bash tools/gpu_r4b.sh
+VARIANTS="${VARIANTS:-full head sarw mcomb sarw_mcomb sarw4_mcomb nocf lutvalu nocrc stamps onchip onchip_sarw onchip_mcomb onchip_sarw_mcomb onchip_sarw4_mcomb onchip_nocf onchip_lutvalu onchip_nocrc}" PMCV="full sarw_mcomb sarw4_mcomb mcomb onchip" bash tools/gpu_r4b.sh

@@ -130,10 +130,12 @@ std::vector<uint32_t> build_wave_tables(const std::vector<uint32_t>& dec) {
   const size_t ids = tpz::kWaveRepWords + tpz::kWaveMatWords;
   std::memcpy(&out[ids], &dec[16 * 256], (size_t)(tpz::kNumCrcTables - 16) * 256 * 4);
   const size_t sh = ids + (size_t)(tpz::kNumCrcTables - 16) * 256;
-  for (int i = 0; i < 4; i++) {
-    const uint32_t z = x8n((uint64_t)(tpz::kCrcChainBytes - 1 - i));
-    for (int b = 0; b < 256; b++) out[sh + (size_t)i * 256 + b] = dec[b] ? multmodp(z, dec[b]) : 0u;
-  }
+  for (int h = 0; h < 2; h++)        // shifts by kCrcChainBytes, then by half of it
+    for (int i = 0; i < 4; i++) {
+      const uint32_t z = x8n((uint64_t)((tpz::kCrcChainBytes >> h) - 1 - i));
+      for (int b = 0; b < 256; b++)
+        out[sh + (size_t)(4 * h + i) * 256 + b] = dec[b] ? multmodp(z, dec[b]) : 0u;
+    }
   return out;
 }
 

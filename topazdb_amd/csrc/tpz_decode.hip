@@ -39,6 +39,17 @@
 #if defined(TPZ_ABL_SARW) && !defined(TPZ_CRC_SARW)
 #define TPZ_CRC_SARW   // variant builds: make variants (libtpz_gpu_sarw.so, onchip_sarw, ...)
 #endif
+#if defined(TPZ_ABL_SARW4)   // four byte chains per lane run (20 bytes each) instead of two
+#define TPZ_CRC_SARW4
+#ifndef TPZ_CRC_SARW
+#define TPZ_CRC_SARW
+#endif
+#endif
+#ifdef TPZ_CRC_SARW4
+#define TPZ_IS_SARW4 1
+#else
+#define TPZ_IS_SARW4 0
+#endif
 #if defined(TPZ_ABL_MCOMB) && !defined(TPZ_CRC_MCOMB)
 #define TPZ_CRC_MCOMB
 #endif
@@ -77,7 +88,8 @@ constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit 
 constexpr int kWaveTabWords = kWaveRepWords + kWaveMatWords + 5 * 256;
 constexpr int kTabOff = kWaveRepWords + kWaveMatWords - 40 * 256;
 #elif defined(TPZ_CRC_SARW)
-constexpr int kWaveTabWords = kWaveRepWords + kWaveIdsWords;
+static_assert(!TPZ_IS_SARW4, "the 4-chain build needs the matrix combine's layout (sarw4_mcomb)");
+constexpr int kWaveTabWords = kWaveRepWords + (kNumCrcTables - 16 + 4) * 256;   // ids 16..44
 constexpr int kTabOff = kWaveRepWords - 16 * 256;
 #elif defined(TPZ_CRC_MCOMB)
 constexpr int kWaveTabWords = 17 * 256 + kWaveMatWords;
@@ -832,9 +844,42 @@ struct CrcLane {
   u32 c2;       // the second byte chain: the run's last 40 bytes
   u32 lr;       // the lane's table replica
 #endif
+#ifdef TPZ_CRC_SARW4
+  u32 c3, c4;   // 4-chain build: the run's quarters 3 and 4
+#endif
 };
 
-#ifdef TPZ_CRC_SARW
+#if defined(TPZ_CRC_SARW4)
+// Step t: bytes [4t, 4t + 4) of each of the run's four 20-byte quarters, one byte chain each.
+__device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
+                                         int t) {
+  const u32* rep = crc_rep(tab);
+  const int a = L.act ? pb + L.seg + 4 * t : -kGuard;
+  const int q = L.act ? kCrcChainBytes / 2 : 0;
+  const u32 w0 = *reinterpret_cast<const u32*>(win + a);
+  const u32 w1 = *reinterpret_cast<const u32*>(win + a + q);
+  const u32 w2 = *reinterpret_cast<const u32*>(win + a + 2 * q);
+  const u32 w3 = *reinterpret_cast<const u32*>(win + a + 3 * q);
+  L.c = sarw4(rep, L.lr, L.c, w0);
+  L.c2 = sarw4(rep, L.lr, L.c2, w1);
+  L.c3 = sarw4(rep, L.lr, L.c3, w2);
+  L.c4 = sarw4(rep, L.lr, L.c4, w3);
+}
+// shift by kCrcChainBytes / 2 (T_19..T_16)
+__device__ __forceinline__ u32 crc_shift_half(const u32* tab, u32 a) {
+#ifdef TPZ_CRC_MCOMB
+  constexpr int id = 41;
+#else
+  constexpr int id = 45;
+#endif
+  return xor3(tlook(tab, id, a & 0xFF), tlook(tab, id + 1, (a >> 8) & 0xFF),
+              tlook(tab, id + 2, (a >> 16) & 0xFF)) ^ tlook(tab, id + 3, a >> 24);
+}
+// The run's raw CRC: Horner over the four quarters' chains.
+__device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) {
+  return crc_shift_half(tab, crc_shift_half(tab, crc_shift_half(tab, L.c) ^ L.c2) ^ L.c3) ^ L.c4;
+}
+#elif defined(TPZ_CRC_SARW)
 // Step t: bytes [8t, 8t + 8) of each of the run's two 40-byte halves, one byte chain per half.
 __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
                                          int t) {
@@ -974,6 +1019,9 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   L.c2 = 0;
   L.lr = lane & 31u;
 #endif
+#ifdef TPZ_CRC_SARW4
+  L.c3 = L.c4 = 0;
+#endif
   u32 carry = 0, rare = 0, cw[5];
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -1014,6 +1062,9 @@ __device__ __forceinline__ u32 wave_crc_w(const u32* tab, const uint8_t* win, in
 #ifdef TPZ_CRC_SARW
   L.c2 = 0;
   L.lr = lane & 31u;
+#endif
+#ifdef TPZ_CRC_SARW4
+  L.c3 = L.c4 = 0;
 #endif
 #pragma unroll
   for (int t = 0; t < kCrcLaneBytes / 16; t++) crc_step(tab, win, pb, L, t);
@@ -1343,10 +1394,15 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     const int ids = kWaveRepWords + kWaveMatWords;     // id 16 in the image
 #if defined(TPZ_CRC_SARW) && defined(TPZ_CRC_MCOMB)
     put(p.wave_tables, 0, kWaveRepWords + kWaveMatWords);
+#ifdef TPZ_CRC_SARW4
+    put(p.wave_tables + ids + (40 - 16) * 256, kWaveRepWords + kWaveMatWords, 256);
+    put(p.wave_tables + ids + (45 - 16) * 256, kWaveRepWords + kWaveMatWords + 256, 4 * 256);
+#else
     put(p.wave_tables + ids + (40 - 16) * 256, kWaveRepWords + kWaveMatWords, 5 * 256);
+#endif
 #elif defined(TPZ_CRC_SARW)
     put(p.wave_tables, 0, kWaveRepWords);
-    put(p.wave_tables + ids, kWaveRepWords, kWaveIdsWords);
+    put(p.wave_tables + ids, kWaveRepWords, kWaveTabWords - kWaveRepWords);
 #elif defined(TPZ_CRC_MCOMB)
     put(p.crc_tables, 0, 16 * 256);
     put(p.crc_tables + kCrcInvTable * 256, 16 * 256, 256);

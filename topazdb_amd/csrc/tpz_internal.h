@@ -36,11 +36,12 @@ constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
 //                    Z_{80 l}(A) = XOR of column j for every set bit j of A; column 4q + c of lane
 //                    l at word 8192 + (q * 64 + l) * 4 + c (one ds_read_b128 per 4 columns)
 //   [10240, ...)     the decode tables' ids 16..40, then the shift by kCrcChainBytes (ids 41..44)
+//                    and by kCrcChainBytes / 2 (ids 45..48: the 4-chain diagnostic build)
 // Each wave-kernel build loads the parts it uses (tpz_decode.hip).
 constexpr int kCrcChainBytes = 40;
 constexpr int kWaveRepWords = 8192;
 constexpr int kWaveMatWords = 2048;
-constexpr int kWaveIdsWords = (kNumCrcTables - 16 + 4) * 256;
+constexpr int kWaveIdsWords = (kNumCrcTables - 16 + 8) * 256;
 constexpr int kWaveTableWords = kWaveRepWords + kWaveMatWords + kWaveIdsWords;
 // Big path entry-table capacity per block and column: slots are only written when 6n <= len
 // (the unified key+value table holds 2 x this).
