@@ -70,3 +70,43 @@ def test_batch_past_4_gib():
         past += int(ext_all[b]) >= (1 << 32)
     assert past >= 20
     ctx.close()
+
+
+def test_config5_batch_per_gpu():
+    """BASELINE.json configs[4]'s per-GPU share at full size on one GPU: 100 GiB over 8 GPUs =
+    12.5 GiB of 4k blocks, replicated on the device from a 2^16-block shard (3.2 M blocks, byte
+    offsets to 2^33.6). Every block's status, count and CRC equal its copy-0 twin's; sampled
+    blocks of every copy are compared byte for byte with the oracle."""
+    assert torch.cuda.is_available()
+    dev = torch.device("cuda", 0)
+    ctx = _lib.Context(0)
+    nb = 1 << 16
+    src, ext = synth.make_region("4k", nb)
+    src = np.ascontiguousarray(src[:int(ext[nb])])
+    ext = np.ascontiguousarray(ext[:nb + 1], np.uint64)
+    full, part = replicate_plan(int(ext[-1]), nb, int(12.5 * (1 << 30)))
+    batch, ext_all = replicate_on_device(src, ext, full, part, dev)
+    assert abs(int(ext_all[-1]) - 12.5 * (1 << 30)) < 128 * int(ext[1] - ext[0]) + int(ext[-1])
+    cols = decode_batch(ctx, batch)
+    torch.cuda.synchronize()
+    ctx.decode_check()
+    st = cols.status[:batch.n_blocks]
+    cnt = cols.count[:batch.n_blocks]
+    crc = cols.crc[:batch.n_blocks]
+    assert int((st != 0).sum()) == 0, "every block OK"
+    for c in range(1, full + (1 if part else 0)):
+        m = nb if c < full else part
+        lo = c * nb
+        assert torch.equal(cnt[lo:lo + m], cnt[:m]) and torch.equal(crc[lo:lo + m], crc[:m]), c
+    rng = np.random.default_rng(5)
+    picks = sorted(set(int(x) for x in rng.integers(0, batch.n_blocks, 300)) | {batch.n_blocks - 1})
+    cnt_h = cnt.cpu().numpy()
+    for b in picks:
+        t = b % nb
+        blk = src[int(ext[t]):int(ext[t + 1])]
+        o = O.decode_batch(blk, np.array([0, len(blk)], np.uint64))
+        assert int(cnt_h[b]) == int(o.count[0])
+        assert slot_entries(cols, int(ext_all[b]), b, int(cnt_h[b])) == o.entries(0), b
+    del cols, batch
+    torch.cuda.empty_cache()
+    ctx.close()
