@@ -253,3 +253,14 @@ def test_host_decoded_bound_truncated_and_other_tags():
     assert _host_bound([trunc]) == 1 and _host_bound([eleven]) == 1
     assert _host_bound([lz4]) == 1001 and _host_bound([plain]) == 21
     assert _host_bound([trunc, lz4, plain, b""]) == 1 + 1001 + 21 + 0
+
+
+def test_variant_builds_load():
+    """Every diagnostic build in topazdb_amd/variants (the tail-timeout build the GPU tests load,
+    the ablation builds the tools time) resolves every symbol: a variant links the product's
+    other objects, so a source file added to the product must reach its link line too."""
+    import ctypes
+    import glob
+    libs = glob.glob(os.path.join(os.path.dirname(_lib.LIB_PATH), "variants", "*.so"))
+    for f in libs:
+        ctypes.CDLL(f)
