@@ -782,7 +782,7 @@ __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const M
   if (cross) nx = src((int)x0 + d1);
   if (__ballot(act && e0 <= x0)) {
     // a lost map race (two entries ended in one chunk): walk forward to the holding entry
-    while (act && e0 <= x0) {
+    while (act && e0 <= x0 && j < last) {   // (bounded: the last segment holds the stream's end)
       j++;
       col.get2(min(j, last), e0, d0, e1, d1);
     }
@@ -1231,24 +1231,28 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       }
       __builtin_amdgcn_wave_barrier();
+      // The stream ends at its last byte: a chunk past it would hold no segment (and the map's
+      // walk to its segment would not end). Slotted: value_start(K) + V. Flat: the values end at
+      // 16 kch + dv + V; with no values the keys end at dk + K (no value chunk at all).
+      const u32 tot = FLAT ? (vc ? vs + vc : (kc ? dk + kc : 0u)) : vs + vc;
 #ifndef TPZ_ABL_NOCOPY
 #if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY)
       if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
         fuse = true;
         f_short = short_segs;
         f_nk = knz + vnz;
-        f_tot = vs + vc;
+        f_tot = tot;
         f_dst = FLAT ? nullptr : o.data + slot_base(ext_b, b);
         if (FLAT) fo = flat_out(o, kf, vf, kc, vc);
       } else
 #endif
       if (FLAT) {
         fo = flat_out(o, kf, vf, kc, vc);
-        copy_stream(Src16{win}, col, map, knz + vnz, vs + vc, FlatDst{&fo}, (u32)kMapLen);
+        copy_stream(Src16{win}, col, map, knz + vnz, tot, FlatDst{&fo}, (u32)kMapLen);
       } else {
-        const u32 nch = (vs + vc + 15) >> 4;
-        copy_stream(Src16{win}, col, map, knz + vnz, vs + vc,
-                    SlotDst{o.data + slot_base(ext_b, b), (nch + 7) & ~7u, vs + vc}, (u32)kMapLen);
+        const u32 nch = (tot + 15) >> 4;
+        copy_stream(Src16{win}, col, map, knz + vnz, tot,
+                    SlotDst{o.data + slot_base(ext_b, b), (nch + 7) & ~7u, tot}, (u32)kMapLen);
       }
 #endif
     }
