@@ -9,7 +9,11 @@
  *   3. compare the region and the block offsets with tpz_build_blocks (the host restatement),
  *      then decode the device region with tpz_decode_blocks and check every block is OK with
  *      the planned entry count;
- *   4. an entry with an empty key must be refused with its index (builder.rs:27).
+ *   4. an entry with an empty key must be refused with its index (builder.rs:27);
+ *   5. the region in the flat layout (tpz_flat_layout + tpz_decode_blocks_flat): the key and
+ *      value columns equal the entries' keys and values back to back;
+ *   6. compaction output with snappy on the device (tpz_compress_blocks), back through the
+ *      codec step to the same bytes.
  * Prints "ok <entries> <blocks>" and exits 0, or the first mismatch and exits 1.
  * Usage: c_encode [n_entries] [block_size]
  */
@@ -147,6 +151,105 @@ int main(int argc, char** argv) {
              first[b + 1] - first[b]);
       return 1;
     }
+
+  /* 5. the same region into the flat layout (tpz_flat_layout + tpz_decode_blocks_flat): the key
+   *    column must be the entries' keys back to back, the value column their values, and every
+   *    {kend, vend} pair the entry's end within its block */
+  {
+    uint64_t* d_fl;
+    const uint64_t st1 = (uint64_t)nb + 1;
+    CHECK_HIP(hipMalloc((void**)&d_fl, 3 * st1 * 8));
+    CHECK_TPZ(tpz_flat_layout(ctx, &batch, d_fl, st));
+    uint64_t* fl = malloc(3 * st1 * 8);
+    CHECK_HIP(hipStreamSynchronize(st));
+    CHECK_HIP(hipMemcpy(fl, d_fl, 3 * st1 * 8, hipMemcpyDeviceToHost));
+    if (fl[nb] != n || fl[st1 + nb] != kpos[n] || fl[2 * st1 + nb] != vpos[n]) {
+      printf("flat totals %llu %llu %llu\n", (unsigned long long)fl[nb],
+             (unsigned long long)fl[st1 + nb], (unsigned long long)fl[2 * st1 + nb]);
+      return 1;
+    }
+    tpz_flat_columns fc;
+    memset(&fc, 0, sizeof fc);
+    CHECK_HIP(hipMalloc((void**)&fc.d_keys, kpos[n] + 16));
+    CHECK_HIP(hipMalloc((void**)&fc.d_values, vpos[n] + 16));
+    CHECK_HIP(hipMalloc((void**)&fc.d_ends, (size_t)n * 8 + 8));
+    fc.d_first = d_fl;
+    fc.d_count = cols.d_count;
+    fc.d_status = cols.d_status;
+    fc.d_crc = cols.d_crc;
+    fc.d_spill_off = cols.d_spill_off;
+    fc.d_spill_used = cols.d_spill_used;
+    CHECK_TPZ(tpz_decode_blocks_flat(ctx, &batch, &fc, st));
+    CHECK_TPZ(tpz_decode_check(ctx, st));
+    uint8_t* fk = malloc(kpos[n] + 1);
+    uint8_t* fv = malloc(vpos[n] + 1);
+    uint32_t* fe = malloc((size_t)n * 8 + 8);
+    CHECK_HIP(hipMemcpy(fk, fc.d_keys, kpos[n], hipMemcpyDeviceToHost));
+    CHECK_HIP(hipMemcpy(fv, fc.d_values, vpos[n], hipMemcpyDeviceToHost));
+    CHECK_HIP(hipMemcpy(fe, fc.d_ends, (size_t)n * 8, hipMemcpyDeviceToHost));
+    CHECK_HIP(hipMemcpy(status, cols.d_status, nb, hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < nb; b++)
+      if (status[b] != TPZ_BLOCK_OK) {
+        printf("flat: block %u status %u\n", b, status[b]);
+        return 1;
+      }
+    if (memcmp(fk, keys, kpos[n]) != 0 || memcmp(fv, vals, vpos[n]) != 0) {
+      printf("flat columns differ from the entries\n");
+      return 1;
+    }
+    for (uint32_t b = 0; b < nb; b++)
+      for (uint32_t e = first[b]; e < first[b + 1]; e++)
+        if (fe[2 * e] != kpos[e + 1] - kpos[first[b]] || fe[2 * e + 1] != vpos[e + 1] - vpos[first[b]]) {
+          printf("flat: entry %u ends %u %u\n", e, fe[2 * e], fe[2 * e + 1]);
+          return 1;
+        }
+    free(fk);
+    free(fv);
+    free(fe);
+    free(fl);
+  }
+
+  /* 6. compaction output with the default codec: the region to snappy blocks on the device
+   *    (tpz_compress_blocks), back through the codec step and the decode: every block OK with its
+   *    planned count */
+  {
+    const uint64_t ccap = tpz_layout_compress_bound(ext[nb], nb);
+    uint8_t *d_c, *d_u;
+    uint64_t *d_cext, *d_uext;
+    CHECK_HIP(hipMalloc((void**)&d_c, ccap));
+    CHECK_HIP(hipMalloc((void**)&d_cext, ((size_t)nb + 1) * 8));
+    CHECK_TPZ(tpz_compress_blocks(ctx, &batch, 2, d_c, d_cext, st));
+    uint64_t* cext = malloc(((size_t)nb + 1) * 8);
+    CHECK_HIP(hipStreamSynchronize(st));
+    CHECK_HIP(hipMemcpy(cext, d_cext, ((size_t)nb + 1) * 8, hipMemcpyDeviceToHost));
+    tpz_batch cb = {d_c, d_cext, nb, cext[nb]};
+    uint64_t* sz = malloc(((size_t)nb + 1) * 8);
+    uint64_t* d_sz;
+    CHECK_HIP(hipMalloc((void**)&d_sz, (size_t)nb * 8));
+    CHECK_TPZ(tpz_decompressed_sizes(ctx, &cb, d_sz, st));
+    CHECK_HIP(hipStreamSynchronize(st));
+    CHECK_HIP(hipMemcpy(sz + 1, d_sz, (size_t)nb * 8, hipMemcpyDeviceToHost));
+    sz[0] = 0;
+    for (uint32_t b = 0; b < nb; b++) sz[b + 1] += sz[b];
+    if (sz[nb] != ext[nb]) {
+      printf("decompressed size %llu != %llu\n", (unsigned long long)sz[nb], (unsigned long long)ext[nb]);
+      return 1;
+    }
+    CHECK_HIP(hipMalloc((void**)&d_u, sz[nb] + 16));
+    CHECK_HIP(hipMalloc((void**)&d_uext, ((size_t)nb + 1) * 8));
+    CHECK_HIP(hipMemcpy(d_uext, sz, ((size_t)nb + 1) * 8, hipMemcpyHostToDevice));
+    CHECK_TPZ(tpz_decompress_blocks(ctx, &cb, d_u, d_uext, cols.d_status, st));
+    CHECK_HIP(hipStreamSynchronize(st));
+    uint8_t* u = malloc(sz[nb] + 1);
+    CHECK_HIP(hipMemcpy(u, d_u, sz[nb], hipMemcpyDeviceToHost));
+    if (memcmp(u, out, ext[nb]) != 0) {
+      printf("snappy round trip differs (%llu compressed bytes)\n", (unsigned long long)cext[nb]);
+      return 1;
+    }
+    free(u);
+    free(sz);
+    free(cext);
+  }
 
   /* an empty key is refused with its index (builder.rs:27 asserts) */
   uint64_t kpos2[3] = {0, 3, 3};

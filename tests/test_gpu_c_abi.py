@@ -65,7 +65,10 @@ def test_c_host_pipeline_golden_sst(tmp_path, name, chunk):
 def test_c_device_encode(tmp_path, n, block_size):
     """The device write side from plain C (examples/c_encode.c): tpz_plan_blocks +
     tpz_encode_blocks against the host restatement tpz_build_blocks (every byte and block
-    offset), the encoded region decoded back by tpz_decode_blocks, an empty key refused."""
+    offset), the encoded region decoded back by tpz_decode_blocks and into the flat layout
+    (tpz_flat_layout + tpz_decode_blocks_flat: the key / value columns are the entries' keys /
+    values back to back), snappy on the device (tpz_compress_blocks) back through the codec step
+    to the same bytes, an empty key refused."""
     exe = _build_c_example(tmp_path, "c_encode")
     r = subprocess.run([exe, str(n), str(block_size)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
