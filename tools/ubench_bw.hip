@@ -123,6 +123,155 @@ __global__ __launch_bounds__(1024) void wave4k_k(const uint4* __restrict__ s, ui
   }
 }
 
+// Persistent copies of 4 KiB chunks (64 lanes x 4 x 16 B), the next chunk's loads in flight while
+// this chunk's stores issue, as the decode's wave path does. How a wave finds its chunks:
+//   MODE 0  rows: wave (x, w) takes chunks k*W + 16x + w (the decode's row layout, static)
+//   MODE 1  contiguous: wave g takes chunks [g*per, (g+1)*per)
+//   MODE 2  dynamic: every chunk claimed from one global counter (claimed two ahead)
+//   MODE 3  dynamic, 4 consecutive chunks per claim
+//   MODE 4  per-XCD counters (blockIdx % 8), 16-chunk groups dealt round-robin to the XCDs, then
+//           the other XCDs' counters once a wave's own runs out
+//   MODE 5  semi-persistent: workgroup x takes the K rows of 16 chunks from 16 K x, then exits
+//           (grid = nchunks / 16 K)
+template <int MODE>
+__global__ __launch_bounds__(1024) void persist_k(const uint4* __restrict__ s, uint4* __restrict__ d,
+                                                 u64 nchunks, u32* ctr, u32 K = 0) {
+  const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpg = blockDim.x >> 6;
+  const u64 W = (u64)gridDim.x * wpg;
+  const u64 g = (u64)blockIdx.x * wpg + wv;
+  const u64 per = (nchunks + W - 1) / W;
+  u64 k = 0;           // static modes: chunks taken so far
+  u32 grp = 0, left = 0;  // MODE 3: current claim
+  u32 xo = 0;          // MODE 4: counter offset being drained
+  const u32 xcd = blockIdx.x & 7;
+  const u64 ngroups = (nchunks + 15) >> 4;
+  auto atom = [&](u32* c, u32 inc) -> u32 {
+    u32 r = 0;
+    if (lane == 0) r = atomicAdd(c, inc);
+    return __builtin_amdgcn_readfirstlane(r);
+  };
+  auto next = [&]() -> u64 {
+    if (MODE == 0) return (k++) * W + g;
+    if (MODE == 5) { const u64 c = ((u64)blockIdx.x * K + k) * wpg + wv; return (k++ < K) ? c : ~0ull; }
+    if (MODE == 1) { const u64 c = g * per + k; return (k++ < per) ? c : ~0ull; }
+    if (MODE == 2) return atom(ctr, 1);
+    if (MODE == 3) {
+      if (!left) { grp = atom(ctr, 4); left = 4; }
+      return (u64)grp + (4 - left--);
+    }
+    // MODE 4: XCD xc's groups are xc, xc + 8, ...; its counter counts chunks of those groups
+    while (xo < 8) {
+      const u32 xc = (xcd + xo) & 7;
+      const u64 mine = (ngroups > xc) ? ((ngroups - xc + 7) >> 3) * 16 : 0;
+      const u32 c = atom(ctr + 64 * xc, 1);
+      if (c < mine) return ((u64)(c >> 4) * 8 + xc) * 16 + (c & 15);
+      xo++;
+    }
+    return ~0ull;
+  };
+  u64 cur = next(), nxt = next();
+  uint4 v[4];
+  if (cur < nchunks)
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = s[cur * 256 + q * 64 + lane];
+  while (cur < nchunks) {
+    const u64 nn = next();
+    uint4 w[4];
+    if (nxt < nchunks)
+#pragma unroll
+      for (int q = 0; q < 4; q++) w[q] = s[nxt * 256 + q * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < 4; q++) d[cur * 256 + q * 64 + lane] = v[q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = w[q];
+    cur = nxt;
+    nxt = nn;
+  }
+}
+
+// rows (MODE 0) with two chunks' loads in flight while a chunk is stored; STORE_FIRST: the
+// chunk's stores issue before the next chunk's loads
+template <bool STORE_FIRST>
+__global__ __launch_bounds__(1024) void rows2_k(const uint4* __restrict__ s, uint4* __restrict__ d, u64 nchunks) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 W = (u64)gridDim.x * (blockDim.x >> 6);
+  u64 c = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  uint4 a[4], b[4];
+  if (c < nchunks)
+#pragma unroll
+    for (int q = 0; q < 4; q++) a[q] = s[c * 256 + q * 64 + lane];
+  if (c + W < nchunks)
+#pragma unroll
+    for (int q = 0; q < 4; q++) b[q] = s[(c + W) * 256 + q * 64 + lane];
+  while (c < nchunks) {
+    uint4 n[4];
+    const u64 c2 = c + 2 * W;
+    if (STORE_FIRST) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) d[c * 256 + q * 64 + lane] = a[q];
+      if (c2 < nchunks)
+#pragma unroll
+        for (int q = 0; q < 4; q++) n[q] = s[c2 * 256 + q * 64 + lane];
+    } else {
+      if (c2 < nchunks)
+#pragma unroll
+        for (int q = 0; q < 4; q++) n[q] = s[c2 * 256 + q * 64 + lane];
+#pragma unroll
+      for (int q = 0; q < 4; q++) d[c * 256 + q * 64 + lane] = a[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) { a[q] = b[q]; b[q] = n[q]; }
+    c += W;
+  }
+}
+
+// rows (MODE 0) with ping-pong buffers a / b (no register moves in the loop: a move of a
+// register whose load is in flight waits for it): chunk c + W's loads in flight while chunk c
+// is stored. Loads and stores past the end go through a buffer descriptor (no branches).
+__device__ __forceinline__ void ld4(__amdgpu_buffer_rsrc_t r, u64 c, u32 lane, uint4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    v[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (u32)(c * 4096 + q * 1024 + lane * 16), 0, 0));
+}
+__device__ __forceinline__ void st4(__amdgpu_buffer_rsrc_t r, u64 c, u32 lane, const uint4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, v[q]), r,
+                                           (u32)(c * 4096 + q * 1024 + lane * 16), 0, 0);
+}
+// (offsets are u32: the buffers are viewed from a base per 4 GiB... the 4.36 GB case uses two
+// halves, see the launch)
+__global__ __launch_bounds__(1024) void pp_k(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, u64 nchunks) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 W = (u64)gridDim.x * (blockDim.x >> 6);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)s, (short)0, (int)(nchunks * 4096), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d, (short)0, (int)(nchunks * 4096), 0x00020000);
+  u64 c = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  uint4 a[4], b[4];
+  ld4(rs, c, lane, a);
+  while (c < nchunks) {
+    ld4(rs, c + W, lane, b);
+    st4(rd, c, lane, a);
+    c += W;
+    if (c >= nchunks) break;
+    ld4(rs, c + W, lane, a);
+    st4(rd, c, lane, b);
+    c += W;
+  }
+}
+
+// non-persistent: one wave per 4 KiB chunk (4 loads, 4 stores), 4 waves per workgroup
+__global__ __launch_bounds__(256) void flat_w4k_k(const uint4* __restrict__ s, uint4* __restrict__ d, u64 nchunks) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 c = (u64)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  uint4 v[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) v[q] = s[c * 256 + q * 64 + lane];
+#pragma unroll
+  for (int q = 0; q < 4; q++) d[c * 256 + q * 64 + lane] = v[q];
+}
+
 int main(int argc, char** argv) {
   std::vector<std::string> vars;
   for (int i = 1; i < argc; i++) vars.push_back(argv[i]);
@@ -130,11 +279,12 @@ int main(int argc, char** argv) {
     vars = {"read", "write", "copy", "copy_ilp1", "copy_ilp8", "copy_nt", "copy_ntl", "copy_g4",
             "copy_g16", "copy_g32", "copy_wave4k", "memcpy", "copy_small", "read", "copy"};
   const u64 N = 4356833280ull;   // 2^20 x 4155 B, the 4k config's input
+  const u64 PPN = 2147479552ull; // pp_*: 2 GiB - 4 KiB (32-bit buffer offsets), same pattern
   uint8_t *a, *b;
   u32* o;
   CHECK(hipMalloc(&a, N));
   CHECK(hipMalloc(&b, N));
-  CHECK(hipMalloc(&o, 4));
+  CHECK(hipMalloc(&o, 4096));
   CHECK(hipMemset(a, 0x5A, N));
   CHECK(hipMemset(b, 0, N));
   hipDeviceProp_t prop;
@@ -164,16 +314,39 @@ int main(int argc, char** argv) {
       else if (v == "copy_flat") copy_flat_k<1, false><<<(u32)((n16 + 255) / 256), 256>>>(s, d, n16);
       else if (v == "copy_flat4") copy_flat_k<4, false><<<(u32)((n16 + 1023) / 1024), 256>>>(s, d, n16);
       else if (v == "copy_flat_nt") copy_flat_k<1, true><<<(u32)((n16 + 255) / 256), 256>>>(s, d, n16);
+      else if (v == "p_rows") persist_k<0><<<cus, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_rows8") persist_k<0><<<cus, 512>>>(s, d, N / 4096, o);
+      else if (v == "p_rows32") persist_k<0><<<cus * 2, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_contig") persist_k<1><<<cus, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_dyn") persist_k<2><<<cus, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_dyn32") persist_k<2><<<cus * 2, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_dyn4") persist_k<3><<<cus, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_xcd") persist_k<4><<<cus, 1024>>>(s, d, N / 4096, o);
+      else if (v == "p_semi4") persist_k<5><<<(u32)(N / 4096 / 64), 1024>>>(s, d, N / 4096, o, 4);
+      else if (v == "p_semi16") persist_k<5><<<(u32)(N / 4096 / 256), 1024>>>(s, d, N / 4096, o, 16);
+      else if (v == "p_semi64") persist_k<5><<<(u32)(N / 4096 / 1024), 1024>>>(s, d, N / 4096, o, 64);
+      else if (v == "p_semi16_256") persist_k<5><<<(u32)(N / 4096 / 64), 256>>>(s, d, N / 4096, o, 16);
+      else if (v == "p_rows_256x4") persist_k<0><<<cus * 4, 256>>>(s, d, N / 4096, o);
+      else if (v == "p_rows2") rows2_k<false><<<cus, 1024>>>(s, d, N / 4096);
+      else if (v == "p_rows2s") rows2_k<true><<<cus, 1024>>>(s, d, N / 4096);
+      else if (v == "p_rows2_8") rows2_k<false><<<cus, 512>>>(s, d, N / 4096);
+      else if (v == "pp") pp_k<<<cus, 1024>>>(a, b, PPN / 4096);
+      else if (v == "pp8") pp_k<<<cus, 512>>>(a, b, PPN / 4096);
+      else if (v == "pp32") pp_k<<<cus * 2, 1024>>>(a, b, PPN / 4096);
+      else if (v == "pp_flat") flat_w4k_k<<<(u32)(PPN / 4096 / 4), 256>>>(s, d, PPN / 4096);
+      else if (v == "flat_w4k") flat_w4k_k<<<(u32)(N / 4096 / 4), 256>>>(s, d, N / 4096);
       else if (v == "memcpy") (void)hipMemcpyAsync(b, a, N, hipMemcpyDeviceToDevice, 0);
       else if (v == "copy_small") copy_k<4, false, false><<<cus * 8, 256>>>(s, d, small16);
     };
     if (v == "read" || v == "write") moved = (double)N;
+    if (v.rfind("pp", 0) == 0) moved = 2.0 * PPN;
     if (v == "copy_small") moved = 2.0 * (128ull << 20);
-    for (int w = 0; w < 3; w++) launch();
+    for (int w = 0; w < 3; w++) { CHECK(hipMemsetAsync(o, 0, 4096)); launch(); }
     CHECK(hipDeviceSynchronize());
     const int reps = 15;
     std::vector<float> ms;
     for (int r = 0; r < reps; r++) {
+      CHECK(hipMemsetAsync(o, 0, 4096));
       CHECK(hipEventRecord(e0));
       launch();
       CHECK(hipEventRecord(e1));

@@ -654,6 +654,7 @@ struct Src16 {
 // Slotted layout: chunk c of the block's stream goes to slot + 16 c; chunks up to npad (the
 // 128-byte line) are written, bytes past the stream (tot) zeroed.
 struct SlotDst {
+  static constexpr bool kFlat = false;
   uint8_t* p;
   u32 npad, tot;
   __device__ __forceinline__ void put(u32 c, uint4 acc, bool act) const {
@@ -738,6 +739,7 @@ __device__ __forceinline__ u32 stream_vstart(u32 K, u32 dk, u32 dv) {
 }
 // The flat destination's put as a copy_window destination (every active chunk stored).
 struct FlatDst {
+  static constexpr bool kFlat = true;
   const FlatOut* d;
   __device__ __forceinline__ void put(u32 c, uint4 acc, bool act) const { d->put(c, acc, !act); }
 };
@@ -782,7 +784,9 @@ __device__ __forceinline__ u32 copy_window(const S& src, const Col& col, const M
   if (cross) nx = src((int)x0 + d1);
   if (__ballot(act && e0 <= x0)) {
     // a lost map race (two entries ended in one chunk): walk forward to the holding entry
-    while (act && e0 <= x0 && j < last) {   // (bounded: the last segment holds the stream's end)
+    // (flat: bounded by the last segment, which a trailing chunk of the virtual stream may lie
+    // past; in the slotted stream the last segment holds the stream's end)
+    while (act && e0 <= x0 && (!D::kFlat || j < last)) {
       j++;
       col.get2(min(j, last), e0, d0, e1, d1);
     }
@@ -1457,23 +1461,27 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     return uni(q);
   };
-  u64 gs_cur, ge_cur, gs_nxt, ge_nxt;
-  auto load_group = [&](u32 q, u64& gs, u64& ge) {
+  // Lane l <= kChunk holds ext[first + l]: block j of the chunk spans lanes j and j + 1 (one
+  // u64 per lane per chunk in flight; two extents per lane cost the loop VGPRs it spilled)
+  u64 gs_cur, gs_nxt;
+  auto load_group = [&](u32 q, u64& gs) {
     // lanes past the chunk or the batch re-read an extent (unconditional: the loads write their
     // destination registers directly, nothing waits for them until the chunk is used)
-    u32 bb = chunk_first(q) + (lane < kChunk ? lane : 0u);
-    bb = bb < p.n_blocks ? bb : p.n_blocks - 1;
 #ifdef TPZ_ABL_ONCHIP
-    bb &= kOnchipMask;   // timing build: the same 4096 blocks over and over (L2/MALL-resident)
+    // timing build: the same 4096 blocks over and over (L2/MALL-resident; chunks tile 4096)
+    u32 bb = (chunk_first(q) & kOnchipMask) + (lane <= kChunk ? lane : 0u);
+#else
+    u32 bb = chunk_first(q) + (lane <= kChunk ? lane : 0u);
 #endif
+    bb = bb < p.n_blocks ? bb : p.n_blocks;
     gs = p.ext[bb];
-    ge = p.ext[bb + 1];
   };
   auto lane64 = [](u64 x, u32 l) { return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l); };
   // Blocks that do not fit a wave slot are sent to their worklist when their chunk becomes
   // current: fewer than 64 entries -> the one-wave-per-block kernel, past the big path's window
   // -> the spill path, else the LDS big path. The decode loop then skips them.
-  auto triage_group = [&](u32 q, u64 gs, u64 ge) {
+  auto triage_group = [&](u32 q, u64 gs) {
+    const u64 ge = ((u64)__shfl_down((u32)(gs >> 32), 1) << 32) | __shfl_down((u32)gs, 1);
     const u32 cf = chunk_first(q), bb = cf + lane;     // (lane < n_blocks - cf: no wrap)
     const bool lng = lane < kChunk && lane < p.n_blocks - cf && ge - gs > kWaveMaxLen;
     if (!__ballot(lng)) return;
@@ -1487,9 +1495,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
   u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
-  load_group(q_cur, gs_cur, ge_cur);
-  load_group(q_nxt, gs_nxt, ge_nxt);
-  triage_group(q_cur, gs_cur, ge_cur);
+  load_group(q_cur, gs_cur);
+  load_group(q_nxt, gs_nxt);
+  triage_group(q_cur, gs_cur);
   u32 j = 0;                              // the block's position in its chunk
   u32 b = chunk_first(q_cur);
 
@@ -1499,7 +1507,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   auto issue = [&](u32 bb, u32 jj, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
     s = lane64(gs_cur, jj);
-    e = lane64(ge_cur, jj);
+    e = lane64(gs_cur, jj + 1);
     const u64 len = e - s;
     if (len > kWaveMaxLen) return;
     const u64 ws = s & ~15ull;
@@ -1550,10 +1558,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       j = 0;
       q_cur = q_nxt;
       gs_cur = gs_nxt;
-      ge_cur = ge_nxt;
       q_nxt = claim_chunk();
-      load_group(q_nxt, gs_nxt, ge_nxt);
-      triage_group(q_cur, gs_cur, ge_cur);
+      load_group(q_nxt, gs_nxt);
+      triage_group(q_cur, gs_cur);
     }
     b = chunk_first(q_cur) + j;
     b = b < p.n_blocks ? b : p.n_blocks;
