@@ -5,7 +5,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ONLY4K="--no-side-configs --config5-gib 0 --no-exact --no-encode"   # the headline decode alone
+ONLY4K="--no-side-configs --config5-gib 0 --no-exact --no-encode --no-flat"   # the headline decode alone
 B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-validate --no-snappy --no-lz4 --no-file-crc --no-seek $ONLY4K"
 # the trace pass runs 40 timed steps so that the first (slower, clock ramp-up) dispatches do not
 # skew the average the bench line is compared with

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 closing run (GPU box): the GPU test suite, smoke, the full bench line, then the
-# rocprofv3 kernel trace and PMC passes of profiles/run_profiles.sh (summaries copied into
-# profiles/r4/ on the CPU side with profiles/summarize.py).
+# rocprofv3 kernel trace and PMC passes of profiles/run_profiles.sh (summarized on the box by
+# profiles/summarize.py into gpurun_out/r4final/profiles_r4, copied to profiles/r4/ here).
 set -o pipefail
 OUT=gpurun_out/r4final
 mkdir -p $OUT; export TMPDIR=/tmp
@@ -11,5 +11,8 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smo
 tail -1 $OUT/smoke.log
 timeout -k 10 900 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['value'], d['roofline'])"
-timeout -k 10 1200 bash profiles/run_profiles.sh $OUT/prof > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+# raw profiler output stays on the box (/tmp); only the summaries come back
+timeout -k 10 1200 bash profiles/run_profiles.sh /tmp/r4prof > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+python3 profiles/summarize.py /tmp/r4prof $OUT/profiles_r4 > $OUT/summarize.log 2>&1 || { tail -20 $OUT/summarize.log; exit 1; }
+cp /tmp/r4prof/trace.log /tmp/r4prof/trace_codecs.log $OUT/profiles_r4/ 2>/dev/null
 echo profiles done
