@@ -110,6 +110,10 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks.restype = C.c_int
         L.tpz_decode_check.argtypes = [C.c_void_p, C.c_void_p]
         L.tpz_decode_check.restype = C.c_int
+        # diagnostic (not in tpz_gpu.h): bench.py's flat copy probe for roofline.copy_ceiling
+        if hasattr(L, "tpz_debug_copy"):   # (diagnostic builds from older trees lack it)
+            L.tpz_debug_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
+            L.tpz_debug_copy.restype = C.c_int
         for f in ("tpz_crc32_ranges",):
             getattr(L, f).argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
             getattr(L, f).restype = C.c_int

@@ -337,28 +337,6 @@ struct Lz4LaneSrc {
     return (u32)(cv >> (8 * (a - cpos))) & 0xFFu;
   }
 };
-// The sizes pass's source: a 64-byte window (four 16-byte loads issued together), so that a
-// literal of up to ~48 bytes is skipped without a new dependent load (the walk's chain of loads
-// is what the pass waits on: one thread per block).
-struct Lz4WideSrc {
-  const uint8_t* src;
-  u64 src_bytes, base;
-  mutable u64 cpos;             // 16-aligned start of the window
-  mutable u128 c0, c1, c2, c3;
-  __device__ u32 byte(int64_t i) const {
-    const u64 a = base + (u64)i;
-    if (a - cpos >= 64) {
-      cpos = a & ~15ull;
-      c0 = ld16c(src, src_bytes, cpos);
-      c1 = ld16c(src, src_bytes, cpos + 16);
-      c2 = ld16c(src, src_bytes, cpos + 32);
-      c3 = ld16c(src, src_bytes, cpos + 48);
-    }
-    const u32 d = (u32)(a - cpos);
-    const u128 v = d < 32 ? (d < 16 ? c0 : c1) : (d < 48 ? c2 : c3);
-    return (u32)(v >> (8 * (d & 15))) & 0xFFu;
-  }
-};
 template <class Src, class Out>
 __device__ int64_t lz4_walk(const Src& in, int64_t iend, const Out& out, int64_t oend) {
   if (oend == 0) return (iend == 1 && in.byte(0) == 0) ? 0 : -1;
@@ -570,8 +548,7 @@ struct Lz4GlobalOut {            // wave-wide copies into global memory
 __device__ __forceinline__ int64_t lz4_block_length(const uint8_t* src, u64 src_bytes, u64 s, u64 len) {
   const int64_t size = lz4_prefix(src + s, len - 1);
   if (size < 0) return -1;
-  return lz4_walk(Lz4WideSrc{src, src_bytes, s + 4, (s + 4 - (1ull << 62)) & ~15ull, 0, 0, 0, 0},
-                  (int64_t)len - 5, Lz4NoOut{}, size);
+  return lz4_walk(Lz4LaneSrc{src, src_bytes, s + 4, s + 4 - (1ull << 62), 0}, (int64_t)len - 5, Lz4NoOut{}, size);
 }
 
 __device__ __forceinline__ int64_t lz4_block_length_bytes(const uint8_t* blk, u64 len) {

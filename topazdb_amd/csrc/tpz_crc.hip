@@ -318,3 +318,27 @@ void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream) {
 }
 
 }  // namespace tpz
+
+// ------------------------------------------------------------------ copy probe (diagnostic)
+// The box's HBM copy rate for bench.py's roofline.copy_ceiling: one 16-byte piece per thread and
+// a grid covering the buffer (each wave loads, stores and ends; MI355X_MICROARCH.md's 6.3 TB/s
+// float4 copy). Persistent or grid-stride copies wait on their own store acknowledgements (the
+// next load's vmcnt counts the stores issued before it) and run at 4.3-4.8 TB/s
+// (tools/ubench_bw.hip), so they understate the ceiling.
+namespace {
+__global__ __launch_bounds__(256) void copy_probe_kernel(const uint4* __restrict__ s, uint4* __restrict__ d,
+                                                         unsigned long long n16) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) d[i] = s[i];
+}
+}  // namespace
+extern "C" int tpz_debug_copy(void* dst, const void* src, unsigned long long bytes, void* stream) {
+  const unsigned long long n16 = bytes / 16;
+  if (!n16) return 0;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u) return -1;
+  const unsigned long long grid = (n16 + 255) / 256;
+  if (grid > 0x7FFFFFFFull) return -1;
+  hipLaunchKernelGGL(copy_probe_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

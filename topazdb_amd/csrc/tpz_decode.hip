@@ -672,20 +672,29 @@ struct SlotDst {
 // Bytes [lo, hi) of the 16-byte chunk v to p[lo .. hi) (p 16-aligned), in naturally aligned
 // pieces: the bytes around them belong to the neighbouring block's keys or values, which
 // another wave writes.
-__device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, u32 lo, u32 hi) {
+__device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t r, u32 base, uint4 v, u32 lo,
+                                              u32 hi) {
   const u64 q0 = (u64)v.y << 32 | v.x, q1 = (u64)v.w << 32 | v.z;
   auto bytes = [&](u32 a) -> u64 {   // the 8 bytes from a (a < 16)
     return a == 0 ? q0 : a >= 8 ? (q1 >> (8 * (a - 8))) : ((q0 >> (8 * a)) | (q1 << (64 - 8 * a)));
   };
+  auto st = [&](u32 a, u32 w) {      // w bytes (1, 2, 4 or 8) from a, naturally aligned
+    const u64 x = bytes(a);
+    if (w == 1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)x, r, base + a, 0, 0);
+    else if (w == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)x, r, base + a, 0, 0);
+    else if (w == 4) __builtin_amdgcn_raw_buffer_store_b32((u32)x, r, base + a, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32, x), r, base + a, 0, 0);
+  };
   u32 a = lo;
-  if ((a & 1u) && a + 1 <= hi) { p[a] = (uint8_t)bytes(a); a += 1; }
-  if ((a & 2u) && a + 2 <= hi) { *reinterpret_cast<uint16_t*>(p + a) = (uint16_t)bytes(a); a += 2; }
-  if ((a & 4u) && a + 4 <= hi) { *reinterpret_cast<u32*>(p + a) = (u32)bytes(a); a += 4; }
-  if ((a & 8u) && a + 8 <= hi) { *reinterpret_cast<u64*>(p + a) = bytes(a); a += 8; }
-  if (a + 8 <= hi) { *reinterpret_cast<u64*>(p + a) = bytes(a); a += 8; }
-  if (a + 4 <= hi) { *reinterpret_cast<u32*>(p + a) = (u32)bytes(a); a += 4; }
-  if (a + 2 <= hi) { *reinterpret_cast<uint16_t*>(p + a) = (uint16_t)bytes(a); a += 2; }
-  if (a + 1 <= hi) p[a] = (uint8_t)bytes(a);
+  if ((a & 1u) && a + 1 <= hi) { st(a, 1); a += 1; }
+  if ((a & 2u) && a + 2 <= hi) { st(a, 2); a += 2; }
+  if ((a & 4u) && a + 4 <= hi) { st(a, 4); a += 4; }
+  if ((a & 8u) && a + 8 <= hi) { st(a, 8); a += 8; }
+  if (a + 8 <= hi) { st(a, 8); a += 8; }
+  if (a + 4 <= hi) { st(a, 4); a += 4; }
+  if (a + 2 <= hi) { st(a, 2); a += 2; }
+  if (a + 1 <= hi) st(a, 1);
 }
 
 // Flat layout: the block's keys go to keys[kf ..] and its values to vals[vf ..], back to back
@@ -696,39 +705,43 @@ __device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, u32 lo, u32 h
 // are stored piecewise (store_partial). The stores go through two descriptors that end at the
 // block's last key / value chunk.
 struct FlatOut {
-  __amdgpu_buffer_rsrc_t rk, rv;   // from the key / value chunk base, 16 kch / 16 vch bytes
-  uint8_t* kb;                     // the 16-aligned key / value chunk bases
-  uint8_t* vb;
-  u32 kch, vch;                    // chunks of each column
-  u32 klo, khi, vlo, vhi;          // valid bytes [lo, hi) of the first / last chunk
+  __amdgpu_buffer_rsrc_t rk, rv;   // from the 16-aligned key / value chunk base, 16 kch / 16 vch bytes
+  u32 ch;                          // kch | vch << 16: the chunks of each column
+  u32 lohi;                        // klo | khi << 8 | vlo << 16 | vhi << 24: the valid bytes
+                                   // [lo, hi) of a column's first / last chunk
   __device__ __forceinline__ void put(u32 c, uint4 acc, bool skip) const {
+    const u32 kch = ch & 0xFFFFu, vch = ch >> 16;
     const bool isk = c < kch;
     const u32 jv = c - kch;
     const bool isv = !isk && jv < vch;
-    const u32 lo = isk ? (c == 0 ? klo : 0u) : (jv == 0 ? vlo : 0u);
-    const u32 hi = isk ? (c + 1 == kch ? khi : 16u) : (jv + 1 == vch ? vhi : 16u);
+    const u32 first = isk ? (c == 0) : (jv == 0), last = isk ? (c + 1 == kch) : (jv + 1 == vch);
+    const u32 sh = isk ? 0u : 16u;   // this column's byte pair in lohi
+    const u32 lo = first ? (lohi >> sh) & 0xFFu : 0u;
+    const u32 hi = last ? (lohi >> (sh + 8)) & 0xFFu : 16u;
     const bool full = lo == 0 && hi == 16;
     const auto v4 = __builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc);
     __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (!skip && isk && full) ? 16 * c : kOob, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (!skip && isv && full) ? 16 * jv : kOob, 0, 0);
     const bool part = !skip && (isk || isv) && !full;
-    if (__ballot(part) && part) store_partial(isk ? kb + 16 * c : vb + 16 * jv, acc, lo, hi);
+    // (one copy of the byte-store cascade for both columns: the descriptor is wave-uniform)
+#pragma unroll 1
+    for (u32 col = 0; col < 2; col++) {
+      const bool mine = part && (col ? isv : isk);
+      if (__ballot(mine) && mine) store_partial(col ? rv : rk, 16 * (col ? jv : c), acc, lo, hi);
+    }
   }
 };
 // The flat destination of block b with K key and V value bytes (dk / dv: its column starts mod 16).
 __device__ __forceinline__ FlatOut flat_out(const Out& o, u64 kf, u64 vf, u32 K, u32 V) {
   FlatOut D;
   const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
-  D.kch = K ? (dk + K + 15) >> 4 : 0u;
-  D.vch = V ? (dv + V + 15) >> 4 : 0u;
-  D.kb = o.keys + (kf & ~15ull);
-  D.vb = o.vals + (vf & ~15ull);
-  D.rk = __builtin_amdgcn_make_buffer_rsrc(D.kb, (short)0, (int)(16 * D.kch), 0x00020000);
-  D.rv = __builtin_amdgcn_make_buffer_rsrc(D.vb, (short)0, (int)(16 * D.vch), 0x00020000);
-  D.klo = dk;
-  D.khi = dk + K - 16 * (D.kch ? D.kch - 1 : 0u);
-  D.vlo = dv;
-  D.vhi = dv + V - 16 * (D.vch ? D.vch - 1 : 0u);
+  const u32 kch = K ? (dk + K + 15) >> 4 : 0u;
+  const u32 vch = V ? (dv + V + 15) >> 4 : 0u;
+  D.ch = kch | vch << 16;
+  D.rk = __builtin_amdgcn_make_buffer_rsrc(o.keys + (kf & ~15ull), (short)0, (int)(16 * kch), 0x00020000);
+  D.rv = __builtin_amdgcn_make_buffer_rsrc(o.vals + (vf & ~15ull), (short)0, (int)(16 * vch), 0x00020000);
+  const u32 khi = dk + K - 16 * (kch ? kch - 1 : 0u), vhi = dv + V - 16 * (vch ? vch - 1 : 0u);
+  D.lohi = dk | khi << 8 | dv << 16 | vhi << 24;
   return D;
 }
 // Where the virtual stream's values start: the key chunks, then dv (flat); value_start(K)
@@ -1100,15 +1113,16 @@ __device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, Pen
 template <class Col, class MapT, int kMapLen, bool BIG, bool FLAT = false>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
-                                             const Out& o, u32 kshift, Stamps& S, PendingCrc& pd) {
+                                             const Out& o, u32 kshift, Stamps& S, PendingCrc& pd,
+                                             u64 kf = 0, u64 vf = 0) {
   const u32 lane = lane_id();
   // the header reads are issued together (one LDS round trip); the checks keep the reference's
   // order
   const u32 tag = win[(int)(a0 + len) - 1];                                    // compress.rs:99
   const u32 stored = bswap32(lds_u32(win, len >= 5 ? a0 + len - 5 : a0));      // block.rs:51
   const u32 n = lds_be16(win, a0);                                             // block.rs:54
-  // flat layout: the block's first key / value byte in the columns (tpz_flat_layout)
-  const u64 kf = FLAT ? o.kfirst[b] : 0ull, vf = FLAT ? o.vfirst[b] : 0ull;
+  // flat layout: kf / vf = the block's first key / value byte in the columns (tpz_flat_layout;
+  // loaded by the caller with the block's prefetch)
   const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
   finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
@@ -1504,8 +1518,13 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // prefetch state for block b
   uint4 v[kWinRounds];
   u64 s_cur = 0, e_cur = 0;
+  u64 kf_cur = 0, vf_cur = 0;     // flat: the block's column starts, loaded one block ahead
   auto issue = [&](u32 bb, u32 jj, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
+    if (FLAT) {
+      kf_cur = p.out.kfirst[bb];
+      vf_cur = p.out.vfirst[bb];
+    }
     s = lane64(gs_cur, jj);
     e = lane64(gs_cur, jj + 1);
     const u64 len = e - s;
@@ -1539,6 +1558,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 
   while (b < p.n_blocks) {
     const u64 s = s_cur, e = e_cur;
+    const u64 kf = kf_cur, vf = vf_cur;
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
     const bool fits = (e - s) <= kWaveMaxLen;
     if (fits) {
@@ -1575,7 +1595,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       const u32 bdec = bcur;
 #endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false, FLAT>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bdec, s, p.out, kshift, S, pd);
+                                                           len64, bdec, s, p.out, kshift, S, pd, kf, vf);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
