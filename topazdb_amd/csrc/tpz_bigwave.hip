@@ -68,8 +68,12 @@ constexpr int kLdsBytes = kCrcRepWords * 4 + kWaves * kWaveLds + kShiftWords * 4
 static_assert(kLdsBytes <= 163840, "bigwave LDS");
 constexpr u32 kOob = 0x80000000u;
 
+// The lane id, laundered: masks and offsets derived from it are recomputed where they are used
+// instead of being hoisted out of the block loop into SGPR pairs that spill (tpz_decode.hip).
 __device__ __forceinline__ u32 lane_id() {
-  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  u32 l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
 }
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ u32 readlane(u32 x, u32 l) { return __builtin_amdgcn_readlane(x, l); }
@@ -493,8 +497,18 @@ __device__ __forceinline__ u32 fused_crc_fold(const FusedCrc& c, const BWParams&
 // waves claim them one at a time from an LDS counter (*pool, starting at lo), so a CU's faster
 // waves take more blocks (its waves do not run at one speed: tpz_decode.hip decode_wave_kernel).
 // Returns the blocks the wave decoded.
+// rare: the worklist pointers (spill list / count, big list / count) from LDS, read only on the
+// paths that append to them; as kernel arguments they were hoisted into SGPRs kept live across
+// the block loop (at its SGPR limit: the spills went to VGPR lanes).
+typedef __attribute__((address_space(1))) u32 gu32;
+__device__ __forceinline__ void append(u32* const* rare, int k, u32 b) {
+  if (lane_id() == 0) {
+    gu32* l = (gu32*)rare[k];
+    l[__hip_atomic_fetch_add((gu32*)rare[k + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = b;
+  }
+}
 __device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u32 lo, u32 cnt,
-                                             u32* pool) {
+                                             u32* pool, u32* const* rare) {
   u32* rep = reinterpret_cast<u32*>(lds);
   for (int i = threadIdx.x; i < kCrcRepWords / 4; i += kThreads)
     reinterpret_cast<uint4*>(rep)[i] = reinterpret_cast<const uint4*>(p.rep)[i];
@@ -551,7 +565,7 @@ __device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u3
       const u32 w0 = readlane(hw, 0);
       const u32 n = ((w0 & 0xFFu) << 8) | ((w0 >> 8) & 0xFFu);                  // block.rs:54
       if (n >= kWave) {                     // (the wave path routes only n < 64 here)
-        if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
+        append(rare, 2, b);
         return;
       }
       u32 st = TPZ_BLOCK_OK, bcnt = n;
@@ -587,7 +601,7 @@ __device__ __forceinline__ u32 bigwave_phase(const BWParams& p, uint8_t* lds, u3
         if (bad || !slots_fit || (u64)vs + vtot > (u64)len + 2) {
           // entries out of range (TPZ_BLOCK_BAD_ENTRY), or entries that overlap or repeat: the
           // spill path decodes the block (CRC included)
-          if (lane == 0) p.spill_list[atomicAdd(p.spill_count, 1u)] = b;
+          append(rare, 0, b);
           return;
         } else {
           BW_ST(0);
@@ -777,13 +791,20 @@ static BWParams bigwave_params(const BigWaveLaunch& a) {
 __global__ __launch_bounds__(kThreads, 1) void decode_bigwave_kernel(BWParams p, u32* ctr) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   __shared__ u32 pool;
+  __shared__ u32* rare[4];
   const u32 na = uni(tail_load(ctr + kTailBw));
   // this workgroup's share of the list: entries [lo, hi)
   const u32 per = (na + gridDim.x - 1) / gridDim.x, lo = blockIdx.x * per;
   const u32 hi = lo + per < na ? lo + per : na;
   if (lo >= hi) return;                              // an empty list costs one load
-  if (threadIdx.x == 0) pool = lo;                   // (the table upload's barrier publishes it)
-  bigwave_phase(p, lds, lo, hi, &pool);
+  if (threadIdx.x == 0) {                            // (the table upload's barrier publishes them)
+    pool = lo;
+    rare[0] = p.spill_list;
+    rare[1] = p.spill_count;
+    rare[2] = p.big_list;
+    rare[3] = p.big_count;
+  }
+  bigwave_phase(p, lds, lo, hi, &pool, rare);
 }
 
 }  // namespace bw

@@ -137,7 +137,14 @@ static_assert((kTableBytes + kGuard + kBigWinBytes + 32 + kBigMapLen * 2 + kBigM
                kBigWaves * 4) % 8 == 0, "big path entry table alignment");
 
 // ------------------------------------------------------------------ small helpers
-__device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// The lane id, laundered: masks and offsets derived from it are recomputed where they are used
+// (one or two VALU) instead of being hoisted out of the block loop into SGPR pairs, which spill
+// (the loop is at its SGPR and VGPR limits).
+__device__ __forceinline__ u32 lane_id() {
+  u32 l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ u64 uni64(u64 x) {
   u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
@@ -301,7 +308,10 @@ __device__ __forceinline__ uint4 zero_head(uint4 v, u32 k) {
 // with every level) and DPP hands it to lane l - 2^k, which XORs it in. Rows of 16 lanes finish
 // in lanes 0, 16, 32, 48; those are shifted by 1280 / 2560 B and read out.
 __device__ __forceinline__ u32 crc_combine(const u32* tab, u32 A) {
-  const u32 lane = lane_id();
+  // (the lane id is laundered so that the six lane masks are recomputed here, one v_cmp each,
+  // instead of being hoisted out of the block loop into SGPR pairs that spill)
+  u32 lane = lane_id();
+  asm volatile("" : "+v"(lane));
   if ((lane & 1u) == 1u) A = crc_shift<0>(tab, A);
   A ^= dpp<kRowShl + 1>(A);
   if ((lane & 3u) == 2u) A = crc_shift<1>(tab, A);
@@ -576,9 +586,18 @@ struct Out {
   const u64* vfirst;
 };
 
+// The worklist pointers (rare paths) are read from a copy of the Out struct in LDS (wave path):
+// kept as kernel arguments, the compiler hoists them out of the block loop into SGPRs that stay
+// live across it, and the loop is at its SGPR limit (spilled SGPRs go to VGPR lanes, and the
+// VGPRs are at their limit too). LDS loads are not hoisted past the loop's LDS stores.
 // Lane 0 appends block b to a worklist (the big path's or the spill path's).
+// (the lists are global memory: a pointer read from the LDS copy is generic, and flat atomics
+// and stores would count in lgkmcnt too)
+typedef __attribute__((address_space(1))) u32 gu32;
 __device__ __forceinline__ void defer_to(u32* list, u32* count, u32 b) {
-  if (lane_id() == 0) list[atomicAdd(count, 1u)] = b;
+  gu32* l = (gu32*)list;
+  gu32* c = (gu32*)count;
+  if (lane_id() == 0) l[__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = b;
 }
 
 // The lanes in `take` append their block bb to a worklist with one atomic per wave (a
@@ -588,9 +607,12 @@ __device__ __forceinline__ void defer_lanes(u32* list, u32* count, bool take, u3
   const u64 m = __ballot(take);
   if (!m) return;
   u32 base = 0;
-  if (lane_id() == (u32)__builtin_ctzll(m)) base = atomicAdd(count, (u32)__builtin_popcountll(m));
+  gu32* l = (gu32*)list;
+  gu32* c = (gu32*)count;
+  if (lane_id() == (u32)__builtin_ctzll(m))
+    base = __hip_atomic_fetch_add(c, (u32)__builtin_popcountll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   base = __builtin_amdgcn_readlane(base, __builtin_ctzll(m));
-  if (take) list[base + __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u))] = bb;
+  if (take) l[base + __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u))] = bb;
 }
 
 // Lane 0 stores block b's status, count and crc. Every lane issues the three buffer stores
@@ -1114,7 +1136,7 @@ template <class Col, class MapT, int kMapLen, bool BIG, bool FLAT = false>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
                                              const Out& o, u32 kshift, Stamps& S, PendingCrc& pd,
-                                             u64 kf = 0, u64 vf = 0) {
+                                             u64 kf = 0, u64 vf = 0, const Out* o_lds = nullptr) {
   const u32 lane = lane_id();
   // the header reads are issued together (one LDS round trip); the checks keep the reference's
   // order
@@ -1124,6 +1146,17 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   // flat layout: kf / vf = the block's first key / value byte in the columns (tpz_flat_layout;
   // loaded by the caller with the block's prefetch)
   const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
+  // The parse's first round reads (lane i: entry i's offset, then its key length) are issued
+  // before the previous block's combine, so their two dependent LDS round trips overlap its six.
+  // The offset is read with the header (speculatively: lanes past n discard it).
+  u32 e_off = 0, e_kl = 0;
+  bool e_ok = false;
+  if (!BIG) {
+    e_off = lds_be16(win, a0 + 2 + 2 * lane);
+    const u32 Pn = len - 5, db0 = a0 + 2 + 2 * n;
+    e_ok = len >= 7 && lane < n && Pn >= 2 + 2 * n && e_off + 2 <= Pn - 2 - 2 * n;
+    e_kl = lds_be16(win, e_ok ? db0 + e_off : a0);
+  }
   finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
@@ -1146,8 +1179,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     cnt = 0;
   } else if (!BIG && n > kWaveMaxN) {
     // the LDS big path (slotted); the spill path writes the flat columns directly
-    if (FLAT) defer_to(o.spill_list, o.spill_count, b);
-    else defer_to(o.defer_list, o.defer_count, b);
+    const Out& oc = o_lds ? *o_lds : o;
+    if (FLAT) defer_to(oc.spill_list, oc.spill_count, b);
+    else defer_to(oc.defer_list, oc.defer_count, b);
     return;
   } else {
     const u32 db = a0 + 2 + 2 * n;   // entries region (Block.data), LDS offset
@@ -1192,9 +1226,15 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       u32 off = 0, kl = 0, vl = 0;
       bool ok = true;
       if (act) {
-        off = lds_be16(win, a0 + 2 + 2 * i);                                      // iterator.rs:74
-        ok = off + 2 <= dl;
-        if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }        // :77-81
+        if (!BIG && g0 == 0) {          // (read before the combine: e_ok = act && off + 2 <= dl)
+          off = e_off;
+          ok = e_ok;
+          if (ok) { kl = e_kl; ok = off + 4 + kl <= dl; }
+        } else {
+          off = lds_be16(win, a0 + 2 + 2 * i);                                    // iterator.rs:74
+          ok = off + 2 <= dl;
+          if (ok) { kl = lds_be16(win, db + off); ok = off + 4 + kl <= dl; }      // :77-81
+        }
         if (ok) { vl = lds_be16(win, db + off + 2 + kl); ok = off + 4 + kl + vl <= dl; } // :81-82
         if (!ok) kl = vl = 0;
       }
@@ -1241,7 +1281,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     if (bad || !slots_fit || vs + vc > len + (FLAT ? 47u : 2u)) {
       // entries out of range (Ok(Block) with per-entry classes: TPZ_BLOCK_BAD_ENTRY), or
       // entries that overlap or repeat: the spill path decodes the block (CRC included)
-      defer_to(o.spill_list, o.spill_count, b);
+      const Out& oc = o_lds ? *o_lds : o;
+      defer_to(oc.spill_list, oc.spill_count, b);
       return;
     } else {
       if (BIG) {
@@ -1385,6 +1426,7 @@ struct Params {
   u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
 };
 
+
 // ------------------------------------------------------------------ wave path kernel
 #ifdef TPZ_ABL_ONCHIP
 // diagnostic (timing only): every wave decodes blocks 0..4095 over and over, so loads and stores
@@ -1400,7 +1442,11 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds) + kTabOff;   // (the layouts: kWaveTabWords)
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
-  if (threadIdx.x == 0) chunk_next = 0;   // (load_tables' barrier publishes it)
+  __shared__ Out out_lds;             // the worklist pointers for the rare paths (see above)
+  if (threadIdx.x == 0) {             // (load_tables' barrier publishes both)
+    chunk_next = 0;
+    out_lds = p.out;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1495,18 +1541,28 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // current: fewer than 64 entries -> the one-wave-per-block kernel, past the big path's window
   // -> the spill path, else the LDS big path. The decode loop then skips them.
   auto triage_group = [&](u32 q, u64 gs) {
-    const u64 ge = ((u64)__shfl_down((u32)(gs >> 32), 1) << 32) | __shfl_down((u32)gs, 1);
+    // lane l's block ends where lane l + 1's starts: a DPP row shift (no LDS), lane 15 from 16
+    // (a chunk is at most a row of 16 blocks)
+    // (no bound_ctrl: a lane whose source is outside its row keeps `old`, here lane 16's value,
+    // in one instruction. A select between a DPP and a readlane became a branch, and DPP reads
+    // of lanes the branch had switched off returned 0.)
+    const u32 glo = (u32)__builtin_amdgcn_update_dpp((int)readlane((u32)gs, 16), (int)(u32)gs,
+                                                     kRowShl + 1, 0xF, 0xF, false);
+    const u32 ghi = (u32)__builtin_amdgcn_update_dpp((int)readlane((u32)(gs >> 32), 16),
+                                                     (int)(u32)(gs >> 32), kRowShl + 1, 0xF, 0xF, false);
+    const u64 ge = ((u64)ghi << 32) | glo;
     const u32 cf = chunk_first(q), bb = cf + lane;     // (lane < n_blocks - cf: no wrap)
     const bool lng = lane < kChunk && lane < p.n_blocks - cf && ge - gs > kWaveMaxLen;
     if (!__ballot(lng)) return;
+    const Out& oc = out_lds;
     u32 nent = 0xFFFFu;
     if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
-    const bool to_bw = lng && nent < 64 && p.out.bw_list && ge - gs <= TPZ_BIGWAVE_BLOCK_BYTES;
+    const bool to_bw = lng && nent < 64 && oc.bw_list && ge - gs <= TPZ_BIGWAVE_BLOCK_BYTES;
     // (flat: every long block to the spill path, which writes the columns directly)
     const bool to_spill = lng && !to_bw && (FLAT || ge - gs > kBigMaxLen);
-    if (p.out.bw_list) defer_lanes(p.out.bw_list, p.out.bw_count, to_bw, (u32)bb);
-    defer_lanes(p.out.spill_list, p.out.spill_count, to_spill, (u32)bb);
-    defer_lanes(p.out.defer_list, p.out.defer_count, lng && !to_bw && !to_spill, (u32)bb);
+    if (oc.bw_list) defer_lanes(oc.bw_list, oc.bw_count, to_bw, (u32)bb);
+    defer_lanes(oc.spill_list, oc.spill_count, to_spill, (u32)bb);
+    defer_lanes(oc.defer_list, oc.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
   u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
   load_group(q_cur, gs_cur);
@@ -1595,7 +1651,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       const u32 bdec = bcur;
 #endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false, FLAT>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bdec, s, p.out, kshift, S, pd, kf, vf);
+                                                           len64, bdec, s, p.out, kshift, S, pd, kf, vf,
+                                                           &out_lds);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);

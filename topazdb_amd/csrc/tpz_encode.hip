@@ -68,7 +68,13 @@ constexpr int kBigSuper = (kBigWin + 5119) / 5120;   // CRC super-rounds
 static_assert(kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves <= 163840, "big encode LDS");
 
 // ------------------------------------------------------------------ small helpers
-__device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// The lane id, laundered: masks and offsets derived from it are recomputed where they are used
+// instead of being hoisted out of the block loop into SGPR pairs that spill (tpz_decode.hip).
+__device__ __forceinline__ u32 lane_id() {
+  u32 l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ u32 readlane(u32 x, int l) { return __builtin_amdgcn_readlane(x, l); }
 template <int CTRL>
