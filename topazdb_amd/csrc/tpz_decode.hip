@@ -742,10 +742,8 @@ struct FlatOut {
     const u32 hi = last ? (lohi >> (sh + 8)) & 0xFFu : 16u;
     const bool full = lo == 0 && hi == 16;
     const auto v4 = __builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc);
-    // (a window usually holds one column only: the other column's store is skipped, wave-uniform)
-    const bool wk = !skip && isk && full, wv = !skip && isv && full;
-    if (__ballot(wk)) __builtin_amdgcn_raw_buffer_store_b128(v4, rk, wk ? 16 * c : kOob, 0, 0);
-    if (__ballot(wv)) __builtin_amdgcn_raw_buffer_store_b128(v4, rv, wv ? 16 * jv : kOob, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (!skip && isk && full) ? 16 * c : kOob, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (!skip && isv && full) ? 16 * jv : kOob, 0, 0);
     const bool part = !skip && (isk || isv) && !full;
     // (one copy of the byte-store cascade for both columns: the descriptor is wave-uniform)
 #pragma unroll 1
