@@ -11,5 +11,7 @@ for c in ${CONFIGS:-4k zipf 64k}; do
   timeout -k 10 400 python3 tools/abl_multi.py --config $c $nb --rounds 5 --steps 10 $v > $OUT/abl_$c.jsonl 2>&1 || { tail $OUT/abl_$c.jsonl; exit 1; }
   echo "== $c"; grep variant $OUT/abl_$c.jsonl
 done
-timeout -k 10 400 python3 tools/enc_probe.py --steps 10 --rounds 5 full encprev > $OUT/enc.jsonl 2>&1 || { tail $OUT/enc.jsonl; exit 1; }
-echo "== encode"; grep -v amdgpu.ids $OUT/enc.jsonl
+if [ -f topazdb_amd/variants/libtpz_gpu_encprev.so ]; then
+  timeout -k 10 400 python3 tools/enc_probe.py --steps 10 --rounds 5 full encprev > $OUT/enc.jsonl 2>&1 || { tail $OUT/enc.jsonl; exit 1; }
+  echo "== encode"; grep -v amdgpu.ids $OUT/enc.jsonl
+fi

@@ -1039,8 +1039,9 @@ template <bool SHORT, bool FLAT, class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
-                                              u32 kshift, Stamps& St) {
-  constexpr bool short_segs = SHORT;
+                                              u32 kshift, Stamps& St, u32 w3 = 5) {
+  // SHORT: windows t < w3 can hold chunks that span three segments (copy_fast3); the others
+  // take copy_fast (a chunk it cannot do sends its window to copy_window, so either is exact)
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
@@ -1066,14 +1067,14 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   for (int t = 0; t < 4; t++) {
     cw[t] = carry;
     crc_step(tab, win, pb, L, t);
-    carry = short_segs ? copy_fast3<FLAT>(src, col, map, F, D, (u32)t, carry, rare)
-                       : copy_fast<FLAT>(src, col, map, F, D, (u32)t, carry, rare);
+    carry = (SHORT && (u32)t < w3) ? copy_fast3<FLAT>(src, col, map, F, D, (u32)t, carry, rare)
+                                   : copy_fast<FLAT>(src, col, map, F, D, (u32)t, carry, rare);
   }
   cw[4] = carry;
   crc_step(tab, win, pb, L, 4);
   if (nw > 4)
-    carry = short_segs ? copy_fast3<FLAT>(src, col, map, F, D, 4u, carry, rare)
-                       : copy_fast<FLAT>(src, col, map, F, D, 4u, carry, rare);
+    carry = (SHORT && 4u < w3) ? copy_fast3<FLAT>(src, col, map, F, D, 4u, carry, rare)
+                               : copy_fast<FLAT>(src, col, map, F, D, 4u, carry, rare);
   TPZ_STAMP(St, 4);
 #ifdef TPZ_ABL_STAMPS
   St.rare += __builtin_popcount(rare);
@@ -1171,6 +1172,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   u32 st = TPZ_BLOCK_OK, cnt = n;
   bool fuse = false;           // copy fused with the CRC (wave path)
   bool f_short = false;        // segments under 16 bytes (copy_fast3)
+  u32 f_w3 = 0;                // the leading windows that can hold them
   u32 f_nk = 0, f_tot = 0;
   uint8_t* f_dst = nullptr;
   FlatOut fo;                  // flat: the block's destination in the key / value columns
@@ -1219,7 +1221,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       }
     }
     u32 kc = 0, vc = 0, knz = 0, vnz = 0;
-    bool bad = false, short_segs = false;
+    bool bad = false, short_k = false, short_v = false;
     for (u32 g0 = 0; g0 < n; g0 += 64) {
       const u32 i = g0 + lane;
       const bool act = i < n;
@@ -1239,7 +1241,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         if (!ok) kl = vl = 0;
       }
       bad |= __ballot(act && !ok) != 0;
-      short_segs |= __ballot((kl != 0 && kl < 16) || (vl != 0 && vl < 16)) != 0;
+      short_k |= __ballot(kl != 0 && kl < 16) != 0;
+      short_v |= __ballot(vl != 0 && vl < 16) != 0;
       const u32 ki = wave_scan_incl(kl) + kc;
       const u32 vi = wave_scan_incl(vl) + vc;
       const u64 kmask = __ballot(kl != 0), vmask = __ballot(vl != 0);
@@ -1298,7 +1301,10 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 #if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY)
       if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
         fuse = true;
-        f_short = short_segs;
+        // short values: every window; short keys only: the windows of the key chunks (the
+        // values start on a chunk of their own)
+        f_w3 = short_v ? 5u : (short_k ? (((FLAT ? dk : 0u) + kc + 15) / 16 + 63) / 64 : 0u);
+        f_short = f_w3 != 0;
         f_nk = knz + vnz;
         f_tot = tot;
         f_dst = FLAT ? nullptr : o.data + slot_base(ext_b, b);
@@ -1338,7 +1344,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       const u32 lc = f_short
           ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
-                                       fo, win, pb, P + k, kshift, S)
+                                       fo, win, pb, P + k, kshift, S, f_w3)
           : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                         fo, win, pb, P + k, kshift, S);
