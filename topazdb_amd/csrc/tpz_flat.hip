@@ -14,10 +14,12 @@
 //   TPZ_BLOCK_BAD_ENTRY record, tpz_spill.hip parse).
 // The CRC is not checked here: a block that fails it keeps its reservation, unwritten.
 //
-// One wave per block, 16 per 1024-thread workgroup: the block is staged into the wave's LDS
-// window with coalesced 16-byte loads (the next block's loads in flight meanwhile), and lanes
-// parse 64 entries at a time from LDS. Reading every block whole moves the batch once: the
-// entry headers are spread over every 64-byte sector of a 4 KiB block anyway.
+// One wave per block (4-wave workgroups, a grid covering the batch): the block is staged into
+// the wave's LDS window with coalesced 16-byte loads, and lanes parse 64 entries at a time from
+// LDS. Reading every block whole moves the batch once: the entry headers are spread over every
+// 64-byte sector of a 4 KiB block anyway. (A persistent version, 16 waves per workgroup looping
+// over blocks with the next block's loads in flight, took 0.87-0.88 ms per 2^20 4 KiB blocks
+// against 0.73-0.74: profiles/r4/flat_layout.txt.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,7 +31,6 @@ namespace {
 typedef uint32_t u32;
 typedef uint64_t u64;
 
-constexpr int kFlWaves = 16;
 constexpr int kFlWin = 4352;                 // a0 (<= 15) + len <= kFlWin: staged
 constexpr u32 kFlMaxLen = kFlWin - 16;
 constexpr int kFlRounds = kFlWin / 1024 + 1;  // 5 x 1 KiB loads per wave
@@ -88,59 +89,41 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const uint8_t* src, u
   return __builtin_amdgcn_make_buffer_rsrc((void*)(src + start), (short)0, (int)rem, 0x00020000);
 }
 
-// first[0 .. nb) = n, first[st .. st + nb) = K, first[2 st .. 2 st + nb) = V of every block
-// (st = nb + 1); flat_scan_* turn them into exclusive prefixes in place.
-__global__ __launch_bounds__(1024) void flat_sizes_kernel(const uint8_t* src, const u64* ext,
+// One block per wave and no loop: 4-wave workgroups that exit after their blocks, a grid
+// covering the batch (a looping wave waits for its own stores' acknowledgements at every next
+// load, tools/ubench_bw.hip; the LDS per workgroup is 17 KiB, so up to 9 workgroups share a CU).
+constexpr int kFl1Waves = 4;
+__global__ __launch_bounds__(256) void flat_sizes1_kernel(const uint8_t* src, const u64* ext,
                                                           u64 src_bytes, u32 nb, u64* first) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kFlWaves * kFlWin];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kFl1Waves * kFlWin];
   const u32 lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* win = lds + wid * kFlWin;
   const u64 st = (u64)nb + 1;
-  const u32 nw = gridDim.x * kFlWaves;
-  u32 b = blockIdx.x * kFlWaves + wid;
-  uint4 v[kFlRounds];
-  u64 s = 0, e = 0;
-  auto issue = [&](u32 bb) {
-    if (bb >= nb) return;
-    s = ext[bb];
-    e = ext[bb + 1];
-    if (e < s || e - s > kFlMaxLen) return;
-    const u64 ws = s & ~15ull, e16 = (e + 15) & ~15ull;
-    const __amdgpu_buffer_rsrc_t rs = src_rsrc(src, src_bytes < e16 ? src_bytes : e16, ws);
+  const u32 b = blockIdx.x * kFl1Waves + wid;
+  if (b >= nb) return;
+  const u64 s = ext[b], e = ext[b + 1];
+  Sizes z{0, 0, 0};
+  if (e >= s) {
+    if (e - s <= kFlMaxLen && e + 16 <= src_bytes) {
+      const u64 ws = s & ~15ull, e16 = (e + 15) & ~15ull;
+      const __amdgpu_buffer_rsrc_t rs = src_rsrc(src, e16, ws);
+      uint4 v[kFlRounds];
 #pragma unroll
-    for (int r = 0; r < kFlRounds; r++)
-      v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
-  };
-  issue(b);
-  while (b < nb) {
-    const u64 cs = s, ce = e;
-    const bool staged = ce >= cs && ce - cs <= kFlMaxLen;
-    if (staged) {
+      for (int r = 0; r < kFlRounds; r++)
+        v[r] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u32)(r * 1024 + lane * 16), 0, 0));
 #pragma unroll
       for (int r = 0; r < kFlRounds; r++)
         if (r * 1024 + lane * 16 < (u32)kFlWin) *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
+      __builtin_amdgcn_wave_barrier();
+      z = block_sizes(win + (s & 15u), e - s);
+    } else {
+      z = block_sizes(src + s, e - s);   // long blocks, and a block at the buffer's end
     }
-    const u32 bc = b;
-    b += nw;
-    __builtin_amdgcn_wave_barrier();
-    issue(b);   // the next block's loads fly while this one is parsed
-    Sizes z{0, 0, 0};
-    if (ce >= cs) {
-      if (staged) {
-        // a piece straddling the end of the buffer came back zeroed: those blocks (the batch's
-        // last ones) parse from global memory instead
-        if (ce + 16 > src_bytes) z = block_sizes(src + cs, ce - cs);
-        else z = block_sizes(win + (cs & 15u), ce - cs);
-      } else {
-        z = block_sizes(src + cs, ce - cs);
-      }
-    }
-    if (lane == 0) {
-      first[bc] = z.n;
-      first[st + bc] = z.k;
-      first[2 * st + bc] = z.v;
-    }
-    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) {
+    first[b] = z.n;
+    first[st + b] = z.k;
+    first[2 * st + b] = z.v;
   }
 }
 
@@ -239,10 +222,8 @@ void launch_flat_layout(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n
     (void)hipMemsetAsync(first, 0, 3 * 8, stream);
     return;
   }
-  u32 grid = (n_blocks + kFlWaves - 1) / kFlWaves;
-  if (grid > 2 * num_cus) grid = 2 * num_cus;   // 16 waves per workgroup, two per CU (LDS 139 KiB)
-  hipLaunchKernelGGL(flat_sizes_kernel, dim3(grid), dim3(1024), 0, stream, src, ext, src_bytes,
-                     n_blocks, first);
+  hipLaunchKernelGGL(flat_sizes1_kernel, dim3((n_blocks + kFl1Waves - 1) / kFl1Waves), dim3(256), 0,
+                     stream, src, ext, src_bytes, n_blocks, first);
   const u32 np = (n_blocks + kScWg - 1) / kScWg;
   hipLaunchKernelGGL(flat_scan_parts, dim3(np, 3), dim3(256), 0, stream, first, n_blocks, part, np);
   hipLaunchKernelGGL(flat_scan_totals, dim3(3), dim3(1024), 0, stream, part, np);
