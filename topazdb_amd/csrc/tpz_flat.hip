@@ -92,14 +92,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rsrc(const uint8_t* src, u
 // One block per wave and no loop: 4-wave workgroups that exit after their blocks, a grid
 // covering the batch (a looping wave waits for its own stores' acknowledgements at every next
 // load, tools/ubench_bw.hip; the LDS per workgroup is 17 KiB, so up to 9 workgroups share a CU).
-constexpr int kFl1Waves = 4;
-__global__ __launch_bounds__(256) void flat_sizes1_kernel(const uint8_t* src, const u64* ext,
+constexpr int kFlWaves = 4;
+__global__ __launch_bounds__(256) void flat_sizes_kernel(const uint8_t* src, const u64* ext,
                                                           u64 src_bytes, u32 nb, u64* first) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kFl1Waves * kFlWin];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kFlWaves * kFlWin];
   const u32 lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* win = lds + wid * kFlWin;
   const u64 st = (u64)nb + 1;
-  const u32 b = blockIdx.x * kFl1Waves + wid;
+  const u32 b = blockIdx.x * kFlWaves + wid;
   if (b >= nb) return;
   const u64 s = ext[b], e = ext[b + 1];
   Sizes z{0, 0, 0};
@@ -222,7 +222,7 @@ void launch_flat_layout(const uint8_t* src, const u64* ext, u64 src_bytes, u32 n
     (void)hipMemsetAsync(first, 0, 3 * 8, stream);
     return;
   }
-  hipLaunchKernelGGL(flat_sizes1_kernel, dim3((n_blocks + kFl1Waves - 1) / kFl1Waves), dim3(256), 0,
+  hipLaunchKernelGGL(flat_sizes_kernel, dim3((n_blocks + kFlWaves - 1) / kFlWaves), dim3(256), 0,
                      stream, src, ext, src_bytes, n_blocks, first);
   const u32 np = (n_blocks + kScWg - 1) / kScWg;
   hipLaunchKernelGGL(flat_scan_parts, dim3(np, 3), dim3(256), 0, stream, first, n_blocks, part, np);
