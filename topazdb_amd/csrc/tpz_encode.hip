@@ -626,9 +626,14 @@ constexpr int kBigEncLds = kTableBytes + kEncGuard + kBigWin + 4 * kBigWaves;
 // block i; the blocks' first/ext come 64 blocks at a time (lane l: the wave's block g*64 + l).
 constexpr int kPre = 8;                      // prefetched 16-B pieces per lane (key, then value)
 
+// The lengths are taken from the raw next offsets where they are used (a block after the
+// load): subtracting at the load made the wave wait for it, and for everything issued before it
+// (the previous block's stores), at the start of every block.
 struct EntryRegs {                           // the lane's entry in a block's first 64
   u64 kp, vp;                                // kpos[x], vpos[x]
-  u32 kl, vl;                                // its key and value lengths (< 2^16 in any block)
+  u32 k1, v1;                                // low words of kpos[x + 1], vpos[x + 1]
+  __device__ __forceinline__ u32 kl() const { return k1 - (u32)kp; }   // < 2^16 in any block
+  __device__ __forceinline__ u32 vl() const { return v1 - (u32)vp; }
 };
 
 __device__ __forceinline__ EntryRegs load_entry(const EncParams& p, u32 a, u32 e, bool live) {
@@ -636,9 +641,9 @@ __device__ __forceinline__ EntryRegs load_entry(const EncParams& p, u32 a, u32 e
   EntryRegs r{0, 0, 0, 0};
   if (live && x < e) {
     r.kp = p.kpos[x];
-    r.kl = (u32)(p.kpos[x + 1] - r.kp);
+    r.k1 = (u32)p.kpos[x + 1];
     r.vp = p.vpos[x];
-    r.vl = (u32)(p.vpos[x + 1] - r.vp);
+    r.v1 = (u32)p.vpos[x + 1];
   }
   return r;
 }
@@ -650,7 +655,7 @@ __device__ __forceinline__ u128 load_piece(const EncParams& p, const EntryRegs& 
 }
 
 __device__ __forceinline__ void issue_pieces(const EncParams& p, const EntryRegs& r, u128 (&pf)[kPre]) {
-  const u32 nk = (r.kl + 15) / 16, nt = nk + (r.vl + 15) / 16;
+  const u32 nk = (r.kl() + 15) / 16, nt = nk + (r.vl() + 15) / 16;
 #pragma unroll
   for (int k = 0; k < kPre; k++) pf[k] = (u32)k < nt ? load_piece(p, r, nk, k) : (u128)0;
 }
@@ -708,15 +713,15 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     return uni(q);
   };
+  // every lane loads (indices clamped to the table, whose n_blocks + 1 entries exist): a masked
+  // load merged into the old registers made the wave wait for it as soon as it was issued
   auto load_group = [&](u32 q, BlockMeta& m) {
     const u32 cf = chunk_first(q);
-    if (lane < kEncChunk && lane < n_blocks - cf) {
-      const u32 b = cf + lane;
-      m.a = p.first[b];
-      m.e = p.first[b + 1];
-      m.o0 = p.ext[b];
-      m.o1 = p.ext[b + 1];
-    }
+    const u32 b = min(cf + min(lane, kEncChunk - 1), n_blocks), b1 = min(b + 1, n_blocks);
+    m.a = p.first[b];
+    m.e = p.first[b1];
+    m.o0 = p.ext[b];
+    m.o1 = p.ext[b1];
   };
   auto pick = [&](const BlockMeta& m, u32 l) {
     BlockMeta r;
@@ -726,6 +731,7 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     r.o1 = ((u64)readlane((u32)(m.o1 >> 32), (int)l) << 32) | readlane((u32)m.o1, (int)l);
     return r;
   };
+  if (n_blocks == 0) return;
   BlockMeta gA{0, 0, 0, 0}, gB{0, 0, 0, 0};                 // chunks qa and qb
   u32 qa = claim_chunk(), qb = claim_chunk();
   load_group(qa, gA);
@@ -771,7 +777,6 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     const u32 P = (u32)(m.o1 - o0 - 5);
     const bool small = P + A <= kEncMaxP;
     if (small) {
-      const u32 kpad = (16 - ((A + P) & 15)) & 15;       // zero bytes up to the 16-byte boundary
       const u32 zn = (A + P + 5 + 24 + 15) / 16;
       for (u32 q = lane; q < zn; q += kWave) reinterpret_cast<uint4*>(W)[q] = make_uint4(0, 0, 0, 0);
       wave_sync();
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
       const u64 vp0 = ((u64)readlane((u32)(cur.vp >> 32), 0) << 32) | readlane((u32)cur.vp, 0);
       if (lane == 0) or_bytes(W, A, be16(nb & 0xFFFFu), 2);         // block.rs:35 (n as u16)
       {                                                              // entries 0..63 from registers
-        const u64 kl = cur.kl, vl = cur.vl;
+        const u64 kl = cur.kl(), vl = cur.vl();
         if (lane < nb) {
           const u64 off = 4ull * lane + (cur.kp - kp0) + (cur.vp - vp0);
           or_bytes(W, A + 2 + 2 * lane, be16((u32)off & 0xFFFFu), 2);   // builder.rs:37
@@ -805,8 +810,15 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
           copy_in(W, pos + 4 + (u32)kl, p.vals, p.val_bytes, vp, (u32)vl);
         }
       }
-      wave_sync();
-      issue_pieces(p, nxt, pf);                                      // block i + 1's pieces
+    } else {                                                         // longer block: big kernel
+      if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
+    }
+    // block i + 1's pieces, from one site: with a copy per branch the array was merged at the
+    // end of the iteration, a register copy that waited for the loads just issued
+    wave_sync();
+    issue_pieces(p, nxt, pf);
+    if (small) {
+      const u32 kpad = (16 - ((A + P) & 15)) & 15;       // zero bytes up to the 16-byte boundary
       // checksum::calculate_checksum over the payload: init 0xFFFFFFFF folded into its first
       // four bytes, raw CRC of payload || 0^kpad, un-shifted, complemented
       if (lane == 0) xor_bytes(W, A, 0xFFFFFFFFull, 4);
@@ -828,9 +840,6 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
       store_block(W, p.out, o0, A, P + 5, lane, kWave);
 #endif
       wave_sync();
-    } else {                                                         // longer block: big kernel
-      if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
-      issue_pieces(p, nxt, pf);
     }
     cur = nxt;
     nxt = nn;
@@ -839,6 +848,9 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
       qa = qb;
       fa = fb;
       gA = gB;
+      // the copy is made before the next loads are issued, so that they land in gB's registers
+      // (not in temporaries copied over as soon as they are issued, which waited for them)
+      asm volatile("" : "+v"(gA.a), "+v"(gA.e), "+v"(gA.o0), "+v"(gA.o1)::"memory");
       qb = claim_chunk();
       fb = chunk_first(qb);
       load_group(qb, gB);
