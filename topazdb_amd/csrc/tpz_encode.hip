@@ -767,9 +767,6 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     }
 #endif
     const BlockMeta m = meta_of(j);
-    const bool has2 = block_of(j + 2) < n_blocks;
-    const BlockMeta m2 = meta_of(has2 ? j + 2 : j);
-    const EntryRegs nn = load_entry(p, m2.a, m2.e, has2);   // block i + 2's kpos / vpos
 
     const u32 a = m.a, nb = m.e - m.a;
     const u64 o0 = m.o0;
@@ -813,9 +810,14 @@ __global__ __launch_bounds__(kEncThreads) void encode_wave_kernel(EncParams p) {
     } else {                                                         // longer block: big kernel
       if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = b;
     }
-    // block i + 1's pieces, from one site: with a copy per branch the array was merged at the
-    // end of the iteration, a register copy that waited for the loads just issued
+    // (the pieces are issued from one site: with a copy per branch the array was merged at the
+    // end of the iteration, a register copy that waited for the loads just issued)
     wave_sync();
+    // block i + 2's kpos / vpos and block i + 1's pieces, issued after the block's first wait
+    // for its own registers (which, issued earlier, also waited for these)
+    const bool has2 = block_of(j + 2) < n_blocks;
+    const BlockMeta m2 = meta_of(has2 ? j + 2 : j);
+    const EntryRegs nn = load_entry(p, m2.a, m2.e, has2);
     issue_pieces(p, nxt, pf);
     if (small) {
       const u32 kpad = (16 - ((A + P) & 15)) & 15;       // zero bytes up to the 16-byte boundary
