@@ -383,6 +383,7 @@ def e2e_rate(ctx, src: np.ndarray, ext: np.ndarray, n_ent: np.ndarray, dev, reps
     return {"gib_s": round(in_bytes / dt / GIB, 2), "s": round(dt, 4),
             "copy_only_gib_s": round(in_bytes / ct / GIB, 2), "copy_only_s": round(ct, 4),
             "frac_of_copy_only": round(ct / dt, 3), "h2d_bytes": int(in_bytes), "d2h_bytes": down,
+            "s_reps": [round(t, 4) for t in ts],
             "numa_cpus": len(cpus), "path": "tpz_decode_blocks_host (C ABI)"}
 
 
@@ -1163,6 +1164,36 @@ def main():
     except Exception as ex:  # reported, never the metric
         log(rank, f"copy ceiling measurement failed: {ex}")
 
+    # The e2e leg runs before config5 and the flat leg: freeing their tens of GB of device memory
+    # (torch.cuda.empty_cache) slows tpz_decode_blocks_host for the next ~1.5 s, 0.1037 -> 0.133 s
+    # per call on the 4k shard, while plain copies are not slowed (tools/e2e_after_free.py,
+    # profiles/r5/e2e_after_free.jsonl).
+    e2e = None
+    if not args.no_e2e:
+        # every rank (BASELINE.json configs[4]: the H2D/D2H-inclusive rate at N GPUs, all ranks
+        # sharing the host's links and memory): per-rank times, max over ranks, all bytes
+        # The pinned footprint is bounded: every local rank pins its buffers at once (~9.2 GB
+        # per rank for the 4k shard, DESIGN.md §6), so the leg runs on the longest prefix of the
+        # shard that fits half of the host's available memory, the same on every rank.
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        avail = mem_available()
+        k = agree_min(dist, e2e_plan(ext, n_ent, avail, local_ranks), dev)
+        r = None
+        if k > 0:
+            try:
+                r = e2e_rate(ctx, src[:int(ext[k])], ext[:k + 1], n_ent[:k], dev)
+                r["sample_blocks"] = k
+                # a prefix of the shard (host memory short): flagged, never a full-shard result
+                r["partial"] = k < len(ext) - 1
+                r["shard_fraction"] = round(float(ext[k] - ext[0]) / float(ext[-1] - ext[0]), 4)
+                r["host_pinned_bytes_per_rank"] = e2e_host_bytes(ext, n_ent, k)
+                r["host_mem_available"] = avail
+            except Exception as ex:  # reported, never the metric
+                log(rank, f"e2e measurement failed: {ex}")
+        else:
+            log(rank, f"e2e skipped: {local_ranks} ranks x one chunk exceed half of "
+                      f"{avail / GIB:.1f} GiB available")
+        e2e = combine_e2e(dist, r, world, dev)   # every rank joins, failed or not
     config5 = None
     if args.config5_gib > 0 and args.config == "4k" and full == 1 and part == 0:
         # BASELINE.json configs[4] on every rank, whatever N (all ranks join its collectives)
@@ -1177,7 +1208,6 @@ def main():
         cols = SlottedColumns(nb_run, batch.src_bytes, local)
     decode_batch(ctx, batch, cols, stream)   # the decoded columns again (the seek field reads them)
 
-    e2e = None
     side = rank == 0 and world == 1   # side measurements: single-GPU runs only (not the metric)
     flat = None
     if side and not args.no_flat and full == 1 and part == 0:
@@ -1196,28 +1226,6 @@ def main():
         except Exception as ex:  # reported, never the metric
             log(rank, f"exact-ends measurement failed: {ex}")
 
-    if not args.no_e2e:
-        # every rank (BASELINE.json configs[4]: the H2D/D2H-inclusive rate at N GPUs, all ranks
-        # sharing the host's links and memory): per-rank times, max over ranks, all bytes
-        # The pinned footprint is bounded: every local rank pins its buffers at once (~9.2 GB
-        # per rank for the 4k shard, DESIGN.md §6), so the leg runs on the longest prefix of the
-        # shard that fits half of the host's available memory, the same on every rank.
-        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        avail = mem_available()
-        k = agree_min(dist, e2e_plan(ext, n_ent, avail, local_ranks), dev)
-        r = None
-        if k > 0:
-            try:
-                r = e2e_rate(ctx, src[:int(ext[k])], ext[:k + 1], n_ent[:k], dev)
-                r["sample_blocks"] = k
-                r["host_pinned_bytes_per_rank"] = e2e_host_bytes(ext, n_ent, k)
-                r["host_mem_available"] = avail
-            except Exception as ex:  # reported, never the metric
-                log(rank, f"e2e measurement failed: {ex}")
-        else:
-            log(rank, f"e2e skipped: {local_ranks} ranks x one chunk exceed half of "
-                      f"{avail / GIB:.1f} GiB available")
-        e2e = combine_e2e(dist, r, world, dev)   # every rank joins, failed or not
 
     fcrc = None
     if side and not args.no_file_crc:

@@ -113,32 +113,6 @@ std::vector<uint32_t> build_rep_tables(const std::vector<uint32_t>& range) {
   return out;
 }
 
-// The wave path's LDS table image (tpz_decode.hip, decode_wave_kernel): T_0 replicated 32
-// times (word b*32 + r = T_0[b]: lane l reads replica l mod 32, so a byte-indexed lookup is
-// bank-conflict-free), then the decode tables' ids 16..40 (the combine's shift operators and
-// the inverse table), then ids 41..44 = T_39..T_36 (the shift by 40 bytes that joins a lane's
-// two byte chains).
-std::vector<uint32_t> build_wave_tables(const std::vector<uint32_t>& dec) {
-  std::vector<uint32_t> out((size_t)tpz::kWaveTableWords);
-  for (int b = 0; b < 256; b++)
-    for (int r = 0; r < 32; r++) out[(size_t)b * 32 + r] = dec[(size_t)b];
-  for (int l = 0; l < 64; l++) {     // the combine matrix: columns of Z_{80 l}
-    const uint32_t z = x8n((uint64_t)tpz::kCrcLaneBytes * (uint64_t)l);
-    for (int j = 0; j < 32; j++)
-      out[tpz::kWaveRepWords + ((size_t)(j >> 2) * 64 + l) * 4 + (j & 3)] = multmodp(z, 1u << j);
-  }
-  const size_t ids = tpz::kWaveRepWords + tpz::kWaveMatWords;
-  std::memcpy(&out[ids], &dec[16 * 256], (size_t)(tpz::kNumCrcTables - 16) * 256 * 4);
-  const size_t sh = ids + (size_t)(tpz::kNumCrcTables - 16) * 256;
-  for (int h = 0; h < 2; h++)        // shifts by kCrcChainBytes, then by half of it
-    for (int i = 0; i < 4; i++) {
-      const uint32_t z = x8n((uint64_t)((tpz::kCrcChainBytes >> h) - 1 - i));
-      for (int b = 0; b < 256; b++)
-        out[sh + (size_t)(4 * h + i) * 256 + b] = dec[b] ? multmodp(z, dec[b]) : 0u;
-    }
-  return out;
-}
-
 }  // namespace
 
 // Device workspace of one stream: the big-path and spill-path worklists, the big path's
@@ -169,7 +143,6 @@ struct tpz_ctx {
   int device = 0;
   uint32_t num_cus = 0;
   uint32_t* d_tables = nullptr;        // block-decode CRC tables
-  uint32_t* d_wave_tables = nullptr;   // the wave path's LDS table image
   uint32_t* d_range_tables = nullptr;  // range-CRC tables
   uint32_t* d_rep_tables = nullptr;    // replicated slice-by-4 tables
   std::mutex mu;  // guards the workspace map and the host pipelines
@@ -306,10 +279,9 @@ tpz_err tpz_ctx_create(int device, tpz_ctx** out) {
   const std::vector<uint32_t> t = build_crc_tables();
   const std::vector<uint32_t> rt = build_range_tables();
   const std::vector<uint32_t> rep = build_rep_tables(rt);
-  const std::vector<uint32_t> wt = build_wave_tables(t);
   hipError_t e = hipSuccess;
   for (auto [dst, v] : {std::make_pair(&c->d_tables, &t), std::make_pair(&c->d_range_tables, &rt),
-                        std::make_pair(&c->d_rep_tables, &rep), std::make_pair(&c->d_wave_tables, &wt)}) {
+                        std::make_pair(&c->d_rep_tables, &rep)}) {
     if (e == hipSuccess) e = hipMalloc(dst, v->size() * 4);
     if (e == hipSuccess) e = hipMemcpy(*dst, v->data(), v->size() * 4, hipMemcpyHostToDevice);
   }
@@ -328,7 +300,6 @@ void tpz_ctx_destroy(tpz_ctx* c) {
   if (c->d_tables) (void)hipFree(c->d_tables);
   if (c->d_range_tables) (void)hipFree(c->d_range_tables);
   if (c->d_rep_tables) (void)hipFree(c->d_rep_tables);
-  if (c->d_wave_tables) (void)hipFree(c->d_wave_tables);
   for (auto& kv : c->ws) free_workspace(kv.second);
   for (void* p : c->pipes) tpz_internal_pipe_destroy(p);
   delete c;
@@ -370,7 +341,6 @@ tpz_err tpz_decode_blocks(tpz_ctx* c, const tpz_batch* b, const tpz_columns* o, 
   a.src_bytes = b->src_bytes;
   a.n_blocks = b->n_blocks;
   a.crc_tables = c->d_tables;
-  a.wave_tables = c->d_wave_tables;
   a.data = o->d_data;
   a.ends = o->d_ends;
   a.count = o->d_count;
@@ -558,7 +528,6 @@ tpz_err tpz_decode_blocks_flat(tpz_ctx* c, const tpz_batch* b, const tpz_flat_co
   a.src_bytes = b->src_bytes;
   a.n_blocks = b->n_blocks;
   a.crc_tables = c->d_tables;
-  a.wave_tables = c->d_wave_tables;
   a.data = nullptr;                 // no slots: every path writes the columns
   a.ends = o->d_ends;
   a.count = o->d_count;

@@ -30,19 +30,6 @@ constexpr int kNumCrcTables = 41;
 constexpr int kCrcInvTable = 40;
 constexpr int kCrcLaneBytes = 80;
 constexpr int kCrcShiftBytes[6] = {80, 160, 320, 640, 1280, 2560};
-// The wave path's table image (tpz_api.cpp build_wave_tables), words:
-//   [0, 8192)        T_0 replicated 32 times (word b * 32 + r = T_0[b])
-//   [8192, 10240)    the combine matrix: lane l's run value A is shifted to the range end as
-//                    Z_{80 l}(A) = XOR of column j for every set bit j of A; column 4q + c of lane
-//                    l at word 8192 + (q * 64 + l) * 4 + c (one ds_read_b128 per 4 columns)
-//   [10240, ...)     the decode tables' ids 16..40, then the shift by kCrcChainBytes (ids 41..44)
-//                    and by kCrcChainBytes / 2 (ids 45..48: the 4-chain diagnostic build)
-// Each wave-kernel build loads the parts it uses (tpz_decode.hip).
-constexpr int kCrcChainBytes = 40;
-constexpr int kWaveRepWords = 8192;
-constexpr int kWaveMatWords = 2048;
-constexpr int kWaveIdsWords = (kNumCrcTables - 16 + 8) * 256;
-constexpr int kWaveTableWords = kWaveRepWords + kWaveMatWords + kWaveIdsWords;
 // Big path entry-table capacity per block and column: slots are only written when 6n <= len
 // (the unified key+value table holds 2 x this).
 constexpr uint32_t kBigMaxSlots = TPZ_LDS_BLOCK_BYTES / 6 + 16;
@@ -89,7 +76,6 @@ struct LaunchArgs {
   uint64_t src_bytes;
   uint32_t n_blocks;
   const uint32_t* crc_tables;
-  const uint32_t* wave_tables;   // the wave path's LDS table image (kWaveTableWords)
   uint8_t* data;
   uint32_t* ends;
   uint32_t* count;
