@@ -36,23 +36,6 @@
 #include <stdint.h>
 
 #include "tpz_internal.h"
-#if defined(TPZ_ABL_SARW) && !defined(TPZ_CRC_SARW)
-#define TPZ_CRC_SARW   // variant builds: make variants (libtpz_gpu_sarw.so, onchip_sarw, ...)
-#endif
-#if defined(TPZ_ABL_SARW4)   // four byte chains per lane run (20 bytes each) instead of two
-#define TPZ_CRC_SARW4
-#ifndef TPZ_CRC_SARW
-#define TPZ_CRC_SARW
-#endif
-#endif
-#ifdef TPZ_CRC_SARW4
-#define TPZ_IS_SARW4 1
-#else
-#define TPZ_IS_SARW4 0
-#endif
-#if defined(TPZ_ABL_MCOMB) && !defined(TPZ_CRC_MCOMB)
-#define TPZ_CRC_MCOMB
-#endif
 // the tail kernel's spill phase (namespace tpz::sp), compiled into this unit
 #include "tpz_spill.hip"
 
@@ -78,35 +61,10 @@ constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B 
 constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads, the 5th partial
 constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
-// The wave path's CRC tables in LDS, words (tab = the pointer the CRC helpers take; ids as in
-// tpz_internal.h; the image parts come from tpz_api.cpp build_wave_tables):
-//   default       [ids 0..40]                                     tab = base
-//   MCOMB         [ids 0..15][id 40 (inv)][matrix 2048]           tab = base
-//   SARW          [T_0 x 32][ids 16..44]                          tab = base + 8192 - 16 * 256
-//   SARW + MCOMB  [T_0 x 32][matrix 2048][ids 40..44]             tab = base + 10240 - 40 * 256
-#if defined(TPZ_CRC_SARW) && defined(TPZ_CRC_MCOMB)
-constexpr int kWaveTabWords = kWaveRepWords + kWaveMatWords + 5 * 256;
-constexpr int kTabOff = kWaveRepWords + kWaveMatWords - 40 * 256;
-#elif defined(TPZ_CRC_SARW)
-static_assert(!TPZ_IS_SARW4, "the 4-chain build needs the matrix combine's layout (sarw4_mcomb)");
-constexpr int kWaveTabWords = kWaveRepWords + (kNumCrcTables - 16 + 4) * 256;   // ids 16..44
-constexpr int kTabOff = kWaveRepWords - 16 * 256;
-#elif defined(TPZ_CRC_MCOMB)
-constexpr int kWaveTabWords = 17 * 256 + kWaveMatWords;
-constexpr int kTabOff = 0;
-#else
-constexpr int kWaveTabWords = kNumCrcTables * 256;
-constexpr int kTabOff = 0;
-#endif
-constexpr int kWaveTabBytes = kWaveTabWords * 4;
-#if defined(TPZ_CRC_SARW) && !defined(TPZ_CRC_MCOMB)
-// the SARW image takes 61 KiB: the entry table holds 2n + 1 <= 255 segments
-constexpr u32 kWaveMaxN = 127;
-constexpr int kWaveTabSlots = 256;
-#else
+// The wave path's CRC tables in LDS: the decode tables, ids 0..40 (tpz_internal.h).
+constexpr int kWaveTabBytes = kTableBytes;
 constexpr u32 kWaveMaxN = 255;                      // the table holds 2n + 1 <= 511 entries
 constexpr int kWaveTabSlots = 512;
-#endif
 constexpr int kWaveMapLen = 288;                    // >= (kWaveMaxLen + 2) / 16 + 3 map slots
 constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveTabSlots * 4 + 2 * kWaveMapLen;
 static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 8 == 0, "slot alignment");
@@ -355,88 +313,6 @@ __device__ __forceinline__ u32 wave_crc(const u32* tab, const uint8_t* win, int 
   }
   return crc_combine(tab, A);
 }
-
-#ifdef TPZ_CRC_SARW
-// Wave path, byte-serial CRC (Sarwate) over T_0 replicated 32 times: word b * 32 + r = T_0[b],
-// lane l reads replica l mod 32, so a lookup with any byte per lane hits 32 distinct banks
-// (ds_read_b32 serves lanes 0-31 and 32-63 in one LDS cycle each) instead of the slice tables'
-// ~3x replays. tab (ids >= 16, as everywhere) sits right after the replicas.
-__device__ __forceinline__ const u32* crc_rep(const u32* tab) { return tab - kTabOff; }
-__device__ __forceinline__ const u32* crc_inv(const u32* tab) { return tab + kCrcInvTable * 256; }
-// c = T_0[(c ^ b) & 0xFF] ^ (c >> 8) for the four bytes of w
-__device__ __forceinline__ u32 sarw4(const u32* rep, u32 lr, u32 c, u32 w) {
-  c ^= w;
-#pragma unroll
-  for (int i = 0; i < 4; i++) c = rep[((c & 0xFFu) << 5) | lr] ^ (c >> 8);
-  return c;
-}
-// shift_k (k zero bytes) and its inverse, for a wave-uniform k < 16
-__device__ __forceinline__ u32 crc_shift_small_w(const u32* tab, u32 a, u32 k) {
-  const u32* rep = crc_rep(tab);
-  const u32 lr = lane_id() & 31u;
-  for (u32 i = 0; i < k; i++) a = rep[((a & 0xFFu) << 5) | lr] ^ (a >> 8);
-  return a;
-}
-__device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k) {
-  const u32* rep = crc_rep(tab);
-  const u32 lr = lane_id() & 31u;
-  for (u32 i = 0; i < k; i++) {
-    const u32 b = crc_inv(tab)[r >> 24];
-    r = ((r ^ rep[(b << 5) | lr]) << 8) | b;
-  }
-  return r;
-}
-// shift by kCrcChainBytes (ids 41..44: T_39..T_36)
-__device__ __forceinline__ u32 crc_shift_chain(const u32* tab, u32 a) {
-  return xor3(tlook(tab, 41, a & 0xFF), tlook(tab, 42, (a >> 8) & 0xFF),
-              tlook(tab, 43, (a >> 16) & 0xFF)) ^ tlook(tab, 44, a >> 24);
-}
-#else
-__device__ __forceinline__ u32 crc_shift_small_w(const u32* tab, u32 a, u32 k) {
-  return crc_shift_small(tab, a, k);
-}
-__device__ __forceinline__ u32 crc_unshift_small_w(const u32* tab, u32 r, u32 k) {
-#ifdef TPZ_CRC_MCOMB
-  for (u32 i = 0; i < k; i++) {            // the inverse table sits at id 16 in this layout
-    const u32 b = tlook(tab, 16, r >> 24);
-    r = ((r ^ tlook(tab, 0, b)) << 8) | b;
-  }
-  return r;
-#else
-  return crc_unshift_small(tab, r, k);
-#endif
-}
-#endif
-
-// The wave path's combine of the lanes' run values (lane l's run ends 80 l bytes before the
-// range end) into R0 of the range.
-#ifdef TPZ_CRC_MCOMB
-// One short chain instead of the tree's six dependent LDS round trips: lane l applies
-// Z_{80 l} (a GF(2) matrix, its columns from LDS in 8 ds_read_b128) to its value, XORing the
-// column of every set bit, and the wave XORs the results.
-__device__ __forceinline__ const u32* crc_mat(const u32* tab) {
-#ifdef TPZ_CRC_SARW
-  return tab - kTabOff + kWaveRepWords;
-#else
-  return tab + 17 * 256;
-#endif
-}
-__device__ __forceinline__ u32 crc_combine_w(const u32* tab, u32 A) {
-  const uint4* M = reinterpret_cast<const uint4*>(crc_mat(tab)) + lane_id();
-  u32 R = 0;
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const uint4 c = M[64 * q];
-    R ^= c.x & (u32)((int)(A << (31 - 4 * q)) >> 31);
-    R ^= c.y & (u32)((int)(A << (30 - 4 * q)) >> 31);
-    R ^= c.z & (u32)((int)(A << (29 - 4 * q)) >> 31);
-    R ^= c.w & (u32)((int)(A << (28 - 4 * q)) >> 31);
-  }
-  return wave_xor(R);
-}
-#else
-__device__ __forceinline__ u32 crc_combine_w(const u32* tab, u32 A) { return crc_combine(tab, A); }
-#endif
 
 // ------------------------------------------------------------------ entry tables
 // The NON-EMPTY keys in order, then the non-empty values in order (one table for the block's
@@ -879,65 +755,8 @@ struct CrcLane {
   int seg;      // the lane's run [seg, seg + 80) relative to the payload start (end-aligned)
   bool act;     // the run overlaps the payload
   u32 c;        // the run's raw CRC so far
-#ifdef TPZ_CRC_SARW
-  u32 c2;       // the second byte chain: the run's last 40 bytes
-  u32 lr;       // the lane's table replica
-#endif
-#ifdef TPZ_CRC_SARW4
-  u32 c3, c4;   // 4-chain build: the run's quarters 3 and 4
-#endif
 };
 
-#if defined(TPZ_CRC_SARW4)
-// Step t: bytes [4t, 4t + 4) of each of the run's four 20-byte quarters, one byte chain each.
-__device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
-                                         int t) {
-  const u32* rep = crc_rep(tab);
-  const int a = L.act ? pb + L.seg + 4 * t : -kGuard;
-  const int q = L.act ? kCrcChainBytes / 2 : 0;
-  const u32 w0 = *reinterpret_cast<const u32*>(win + a);
-  const u32 w1 = *reinterpret_cast<const u32*>(win + a + q);
-  const u32 w2 = *reinterpret_cast<const u32*>(win + a + 2 * q);
-  const u32 w3 = *reinterpret_cast<const u32*>(win + a + 3 * q);
-  L.c = sarw4(rep, L.lr, L.c, w0);
-  L.c2 = sarw4(rep, L.lr, L.c2, w1);
-  L.c3 = sarw4(rep, L.lr, L.c3, w2);
-  L.c4 = sarw4(rep, L.lr, L.c4, w3);
-}
-// shift by kCrcChainBytes / 2 (T_19..T_16)
-__device__ __forceinline__ u32 crc_shift_half(const u32* tab, u32 a) {
-#ifdef TPZ_CRC_MCOMB
-  constexpr int id = 41;
-#else
-  constexpr int id = 45;
-#endif
-  return xor3(tlook(tab, id, a & 0xFF), tlook(tab, id + 1, (a >> 8) & 0xFF),
-              tlook(tab, id + 2, (a >> 16) & 0xFF)) ^ tlook(tab, id + 3, a >> 24);
-}
-// The run's raw CRC: Horner over the four quarters' chains.
-__device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) {
-  return crc_shift_half(tab, crc_shift_half(tab, crc_shift_half(tab, L.c) ^ L.c2) ^ L.c3) ^ L.c4;
-}
-#elif defined(TPZ_CRC_SARW)
-// Step t: bytes [8t, 8t + 8) of each of the run's two 40-byte halves, one byte chain per half.
-__device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
-                                         int t) {
-  typedef u32 u32x2 __attribute__((ext_vector_type(2)));
-  const u32* rep = crc_rep(tab);
-  const int a = L.act ? pb + L.seg + 8 * t : -kGuard;  // 8-byte aligned either way
-  const int a2 = L.act ? a + kCrcChainBytes : -kGuard;
-  const u32x2 w = *reinterpret_cast<const u32x2*>(win + a);
-  const u32x2 w2 = *reinterpret_cast<const u32x2*>(win + a2);
-  L.c = sarw4(rep, L.lr, L.c, w.x);
-  L.c2 = sarw4(rep, L.lr, L.c2, w2.x);
-  L.c = sarw4(rep, L.lr, L.c, w.y);
-  L.c2 = sarw4(rep, L.lr, L.c2, w2.y);
-}
-// The run's raw CRC: the first half's chain shifted past the second half, XOR the second's.
-__device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) {
-  return crc_shift_chain(tab, L.c) ^ L.c2;
-}
-#else
 __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int pb, CrcLane& L,
                                          int t) {
   typedef u32 u32x4 __attribute__((ext_vector_type(4)));
@@ -948,7 +767,6 @@ __device__ __forceinline__ void crc_step(const u32* tab, const uint8_t* win, int
   L.c = slice16(tab, w.x ^ L.c, w.y, w.z, w.w);
 }
 __device__ __forceinline__ u32 crc_lane_value(const u32* tab, const CrcLane& L) { return L.c; }
-#endif
 
 struct FastWin {
   u32 nk, tot, nch, npad, last;
@@ -1057,13 +875,6 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
   L.act = L.seg + kCrcLaneBytes > 0;
   L.c = 0;
-#ifdef TPZ_CRC_SARW
-  L.c2 = 0;
-  L.lr = lane & 31u;
-#endif
-#ifdef TPZ_CRC_SARW4
-  L.c3 = L.c4 = 0;
-#endif
   u32 carry = 0, rare = 0, cw[5];
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -1093,26 +904,200 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   return crc_lane_value(tab, L);   // the lane's raw run CRC: crc_combine gives R0 of the range
 }
 
-#if defined(TPZ_CRC_SARW) || defined(TPZ_CRC_MCOMB)
-// wave_crc for a wave-path block (Pa <= 5120): its steps and combine (crc_step, crc_combine_w).
-__device__ __forceinline__ u32 wave_crc_w(const u32* tab, const uint8_t* win, int pb, u32 Pa) {
-  const u32 lane = lane_id();
-  CrcLane L;
-  L.seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
-  L.act = L.seg + kCrcLaneBytes > 0;
-  L.c = 0;
-#ifdef TPZ_CRC_SARW
-  L.c2 = 0;
-  L.lr = lane & 31u;
-#endif
-#ifdef TPZ_CRC_SARW4
-  L.c3 = L.c4 = 0;
-#endif
-#pragma unroll
-  for (int t = 0; t < kCrcLaneBytes / 16; t++) crc_step(tab, win, pb, L, t);
-  return crc_combine_w(tab, crc_lane_value(tab, L));
+// ------------------------------------------------------------------ pipelined copy + CRC
+// LDS reads return in issue order and `s_waitcnt lgkmcnt(N)` waits for all but the N youngest,
+// so waiting for one read also waits for every read issued before it. copy_crc_fused interleaves
+// the copy's and the CRC's chains instruction by instruction, and the compiler's order made
+// almost every wait a full drain (lgkmcnt(0)): each window's map read waited for the CRC lookups
+// issued just before it, its gathers for both, and so on — about five LDS round trips per window
+// in series. Here the two chains are staged so that each wait targets reads issued one stage
+// earlier, with the other chain's reads behind them still in flight:
+//   A  map reads of windows 0-3, CRC data of step 0
+//   B  the four windows' prefix max (their DPP chains interleave), carries, entry reads
+//   C  lookups of step 0, data of step 1
+//   D  gathers of window 0
+//   then per t: CRC step t+1 (xor of step t's lookups, lookups of step t+1, data of step t+2),
+//               window t stored and window t+1's gathers issued
+// __builtin_amdgcn_sched_barrier(0) between stages keeps the compiler from re-merging them; the
+// waitcnt pass then counts the waits (lgkmcnt(N), N > 0). Blocks whose stream needs a fifth window
+// (more than 4096 B of keys and values) copy it afterwards with copy_fast.
+typedef u32 u32x2v __attribute__((ext_vector_type(2)));
+typedef u32 u32x4v __attribute__((ext_vector_type(4)));
+struct Gath {
+  u32x2v a, b, c;
+};
+// the three 8-byte-aligned LDS words holding bytes [x, x + 16) (issued, not waited for)
+__device__ __forceinline__ Gath gath_issue(const uint8_t* base, int x) {
+  const u32x2v* p = reinterpret_cast<const u32x2v*>(base + (x & ~7));
+  Gath g;
+  g.a = p[0];
+  g.b = p[1];
+  g.c = p[2];
+  return g;
 }
-#endif
+// bytes [x, x + 16) from the gathered words: a one-bit dword select + alignbyte (lds_window16)
+__device__ __forceinline__ uint4 gath_finish(Gath g, int x) {
+  asm volatile("" : "+v"(g.a), "+v"(g.b), "+v"(g.c));
+  const u32 s = (u32)x & 3u;
+  const bool h = ((u32)x & 4u) != 0;
+  const u32 s0 = h ? g.a.y : g.a.x, s1 = h ? g.b.x : g.a.y, s2 = h ? g.b.y : g.b.x,
+            s3 = h ? g.c.x : g.b.y, s4 = h ? g.c.y : g.c.x;
+  return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, s), __builtin_amdgcn_alignbyte(s2, s1, s),
+                    __builtin_amdgcn_alignbyte(s3, s2, s), __builtin_amdgcn_alignbyte(s4, s3, s));
+}
+// the 16 lookups of a slice-by-16 step over (w0 ^ c, w1, w2, w3), issued
+struct Look16 {
+  u32 r[16];
+};
+__device__ __forceinline__ Look16 look_issue(const u32* tab, u32x4v w, u32 c) {
+  Look16 L;
+  const u32 w0 = w.x ^ c;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    L.r[i] = tlook(tab, 15 - i, (w0 >> (8 * i)) & 0xFF);
+    L.r[4 + i] = tlook(tab, 11 - i, (w.y >> (8 * i)) & 0xFF);
+    L.r[8 + i] = tlook(tab, 7 - i, (w.z >> (8 * i)) & 0xFF);
+    L.r[12 + i] = tlook(tab, 3 - i, (w.w >> (8 * i)) & 0xFF);
+  }
+  return L;
+}
+__device__ __forceinline__ u32 look_xor(const Look16& L) {
+  u32 c = xor3(L.r[0], L.r[1], L.r[2]);
+  c = xor3(c, L.r[3], L.r[4]);
+  c = xor3(c, L.r[5], L.r[6]);
+  c = xor3(c, L.r[7], L.r[8]);
+  c = xor3(c, L.r[9], L.r[10]);
+  c = xor3(c, L.r[11], L.r[12]);
+  c = xor3(c, L.r[13], L.r[14]);
+  return c ^ L.r[15];
+}
+#define TPZ_SB() __builtin_amdgcn_sched_barrier(0)
+
+// One copy window of copy_crc_piped, stage by stage.
+struct PWin {
+  u32 m, j;          // map slot, then the chunk's first segment
+  u32 e0, e1;
+  int d0, d1;
+  bool act, cross;
+  Gath ga, gn;
+};
+
+template <bool FLAT>
+__device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& col,
+                                              const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
+                                              const FlatOut& D, const uint8_t* win, int pb, u32 Pa) {
+  const u32 lane = lane_id();
+  FastWin F;
+  F.nk = nk;
+  F.tot = tot;
+  F.nch = (tot + 15) >> 4;
+  F.npad = FLAT ? F.nch : (F.nch + 7) & ~7u;
+  F.last = nk ? nk - 1 : 0u;
+  F.out = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, FLAT ? 0 : (int)(F.npad * 16), 0x00020000);
+  const u32 nw = (F.npad + 63) >> 6;
+  const int seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
+  const bool cact = seg + kCrcLaneBytes > 0;
+  auto dread = [&](int t) -> u32x4v {   // CRC data of step t (lanes before the payload: the guard)
+    return *reinterpret_cast<const u32x4v*>(win + (cact ? pb + seg + 16 * t : -kGuard));
+  };
+  PWin W[4];
+  // A: map reads, CRC data of step 0
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const u32 c = 64 * w + lane;
+    W[w].act = c < F.nch;
+    W[w].m = map[min(c, (u32)kWaveMapLen - 1)];
+  }
+  u32x4v dA = dread(0);
+  TPZ_SB();
+  // B: prefix max per window (independent DPP chains), carries, entries j and j + 1
+#pragma unroll
+  for (int w = 0; w < 4; w++) W[w].j = wave_scan_max(W[w].act ? W[w].m : 0u);
+  u32 cw[5];
+  cw[0] = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    W[w].j = max(W[w].j, cw[w]);
+    cw[w + 1] = readlane(W[w].j, 63);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) col.get2(min(W[w].j, F.last), W[w].e0, W[w].d0, W[w].e1, W[w].d1);
+  TPZ_SB();
+  // C: lookups of step 0, data of step 1
+  Look16 LK = look_issue(tab, dA, 0u);
+  u32x4v dB = dread(1);
+  TPZ_SB();
+  u32 rare = 0;
+  auto gissue = [&](PWin& P, u32 w) {
+    const u32 x0 = 16 * (64 * w + lane);
+    P.cross = P.act && P.j + 1 < F.nk && P.e0 < x0 + 16;
+    P.ga = gath_issue(win, P.act ? (int)x0 + P.d0 : -kGuard);
+    P.gn = gath_issue(win, P.cross ? (int)x0 + P.d1 : -kGuard);
+  };
+  auto finish = [&](PWin& P, u32 w) {
+    const u32 c = 64 * w + lane;
+    const u32 x0 = 16 * c;
+    // a window where a lane needs copy_window's rare path is left to it whole
+    const bool rw = __ballot(P.act && (P.e0 <= x0 || (P.cross && P.e1 < x0 + 16 && P.j + 2 < F.nk))) != 0;
+    if (rw) rare |= 1u << w;
+    uint4 acc = gath_finish(P.ga, P.act ? (int)x0 + P.d0 : -kGuard);
+    const uint4 nx = gath_finish(P.gn, P.cross ? (int)x0 + P.d1 : -kGuard);
+    if (P.cross) acc = merge_at(acc, nx, (int)(P.e0 - x0));
+    if (FLAT)
+      D.put(c, acc, rw);
+    else
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc), F.out, rw ? kOob : x0, 0, 0);
+  };
+  // D: gathers of window 0
+  gissue(W[0], 0);
+  TPZ_SB();
+  u32 crc = 0;
+  // E: CRC step 1 ; F: window 0 out, window 1 gathers
+  crc = look_xor(LK);
+  LK = look_issue(tab, dB, crc);
+  dA = dread(2);
+  TPZ_SB();
+  finish(W[0], 0);
+  gissue(W[1], 1);
+  TPZ_SB();
+  // G: CRC step 2 ; H: window 1 out, window 2 gathers
+  crc = look_xor(LK);
+  LK = look_issue(tab, dA, crc);
+  dB = dread(3);
+  TPZ_SB();
+  finish(W[1], 1);
+  gissue(W[2], 2);
+  TPZ_SB();
+  // I: CRC step 3 ; J: window 2 out, window 3 gathers
+  crc = look_xor(LK);
+  LK = look_issue(tab, dB, crc);
+  dA = dread(4);
+  TPZ_SB();
+  finish(W[2], 2);
+  gissue(W[3], 3);
+  TPZ_SB();
+  // K: CRC step 4 ; L: window 3 out
+  crc = look_xor(LK);
+  LK = look_issue(tab, dA, crc);
+  TPZ_SB();
+  finish(W[3], 3);
+  TPZ_SB();
+  crc = look_xor(LK);
+  if (nw > 4) {
+    (void)copy_fast<FLAT>(Src16{win}, col, map, F, D, 4u, cw[4], rare);
+  }
+  if (rare) {
+    for (u32 w = 0; w < nw; w++)
+      if (rare & (1u << w)) {
+        if (FLAT)
+          copy_window(Src16{win}, col, map, nk, F.tot, FlatDst{&D}, (u32)kWaveMapLen, w, cw[w]);
+        else
+          copy_window(Src16{win}, col, map, nk, F.tot, SlotDst{dst, F.npad, F.tot}, (u32)kWaveMapLen, w, cw[w]);
+      }
+  }
+  return crc;
+}
+
 
 // The wave path defers a block's CRC combine and status write into the next block's decode
 // (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
@@ -1125,9 +1110,9 @@ struct PendingCrc {
 
 __device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
   if (!pd.live) return;
-  const u32 R = crc_combine_w(tab, pd.lc);
-  const u32 crc = (R == crc_shift_small_w(tab, ~pd.stored, pd.k)) ? pd.stored
-                                                                   : ~crc_unshift_small_w(tab, R, pd.k);
+  const u32 R = crc_combine(tab, pd.lc);
+  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
+                                                                   : ~crc_unshift_small(tab, R, pd.k);
   const bool ok = crc == pd.stored;                                            // checksum.rs:17
   put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
   pd.live = 0;
@@ -1347,23 +1332,24 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
           ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                        fo, win, pb, P + k, kshift, S, f_w3)
+#ifndef TPZ_ABL_PIPED
           : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                         fo, win, pb, P + k, kshift, S);
+#else
+          : copy_crc_piped<FLAT>(tab, *reinterpret_cast<const ColSmall*>(&col),
+                                 reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, fo, win,
+                                 pb, P + k);
+#endif
       pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
       return;
     } else {
-#if defined(TPZ_CRC_SARW) || defined(TPZ_CRC_MCOMB)
-      if constexpr (!BIG) {
-        R = wave_crc_w(tab, win, pb, P + k);
-      } else
-#endif
         R = wave_crc(tab, win, pb, P + k);
     }
     if constexpr (BIG)
       crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
     else
-      crc = (R == crc_shift_small_w(tab, ~stored, k)) ? stored : ~crc_unshift_small_w(tab, R, k);
+      crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
 #if defined(TPZ_ABL_NOCF) || defined(TPZ_ABL_LUTVALU)
     asm volatile("" ::"v"(R));   // keep the CRC work, report a match (timing builds only)
     crc = stored;
@@ -1427,7 +1413,6 @@ struct Params {
   u64 src_bytes;
   u32 n_blocks;
   const u32* crc_tables;
-  const u32* wave_tables;  // the wave path's table image (TPZ_CRC_SARW builds)
   Out out;
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
@@ -1448,7 +1433,7 @@ __device__ unsigned long long g_wave_ends[3 * 8192];
 template <bool FLAT>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
-  u32* tab = reinterpret_cast<u32*>(lds) + kTabOff;   // (the layouts: kWaveTabWords)
+  u32* tab = reinterpret_cast<u32*>(lds);
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   __shared__ Out out_lds;             // the worklist pointers for the rare paths (see above)
   if (threadIdx.x == 0) {             // (load_tables' barrier publishes both)
@@ -1459,35 +1444,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #ifdef TPZ_ABL_WAVEENDS
   const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  {
-    // the build's table layout from the decode tables (ids) and the wave image (kWaveTableWords)
-    u32* base = reinterpret_cast<u32*>(lds);
-    auto put = [&](const u32* src, int dst_word, int words) {
-      const uint4* s = reinterpret_cast<const uint4*>(src);
-      uint4* d = reinterpret_cast<uint4*>(base + dst_word);
-      for (int i = threadIdx.x; i < words / 4; i += blockDim.x) d[i] = s[i];
-    };
-    const int ids = kWaveRepWords + kWaveMatWords;     // id 16 in the image
-#if defined(TPZ_CRC_SARW) && defined(TPZ_CRC_MCOMB)
-    put(p.wave_tables, 0, kWaveRepWords + kWaveMatWords);
-#ifdef TPZ_CRC_SARW4
-    put(p.wave_tables + ids + (40 - 16) * 256, kWaveRepWords + kWaveMatWords, 256);
-    put(p.wave_tables + ids + (45 - 16) * 256, kWaveRepWords + kWaveMatWords + 256, 4 * 256);
-#else
-    put(p.wave_tables + ids + (40 - 16) * 256, kWaveRepWords + kWaveMatWords, 5 * 256);
-#endif
-#elif defined(TPZ_CRC_SARW)
-    put(p.wave_tables, 0, kWaveRepWords);
-    put(p.wave_tables + ids, kWaveRepWords, kWaveTabWords - kWaveRepWords);
-#elif defined(TPZ_CRC_MCOMB)
-    put(p.crc_tables, 0, 16 * 256);
-    put(p.crc_tables + kCrcInvTable * 256, 16 * 256, 256);
-    put(p.wave_tables + kWaveRepWords, 17 * 256, kWaveMatWords);
-#else
-    put(p.crc_tables, 0, kNumCrcTables * 256);
-#endif
-    __syncthreads();
-  }
+  load_tables(tab, p.crc_tables);
 
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
@@ -2118,7 +2075,6 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.src_bytes = a.src_bytes;
   p.n_blocks = a.n_blocks;
   p.crc_tables = a.crc_tables;
-  p.wave_tables = a.wave_tables;
   p.big_scratch = a.big_scratch;
   p.spill_used = a.spill_used;
   p.out = Out{a.data, a.ends, a.count, a.status, a.crc, a.defer_list, a.defer_count,
