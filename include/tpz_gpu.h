@@ -262,8 +262,10 @@ tpz_err tpz_decode_blocks(tpz_ctx* ctx, const tpz_batch* batch, const tpz_column
  * TPZ_ERR_INTERNAL (and the flag cleared) when a tail workgroup's bounded wait for the big
  * path timed out, so that blocks of the spill worklist may have been left undecoded (their
  * status/count/crc are then unspecified). The wait only times out if the device stalls for
- * about a second; a caller that cannot trust its outputs otherwise checks after each batch
- * (tpz_decode_blocks_host and the Python layer do). */
+ * about a second. The flag is sticky per stream: it covers every decode queued on `stream`
+ * since the previous check, so a device-resident integration calls this once per batch (after
+ * the batch's decode, before it trusts the outputs; tpz_decode_blocks_host and the Python layer
+ * do). The flag is read and cleared in stream order (no null-stream copy). */
 tpz_err tpz_decode_check(tpz_ctx* ctx, void* stream);
 
 /* The exact ends layout. The slotted ends reserve the worst case (a pair per 6 input bytes,
@@ -400,6 +402,23 @@ tpz_err tpz_host_decoded_bound(const uint8_t* h_src, const uint64_t* h_ext, uint
 tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext,
                                uint32_t n_blocks, const tpz_host_columns* out,
                                uint32_t chunk_blocks);
+
+/* SsTable::read_block's checks for a run of blocks in host memory, with the decoded columns left
+ * on the device: the reference's Block is {data: payload[2 + 2n ..], offsets} of the block's
+ * Uncompress form (src/block.rs:46-65), so a host that holds the block bytes needs only the
+ * device's verdict (CRC, tag, header) and, for snappy / lz4 blocks, the decompressed bytes to
+ * build it without a copy (rust/topazdb-gpu/src/table/gpu.rs, read_blocks_gpu). Same pipeline as
+ * tpz_decode_blocks_host (chunked H2D, codec step, decode) without the slot, ends and spill
+ * downloads. Outputs: h_status, h_crc, h_count (n each, as tpz_host_columns); h_dext (n + 1, may
+ * be NULL for a batch without snappy / lz4 blocks; h_ext is then the decoded layout); h_plain /
+ * plain_cap: for a batch with snappy / lz4 blocks, h_dext[n] bytes receiving every block's
+ * Uncompress form at h_dext[i] (tpz_host_decoded_bound bounds it); unused (may be NULL)
+ * otherwise. Returns TPZ_ERR_NOMEM when plain_cap < h_dext[n] (h_dext[n] then holds the size
+ * needed). */
+tpz_err tpz_verify_blocks_host(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext,
+                               uint32_t n_blocks, uint8_t* h_status, uint32_t* h_crc,
+                               uint32_t* h_count, uint8_t* h_plain, uint64_t plain_cap,
+                               uint64_t* h_dext, uint32_t chunk_blocks);
 
 /* ---- whole-range CRC-32 ------------------------------------------------------------------
  * Ranges use the batch type: range i is d_src[d_ext[i] .. d_ext[i+1]) (d_ext non-decreasing,
@@ -591,8 +610,12 @@ int tpz_lz4_encode_blocks(const uint8_t* h_src, const uint64_t* h_ext, uint64_t 
  * bytes written), so BlockMeta::offset of block i is d_dst_ext[i] (src/table/builder.rs:74-84).
  * Blocks with another tag are copied unchanged; any other codec is TPZ_ERR_INVALID_ARG. The
  * streams decode with snap / liblz4 to exactly payload | crc; they are not byte-identical to
- * those libraries' encoders. d_dst needs tpz_layout_compress_bound(src_bytes, n_blocks) bytes.
- * Asynchronous on `stream`; uses the stream's workspace (scratch of that bound). */
+ * those libraries' encoders. Blocks whose payload is longer than 4,336 bytes (block_size past
+ * 4 KiB) are emitted as literal elements only: valid streams, a few bytes larger than the
+ * payload (the match finder works on blocks staged whole in LDS). d_dst needs
+ * tpz_layout_compress_bound(src_bytes, n_blocks) bytes. batch->d_src and d_dst must be 16-byte
+ * aligned (TPZ_ERR_INVALID_ARG otherwise). Asynchronous on `stream`; uses the stream's workspace
+ * (scratch of that bound). */
 uint64_t tpz_layout_compress_bound(uint64_t src_bytes, uint64_t n_blocks);
 tpz_err tpz_compress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint32_t codec, uint8_t* d_dst,
                             uint64_t* d_dst_ext, void* stream);

@@ -1,4 +1,5 @@
-//! `Block::from_columns`: one block of a device decode back into the reference's `Block`.
+//! `Block::from_verified` / `Block::from_columns`: one block of a device decode as the
+//! reference's `Block`.
 //!
 //! Drop-in module for topazdb: copy to `src/block/gpu.rs` and add `pub mod gpu;` to
 //! `src/block.rs`. As a child of `block` it may build `Block { data, offsets }`
@@ -87,7 +88,22 @@ impl HostDecode {
 }
 
 impl Block {
-    /// The reference's `Block` for block i of a device decode: `data` holds the entries encoded
+    /// The reference's `Block` from the Uncompress form `b` of a block (payload | crc | tag 1)
+    /// whose tag, CRC and header the device has verified (`tpz_verify_blocks_host` status OK,
+    /// OK_SPILLED or BAD_ENTRY, so `b.len() >= 7 + 2n`): exactly what `Block::decode(b)` returns
+    /// (`src/block.rs:46-65`: `n`, the `n` big-endian offsets, `data` = the payload after them),
+    /// with `data` a slice of `b`, no copy. For an Uncompress block `b` is a slice of the bytes
+    /// `FileObject::read` returned, for a snappy / lz4 block of the device's decompressed bytes.
+    /// A BAD_ENTRY block is the reference's `Ok(Block)` too: its iterator panics by itself on
+    /// the out-of-range entries (`iterator.rs:74-82`).
+    pub fn from_verified(b: &Bytes) -> Block {
+        let n = u16::from_be_bytes([b[0], b[1]]) as usize;
+        let offsets = (0..n).map(|j| u16::from_be_bytes([b[2 + 2 * j], b[3 + 2 * j]])).collect();
+        Block { data: b.slice(2 + 2 * n..b.len() - 5), offsets }
+    }
+
+    /// The reference's `Block` for block i of a device decode (device-column consumers: the
+    /// columns are already on the host): `data` holds the entries encoded
     /// as `Entry::encode` writes them (`src/block/builder.rs:72-81`: klen, key, vlen, value;
     /// big-endian u16 lengths) and `offsets` their positions, so `BlockIterator` reads exactly the
     /// keys and values the reference's own `Block::decode` + iterator read from the block bytes.

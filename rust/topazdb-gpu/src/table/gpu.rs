@@ -11,15 +11,19 @@
 //! ```
 //!
 //! The blocks go in as `FileObject::read` returns them (`src/table/file_object.rs:23-27`, one
-//! `pread` of the run), through the library's chunked H2D -> codec step (snappy / lz4) ->
-//! decode + CRC -> D2H pipeline, and come back as `Arc<Block>`s built from the device's
-//! columns (`Block::from_columns`, `src/block/gpu.rs`), or as the reference's `Err` for a
-//! block the reference rejects.
+//! `pread` of the run) and through the library's chunked H2D -> codec step (snappy / lz4) ->
+//! decode + CRC pipeline (`tpz_verify_blocks_host`). The reference's `Block` is a view of the
+//! block's own bytes (`src/block.rs:46-65`), so the host needs only the device's verdict and,
+//! for snappy / lz4 blocks, the decompressed bytes: each `Arc<Block>` is `Block::from_verified`
+//! over a slice of the run (`Bytes`, no copy), or the reference's `Err` for a block the
+//! reference rejects. `decode_host` (the columns in host memory, `Block::from_columns`) stays
+//! for consumers of the decoded keys and values themselves.
 use std::ffi::CStr;
 use std::os::raw::c_char;
 use std::sync::Arc;
 
 use anyhow::{anyhow, bail, Result};
+use bytes::Bytes;
 use tpz_gpu_sys as ffi;
 
 use super::SsTable;
@@ -100,6 +104,54 @@ impl GpuDecoder {
     }
 }
 
+/// `tpz_verify_blocks_host`'s outputs for a run of blocks.
+pub struct HostVerify {
+    pub status: Vec<u8>,
+    pub crc: Vec<u32>,
+    pub count: Vec<u32>,
+    /// the decoded extents and bytes (every block's Uncompress form) when the run holds snappy /
+    /// lz4 blocks; `None` when the run itself is the Uncompress form
+    pub plain: Option<(Vec<u64>, Bytes)>,
+}
+
+impl GpuDecoder {
+    /// The device's verdict on `n` blocks of `region` (`ext` holds n + 1 offsets), the decoded
+    /// columns left on the device; for a run with snappy / lz4 blocks also their decompressed
+    /// bytes (grown until they fit: TPZ_ERR_NOMEM returns the size needed in h_dext[n]).
+    pub fn verify_host(&self, region: &[u8], ext: &[u64]) -> Result<HostVerify> {
+        let n = ext.len() - 1;
+        let codec = (0..n).any(|i| ext[i + 1] > ext[i] && matches!(region[ext[i + 1] as usize - 1], 2 | 3));
+        let mut out = HostVerify { status: vec![0; n], crc: vec![0; n], count: vec![0; n], plain: None };
+        let mut dext = vec![0u64; n + 1];
+        let mut plain: Vec<u8> = Vec::new();
+        if codec {
+            let mut bound = 0u64;
+            check(unsafe { ffi::tpz_host_decoded_bound(region.as_ptr(), ext.as_ptr(), n as u32, &mut bound) },
+                  "tpz_host_decoded_bound")?;
+            plain.resize(bound as usize, 0);
+        }
+        loop {
+            let rc = unsafe {
+                ffi::tpz_verify_blocks_host(self.ctx, region.as_ptr(), ext.as_ptr(), n as u32,
+                                            out.status.as_mut_ptr(), out.crc.as_mut_ptr(),
+                                            out.count.as_mut_ptr(),
+                                            if codec { plain.as_mut_ptr() } else { std::ptr::null_mut() },
+                                            plain.len() as u64, dext.as_mut_ptr(), 0)
+            };
+            match rc {
+                ffi::TPZ_SUCCESS => break,
+                ffi::TPZ_ERR_NOMEM if codec => plain.resize(plain.len().max(dext[n] as usize), 0),
+                e => check(e, "tpz_verify_blocks_host")?,
+            }
+        }
+        if codec {
+            plain.truncate(dext[n] as usize);
+            out.plain = Some((dext, Bytes::from(plain)));
+        }
+        Ok(out)
+    }
+}
+
 impl Drop for GpuDecoder {
     fn drop(&mut self) {
         unsafe { ffi::tpz_ctx_destroy(self.ctx) };
@@ -130,19 +182,24 @@ impl SsTable {
     pub fn read_blocks_gpu(&self, gpu: &GpuDecoder, first: usize, n: usize) -> Vec<Result<Arc<Block>>> {
         let off = |i: usize| self.block_metas.get(i).map(|m| m.offset).unwrap_or(self.block_meta_offset);
         let lo = off(first);
+        // Vec -> Bytes keeps the allocation: every Uncompress block's Block is a slice of it
         let region = match self.file.read(lo, off(first + n) - lo) {
-            Ok(r) => r,
+            Ok(r) => Bytes::from(r),
             Err(e) => return (0..n).map(|_| Err(anyhow!("{e}"))).collect(),
         };
         let ext: Vec<u64> = (first..=first + n).map(|i| (off(i) - lo) as u64).collect();
-        let out = match gpu.decode_host(&region, &ext) {
-            Ok(o) => o,
+        let v = match gpu.verify_host(&region, &ext) {
+            Ok(v) => v,
             Err(e) => return (0..n).map(|_| Err(anyhow!("{e}"))).collect(),
         };
         (0..n)
-            .map(|i| match out.status[i] {
+            .map(|i| match v.status[i] {
                 ffi::TPZ_BLOCK_OK | ffi::TPZ_BLOCK_OK_SPILLED | ffi::TPZ_BLOCK_BAD_ENTRY => {
-                    Ok(Arc::new(Block::from_columns(&out, i)))
+                    let b = match &v.plain {
+                        Some((dext, plain)) => plain.slice(dext[i] as usize..dext[i + 1] as usize),
+                        None => region.slice(ext[i] as usize..ext[i + 1] as usize),
+                    };
+                    Ok(Arc::new(Block::from_verified(&b)))
                 }
                 ffi::TPZ_BLOCK_MALFORMED => panic!("block {} is malformed", first + i),
                 st => {
@@ -150,7 +207,7 @@ impl SsTable {
                     // carries the stored CRC, which sits inside the decompressed form of a
                     // snappy / lz4 block); the device status and CRC agree with it
                     let b = &region[ext[i] as usize..ext[i + 1] as usize];
-                    Err(Block::decode(b).err().unwrap_or_else(|| block_error(st, 0, out.crc[i])))
+                    Err(Block::decode(b).err().unwrap_or_else(|| block_error(st, 0, v.crc[i])))
                 }
             })
             .collect()

@@ -172,6 +172,10 @@ extern "C" {
     pub fn tpz_decode_blocks_host(ctx: *mut TpzCtx, h_src: *const u8, h_ext: *const u64,
                                   n_blocks: u32, out: *const TpzHostColumns,
                                   chunk_blocks: u32) -> TpzErr;
+    pub fn tpz_verify_blocks_host(ctx: *mut TpzCtx, h_src: *const u8, h_ext: *const u64,
+                                  n_blocks: u32, h_status: *mut u8, h_crc: *mut u32,
+                                  h_count: *mut u32, h_plain: *mut u8, plain_cap: u64,
+                                  h_dext: *mut u64, chunk_blocks: u32) -> TpzErr;
     pub fn tpz_crc32_ranges(ctx: *mut TpzCtx, ranges: *const TpzBatch, d_crc: *mut u32,
                             stream: *mut c_void) -> TpzErr;
     pub fn tpz_verify_files(ctx: *mut TpzCtx, files: *const TpzBatch, d_crc: *mut u32,

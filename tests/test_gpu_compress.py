@@ -73,6 +73,12 @@ def test_configs_round_trip(ctx, kind, codec):
     check_round_trip(src, ext, out, oext, codec)
     if kind == "4kc":   # compressible shape: the codec pays off
         assert oext[-1] < 0.8 * ext[-1], oext[-1] / ext[-1]
+    if kind == "64k":   # payloads past the 4,336-byte LDS window: literal elements only
+        # (tpz_gpu.h, tpz_compress_blocks): a valid stream a few bytes larger than the block
+        d_in = np.diff(np.asarray(ext, np.int64))
+        d_out = np.diff(np.asarray(oext, np.int64))
+        assert (d_out >= d_in).all(), "a long block was compressed"
+        assert (d_out <= d_in + 8 + d_in // 255).all(), (d_out - d_in).max()
 
 
 @pytest.mark.parametrize("codec", [2, 3])

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: pipelined copy+CRC with the previous block's combine spread over its stages
+# (TPZ_ABL_PIPED) — parity through the piped build, then A/B: c8b18cf (HEAD before), full (this
+# tree's default: combine at the block's exit), piped; on chip too.
+set -o pipefail
+OUT=gpurun_out/r5e
+mkdir -p $OUT
+TPZ_LIB_PATH=$PWD/topazdb_amd/variants/libtpz_gpu_piped.so timeout -k 10 400 python3 -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_gpu_flat.py tests/test_gpu_exact.py tests/test_gpu_bad_entry.py tests/test_gpu_spill.py -x -q --timeout 120 --timeout-method thread > $OUT/t.log 2>&1 || { tail -40 $OUT/t.log; exit 1; }
+tail -2 $OUT/t.log
+timeout -k 10 300 python3 -u tools/abl_multi.py --rounds 5 c8b18cf full piped onchip onchip_piped > $OUT/abl.jsonl 2> $OUT/abl.err || { tail -20 $OUT/abl.err; exit 1; }
+cat $OUT/abl.jsonl
+timeout -k 10 300 python3 -u tools/abl_multi.py --rounds 3 --config zipf c8b18cf full piped > $OUT/abl_zipf.jsonl 2> $OUT/abl_zipf.err || { tail -20 $OUT/abl_zipf.err; exit 1; }
+cat $OUT/abl_zipf.jsonl

@@ -153,6 +153,10 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
+        L.tpz_verify_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_uint64, C.c_void_p, C.c_uint32]
+        L.tpz_verify_blocks_host.restype = C.c_int
         L.tpz_host_decoded_bound.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(C.c_uint64)]
         L.tpz_host_decoded_bound.restype = C.c_int
@@ -312,6 +316,41 @@ class Context:
         if rc not in (SUCCESS, ERR_NOMEM):
             check(rc, "tpz_decode_blocks_host")
         return rc
+
+    def verify_host(self, region, ext, chunk_blocks: int = 0):
+        """tpz_verify_blocks_host over blocks in host memory: the device's verdict (status, crc,
+        count) with the decoded columns left on the device, and for a run with snappy / lz4
+        blocks the decoded extents and bytes (every block's Uncompress form). Returns
+        (status, crc, count, dext, plain); dext / plain are None for an Uncompress run."""
+        import numpy as np
+        src = np.ascontiguousarray(np.frombuffer(bytes(region), np.uint8) if not isinstance(region, np.ndarray) else region, np.uint8)
+        e = np.ascontiguousarray(ext, np.uint64)
+        n = len(e) - 1
+        status = np.zeros(n, np.uint8)
+        crc = np.zeros(n, np.uint32)
+        count = np.zeros(n, np.uint32)
+        dext = np.zeros(n + 1, np.uint64)
+        codec = bool(n) and any(e[i + 1] > e[i] and src[int(e[i + 1]) - 1] in (2, 3) for i in range(n))
+        plain = None
+        if codec:
+            bound = C.c_uint64(0)
+            check(lib().tpz_host_decoded_bound(C.c_void_p(src.ctypes.data), C.c_void_p(e.ctypes.data), n,
+                                               C.byref(bound)), "tpz_host_decoded_bound")
+            plain = np.zeros(max(int(bound.value), 1), np.uint8)
+        while True:
+            rc = lib().tpz_verify_blocks_host(
+                self.handle, C.c_void_p(src.ctypes.data if src.size else None), C.c_void_p(e.ctypes.data), n,
+                C.c_void_p(status.ctypes.data), C.c_void_p(crc.ctypes.data),
+                C.c_void_p(count.ctypes.data), C.c_void_p(plain.ctypes.data if codec else None),
+                plain.size if codec else 0, C.c_void_p(dext.ctypes.data), chunk_blocks)
+            if rc == ERR_NOMEM and codec:
+                plain = np.zeros(max(int(dext[n]), plain.size + 1), np.uint8)
+                continue
+            check(rc, "tpz_verify_blocks_host")
+            break
+        if not codec:
+            return status, crc, count, None, None
+        return status, crc, count, dext, plain[:int(dext[n])]
 
     def decompressed_sizes_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
                                 d_size: int, stream: int = 0) -> None:

@@ -376,12 +376,15 @@ tpz_err tpz_decode_check(tpz_ctx* c, void* stream) {
     auto it = c->ws.find(stream);
     if (it != c->ws.end()) tail = it->second.d_tail;
   }
-  TPZ_HIP(hipStreamSynchronize((hipStream_t)stream));
-  if (!tail) return TPZ_SUCCESS;
+  hipStream_t s = (hipStream_t)stream;
+  if (!tail) return hip_fail(hipStreamSynchronize(s), "tpz_decode_check");
+  // read and clear the stream's flag in stream order (after every decode queued before it; the
+  // null stream is not involved), then wait for both
   uint32_t flag = 0;
-  TPZ_HIP(hipMemcpy(&flag, tail + tpz::kTailError, 4, hipMemcpyDeviceToHost));
+  TPZ_HIP(hipMemcpyAsync(&flag, tail + tpz::kTailError, 4, hipMemcpyDeviceToHost, s));
+  TPZ_HIP(hipMemsetAsync(tail + tpz::kTailError, 0, 4, s));
+  TPZ_HIP(hipStreamSynchronize(s));
   if (!flag) return TPZ_SUCCESS;
-  TPZ_HIP(hipMemset(tail + tpz::kTailError, 0, 4));
   g_last_error = "tpz_decode_blocks: a tail workgroup's wait for the big path timed out; spill "
                  "blocks of a batch on this stream may be undecoded";
   return TPZ_ERR_INTERNAL;
@@ -566,6 +569,9 @@ tpz_err tpz_compress_blocks(tpz_ctx* c, const tpz_batch* b, uint32_t codec, uint
                             uint64_t* d_dst_ext, void* stream) {
   if (!c || !b || !d_dst_ext || (codec != 2 && codec != 3)) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks && (!b->d_src || !b->d_ext || !d_dst)) return TPZ_ERR_INVALID_ARG;
+  // the match finder loads the blocks in aligned 16-byte pieces and the pack kernel stores them
+  // the same way (tpz_compress.hip): both buffers 16-byte aligned, as tpz_decode_blocks_flat asks
+  if (((uintptr_t)b->d_src | (uintptr_t)d_dst) & 15u) return TPZ_ERR_INVALID_ARG;
   TPZ_HIP(hipSetDevice(c->device));
   const uint64_t scratch = tpz::compress_scratch_bytes(b->src_bytes, b->n_blocks);
   const uint64_t parts = (uint64_t)tpz::flat_scan_parts_words(b->n_blocks);

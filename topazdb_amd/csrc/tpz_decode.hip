@@ -904,6 +904,36 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   return crc_lane_value(tab, L);   // the lane's raw run CRC: crc_combine gives R0 of the range
 }
 
+// The wave path defers a block's CRC combine and status write into the next block's decode
+// (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
+// and parse round trips instead of ending the block's dependent chain.
+struct PendingCrc {
+  u32 live;            // (uniform) a block's combine is pending
+  u32 b, st, cnt, stored, k;
+  u32 lc;              // per lane: the raw CRC of the lane's 80-byte run
+};
+
+// (Every decode_block exit that does not hand the pending combine to copy_crc_piped runs it.)
+__device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
+  if (!pd.live) return;
+  const u32 R = crc_combine(tab, pd.lc);
+  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
+                                                                   : ~crc_unshift_small(tab, R, pd.k);
+  const bool ok = crc == pd.stored;                                            // checksum.rs:17
+  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
+  pd.live = 0;
+}
+
+struct FinishAtExit {
+  const u32* tab;
+  const Out& o;
+  PendingCrc& pd;
+  bool on;
+  __device__ __forceinline__ ~FinishAtExit() {
+    if (on) finish_pending(tab, o, pd);
+  }
+};
+
 // ------------------------------------------------------------------ pipelined copy + CRC
 // LDS reads return in issue order and `s_waitcnt lgkmcnt(N)` waits for all but the N youngest,
 // so waiting for one read also waits for every read issued before it. copy_crc_fused interleaves
@@ -982,10 +1012,41 @@ struct PWin {
   Gath ga, gn;
 };
 
+// The previous block's CRC combine (PendingCrc, crc_combine's six tree levels) runs between the
+// stages too, one level per stage: level J's lookups are issued in one stage and used (XOR, DPP
+// hand-down) in the next, so its six dependent LDS round trips overlap the copy's and the CRC's.
+template <int J>
+__device__ __forceinline__ bool comb_lane(u32 lane) {
+  return J == 0 ? (lane & 1u) == 1u : J == 1 ? (lane & 3u) == 2u : J == 2 ? (lane & 7u) == 4u
+       : J == 3 ? (lane & 15u) == 8u : J == 4 ? (lane & 31u) == 16u : (lane & 47u) == 32u;
+}
+struct CombLv {
+  u32 r0, r1, r2, r3;
+};
+template <int J>
+__device__ __forceinline__ CombLv comb_issue(const u32* tab, u32 A) {
+  CombLv c{0u, 0u, 0u, 0u};
+  if (comb_lane<J>(lane_id())) {        // exec-masked: fewer lanes touch LDS at each level
+    constexpr int b0 = 16 + 4 * J;
+    c.r0 = tlook(tab, b0, A & 0xFF);
+    c.r1 = tlook(tab, b0 + 1, (A >> 8) & 0xFF);
+    c.r2 = tlook(tab, b0 + 2, (A >> 16) & 0xFF);
+    c.r3 = tlook(tab, b0 + 3, A >> 24);
+  }
+  return c;
+}
+template <int J>
+__device__ __forceinline__ u32 comb_use(u32 A, const CombLv& c) {
+  if (comb_lane<J>(lane_id())) A = xor3(c.r0, c.r1, c.r2) ^ c.r3;
+  if (J < 4) A ^= dpp<kRowShl + (1 << (J < 4 ? J : 0))>(A);
+  return A;
+}
+
 template <bool FLAT>
 __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
-                                              const FlatOut& D, const uint8_t* win, int pb, u32 Pa) {
+                                              const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
+                                              const Out& o, PendingCrc& pd) {
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
@@ -1009,6 +1070,10 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
     W[w].m = map[min(c, (u32)kWaveMapLen - 1)];
   }
   u32x4v dA = dread(0);
+  // the pending combine: level 0, and shift_k(~stored), the value R is compared with
+  u32 cA = pd.lc;
+  CombLv cl = comb_issue<0>(tab, cA);
+  const u32 want = crc_shift_small(tab, ~pd.stored, pd.k);
   TPZ_SB();
   // B: prefix max per window (independent DPP chains), carries, entries j and j + 1
 #pragma unroll
@@ -1022,10 +1087,14 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   }
 #pragma unroll
   for (int w = 0; w < 4; w++) col.get2(min(W[w].j, F.last), W[w].e0, W[w].d0, W[w].e1, W[w].d1);
+  cA = comb_use<0>(cA, cl);
+  cl = comb_issue<1>(tab, cA);
   TPZ_SB();
   // C: lookups of step 0, data of step 1
   Look16 LK = look_issue(tab, dA, 0u);
   u32x4v dB = dread(1);
+  cA = comb_use<1>(cA, cl);
+  cl = comb_issue<2>(tab, cA);
   TPZ_SB();
   u32 rare = 0;
   auto gissue = [&](PWin& P, u32 w) {
@@ -1050,20 +1119,34 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   };
   // D: gathers of window 0
   gissue(W[0], 0);
+  cA = comb_use<2>(cA, cl);
+  cl = comb_issue<3>(tab, cA);
   TPZ_SB();
   u32 crc = 0;
   // E: CRC step 1 ; F: window 0 out, window 1 gathers
   crc = look_xor(LK);
   LK = look_issue(tab, dB, crc);
   dA = dread(2);
+  cA = comb_use<3>(cA, cl);
+  cl = comb_issue<4>(tab, cA);
   TPZ_SB();
   finish(W[0], 0);
   gissue(W[1], 1);
+  cA = comb_use<4>(cA, cl);
+  cl = comb_issue<5>(tab, cA);
   TPZ_SB();
   // G: CRC step 2 ; H: window 1 out, window 2 gathers
   crc = look_xor(LK);
   LK = look_issue(tab, dA, crc);
   dB = dread(3);
+  cA = comb_use<5>(cA, cl);
+  if (pd.live) {   // the previous block's status, count and CRC (finish_pending)
+    const u32 R = readlane(cA, 0) ^ readlane(cA, 16) ^ readlane(cA, 32) ^ readlane(cA, 48);
+    const u32 crc_prev = R == want ? pd.stored : ~crc_unshift_small(tab, R, pd.k);
+    const bool ok = crc_prev == pd.stored;                                     // checksum.rs:17
+    put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc_prev);
+    pd.live = 0;
+  }
   TPZ_SB();
   finish(W[1], 1);
   gissue(W[2], 2);
@@ -1099,25 +1182,6 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
 }
 
 
-// The wave path defers a block's CRC combine and status write into the next block's decode
-// (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
-// and parse round trips instead of ending the block's dependent chain.
-struct PendingCrc {
-  u32 live;            // (uniform) a block's combine is pending
-  u32 b, st, cnt, stored, k;
-  u32 lc;              // per lane: the raw CRC of the lane's 80-byte run
-};
-
-__device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
-  if (!pd.live) return;
-  const u32 R = crc_combine(tab, pd.lc);
-  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
-                                                                   : ~crc_unshift_small(tab, R, pd.k);
-  const bool ok = crc == pd.stored;                                            // checksum.rs:17
-  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
-  pd.live = 0;
-}
-
 // Decode the block whose bytes are at win[a0 .. a0+len) (LDS), block index b. `map` is the
 // stream's chunk map (kMapLen slots, LDS), `col` its entry table.
 template <class Col, class MapT, int kMapLen, bool BIG, bool FLAT = false>
@@ -1145,7 +1209,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     e_ok = len >= 7 && lane < n && Pn >= 2 + 2 * n && e_off + 2 <= Pn - 2 - 2 * n;
     e_kl = lds_be16(win, e_ok ? db0 + e_off : a0);
   }
-  finish_pending(tab, o, pd);     // the previous block's combine, behind this block's reads
+  // The previous block's combine: copy_crc_piped runs it level by level between its own stages;
+  // every other exit of this block runs it whole (FinishAtExit).
+  FinishAtExit fin{tab, o, pd, true};
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
   if (tag != 1) { put_meta(o, b, TPZ_BLOCK_UNSUPPORTED_CODEC, 0, 0); return; }
@@ -1328,19 +1394,25 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
 #else
     u32 R;
     if (!BIG && fuse) {
-      const u32 lc = f_short
+      u32 lc;
+      fin.on = false;      // the previous block's combine runs here, before pd is reused
+#ifdef TPZ_ABL_PIPED
+      if (!f_short) {
+        lc = copy_crc_piped<FLAT>(tab, *reinterpret_cast<const ColSmall*>(&col),
+                                  reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, fo,
+                                  win, pb, P + k, o, pd);
+      } else
+#endif
+      {
+        finish_pending(tab, o, pd);
+        lc = f_short
           ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                        fo, win, pb, P + k, kshift, S, f_w3)
-#ifndef TPZ_ABL_PIPED
           : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                         fo, win, pb, P + k, kshift, S);
-#else
-          : copy_crc_piped<FLAT>(tab, *reinterpret_cast<const ColSmall*>(&col),
-                                 reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, fo, win,
-                                 pb, P + k);
-#endif
+      }
       pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
       return;
     } else {

@@ -235,6 +235,16 @@ extern "C" tpz_err tpz_host_decoded_bound(const uint8_t* h_src, const uint64_t* 
   return TPZ_SUCCESS;
 }
 
+// The verify-only outputs (tpz_verify_blocks_host): the columns stay on the device; the host gets
+// each block's status / count / crc and, for a batch with snappy / lz4 blocks, the decoded bytes.
+struct VerifyOut {
+  uint8_t* h_plain;
+  uint64_t plain_cap;
+};
+
+static tpz_err host_pipeline(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext, uint32_t n,
+                             const tpz_host_columns* o, uint32_t chunk_blocks, const VerifyOut* vo);
+
 extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
                                           const uint64_t* h_ext, uint32_t n,
                                           const tpz_host_columns* o, uint32_t chunk_blocks) {
@@ -242,6 +252,30 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
       !o->h_spill_off || !o->h_spill_used || (n && (!h_src || !o->h_data)) ||
       (o->ends_cap && !o->h_ends) || (o->spill_cap && !o->h_spill))
     return TPZ_ERR_INVALID_ARG;
+  return host_pipeline(ctx, h_src, h_ext, n, o, chunk_blocks, nullptr);
+}
+
+extern "C" tpz_err tpz_verify_blocks_host(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext,
+                                          uint32_t n, uint8_t* h_status, uint32_t* h_crc,
+                                          uint32_t* h_count, uint8_t* h_plain, uint64_t plain_cap,
+                                          uint64_t* h_dext, uint32_t chunk_blocks) {
+  if (!ctx || !h_ext || !h_status || !h_crc || !h_count || (n && !h_src) ||
+      (plain_cap && !h_plain))
+    return TPZ_ERR_INVALID_ARG;
+  uint64_t used = 0;
+  tpz_host_columns o{};
+  o.h_count = h_count;
+  o.h_status = h_status;
+  o.h_crc = h_crc;
+  o.h_spill_used = &used;
+  o.h_dext = h_dext;
+  const VerifyOut vo{h_plain, plain_cap};
+  return host_pipeline(ctx, h_src, h_ext, n, &o, chunk_blocks, &vo);
+}
+
+static tpz_err host_pipeline(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t* h_ext, uint32_t n,
+                             const tpz_host_columns* o, uint32_t chunk_blocks, const VerifyOut* vo) {
+  const bool verify = vo != nullptr;
   // One pass over the extents (non-decreasing) and the blocks' tag bytes (a snappy / lz4 block
   // anywhere: the decoded extents differ from h_ext for the whole batch), on up to 16 host
   // threads: the tags sit one per block, a page apart, and a single-thread walk over 2^20 of them
@@ -274,9 +308,11 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     if (bad) return TPZ_ERR_INVALID_ARG;
     codec = any_codec;
   }
-  o->h_first[0] = 0;
+  if (o->h_first) o->h_first[0] = 0;
   *o->h_spill_used = 0;
   if (codec && !o->h_dext) return TPZ_ERR_INVALID_ARG;
+  // verify mode: a codec batch's decoded bytes come back (the Uncompress form of every block)
+  if (verify && codec && !vo->h_plain) return TPZ_ERR_INVALID_ARG;
   if (o->h_dext && !codec)
     for (uint32_t i = 0; i <= n; i++) o->h_dext[i] = h_ext[i];
   if (n == 0) return TPZ_SUCCESS;
@@ -294,11 +330,15 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     const uint32_t hi = std::min(n, lo + cb);
     max_span = std::max<uint64_t>(max_span, h_ext[hi] - (h_ext[lo] - h_ext[lo] % 384));
   }
-  Pin pin_src, pin_data, pin_ends, pin_spill;
+  Pin pin_src, pin_data, pin_ends, pin_spill, pin_plain;
   pin_src.pin(h_src + h_ext[0], h_ext[n] - h_ext[0]);
-  pin_data.pin(o->h_data, data_cap);
-  pin_ends.pin(o->h_ends, o->ends_cap * 4);
-  pin_spill.pin(o->h_spill, o->spill_cap);
+  if (!verify) {
+    pin_data.pin(o->h_data, data_cap);
+    pin_ends.pin(o->h_ends, o->ends_cap * 4);
+    pin_spill.pin(o->h_spill, o->spill_cap);
+  } else if (codec) {
+    pin_plain.pin(vo->h_plain, vo->plain_cap);
+  }
 
   // a pipeline of the context's pool (or a new one, returned to the pool at the end)
   TpzHostPipe* P = static_cast<TpzHostPipe*>(tpz_internal_pipe_acquire(ctx));
@@ -456,7 +496,7 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   };
 
   uint64_t g_first = 0, g_spill = 0;
-  bool short_ends = false, short_spill = false, short_data = false;
+  bool short_ends = false, short_spill = false, short_data = false, short_plain = false;
   auto finish = [&](Slot& S) -> tpz_err {
     PIPE_HIP(hipEventSynchronize(S.ev));
     const uint32_t m = S.hi - S.lo;
@@ -501,11 +541,26 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
     const uint64_t dbase = codec ? S.h_meta.as<ChunkMeta>()->dbase384 : S.base;
     if (codec)
       for (uint32_t i = 0; i <= m; i++) o->h_dext[S.lo + i] = gx[i];
+    PIPE_HIP(hipStreamWaitEvent(P->down, S.ev, 0));
+    if (verify) {
+      // the decoded (Uncompress) bytes of a codec chunk: device byte e - dbase holds batch byte e
+      if (codec && e_hi > e_lo) {
+        if (e_hi <= vo->plain_cap)
+          PIPE_HIP(hipMemcpyAsync(vo->h_plain + e_lo, S.d_dst.as<uint8_t>() + (e_lo - dbase),
+                                  e_hi - e_lo, hipMemcpyDeviceToHost, P->down));
+        else
+          short_plain = true;
+      }
+      std::memcpy(o->h_count + S.lo, S.h_count.p, m * 4);
+      std::memcpy(o->h_status + S.lo, S.h_status.p, m);
+      std::memcpy(o->h_crc + S.lo, S.h_crc.p, m * 4);
+      PIPE_HIP(hipEventRecord(S.ev_down, P->down));
+      return TPZ_SUCCESS;
+    }
     // the chunk's own slots, into the batch's slotted layout
     const uint64_t d0 = tpz_slot_base(e_lo - dbase, 0);
     const uint64_t d1 = tpz_slot_base(e_hi - dbase, m);
     const uint64_t h0 = tpz_slot_base(e_lo, S.lo);
-    PIPE_HIP(hipStreamWaitEvent(P->down, S.ev, 0));
     if (h0 + (d1 - d0) <= data_cap) {
       PIPE_HIP(hipMemcpyAsync(o->h_data + h0, S.d_data.as<uint8_t>() + d0, d1 - d0,
                               hipMemcpyDeviceToHost, P->down));
@@ -583,5 +638,5 @@ extern "C" tpz_err tpz_decode_blocks_host(tpz_ctx* ctx, const uint8_t* h_src,
   // every chunk decoded to completion (tpz_decode_check: no timed-out tail wait on comp)
   const tpz_err chk = tpz_decode_check(ctx, P->comp);
   if (chk != TPZ_SUCCESS) return chk;
-  return (short_ends || short_spill || short_data) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
+  return (short_ends || short_spill || short_data || short_plain) ? TPZ_ERR_NOMEM : TPZ_SUCCESS;
 }

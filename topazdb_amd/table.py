@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from ._lib import (BLOCK_BAD_ENTRY, BLOCK_BAD_TAG, BLOCK_CHECKSUM_MISMATCH, BLOCK_EMPTY,
-                   BLOCK_MALFORMED, BLOCK_OK, ENTRY_BAD_KEY, ENTRY_OK, Context)
+                   BLOCK_MALFORMED, BLOCK_OK, ENTRY_BAD_KEY, ENTRY_BAD_VALUE, ENTRY_OK, Context)
 from .batch import DeviceBatch, decode_batch, decompress_batch, exact_columns, verify_files
 
 CHECKSUM_SIZE = 4  # src/checksum.rs:4
@@ -109,6 +109,42 @@ class Block:
         return b"".join(struct.pack(">H", len(k)) + k + struct.pack(">H", len(v)) + v
                         for k, v in ((self.key_at(i), self.value_at(i))
                                      for i in range(self.num_entries)))
+
+    @staticmethod
+    def from_verified(b: bytes) -> "Block":
+        """The reference's Block::decode (src/block.rs:46-65) of a block's Uncompress form `b`
+        (payload | crc | tag) whose tag, CRC and header the device has verified
+        (tpz_verify_blocks_host: OK, OK_SPILLED or BAD_ENTRY, so len(b) >= 7 + 2n): n, the n
+        big-endian offsets, data = payload[2 + 2n:] — the view rust/topazdb-gpu/src/block/gpu.rs
+        Block::from_verified builds without a copy. Each entry as BlockIterator::seek_to reads
+        it (iterator.rs:74-82): an offset at or past data's end, or a key running past it, is
+        ENTRY_BAD_KEY; a value length or value running past it, ENTRY_BAD_VALUE (its key reads)."""
+        b = bytes(b)
+        n = struct.unpack(">H", b[:2])[0]
+        offs = struct.unpack(">%dH" % n, b[2:2 + 2 * n])
+        data = b[2 + 2 * n:len(b) - 5]
+        dl = len(data)
+        keys, vals, kpos, vpos, cls = [], [], [0], [0], []
+        for off in offs:
+            k = v = b""
+            c = ENTRY_BAD_KEY
+            if off + 2 <= dl:                                            # iterator.rs:74-77
+                kl = struct.unpack(">H", data[off:off + 2])[0]
+                if off + 2 + kl <= dl:                                   # :78
+                    k = data[off + 2:off + 2 + kl]
+                    c = ENTRY_BAD_VALUE
+                    p = off + 2 + kl
+                    if p + 2 <= dl:                                      # :81
+                        vl = struct.unpack(">H", data[p:p + 2])[0]
+                        if p + 2 + vl <= dl:                             # :82
+                            v = data[p + 2:p + 2 + vl]
+                            c = ENTRY_OK
+            keys.append(k)
+            vals.append(v)
+            kpos.append(kpos[-1] + len(k))
+            vpos.append(vpos[-1] + len(v))
+            cls.append(c)
+        return Block(b"".join(keys), kpos, b"".join(vals), vpos, len(b) - 5, cls)
 
     @staticmethod
     def from_dense(d, b: int, payload_len: int | None = None) -> "Block":
