@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5: early combine after short-segment blocks (zipf) — parity (default and piped builds),
+# A/B against c8b18cf on 4k and zipf.
+set -o pipefail
+OUT=gpurun_out/r5i
+mkdir -p $OUT
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_decode.py tests/test_gpu_flat.py tests/test_gpu_bad_entry.py tests/test_gpu_fullsize.py -x -q --timeout 120 --timeout-method thread > $OUT/t.log 2>&1 || { tail -40 $OUT/t.log; exit 1; }
+tail -2 $OUT/t.log
+TPZ_LIB_PATH=$PWD/topazdb_amd/variants/libtpz_gpu_piped.so timeout -k 10 400 python3 -u -m pytest tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_gpu_flat.py tests/test_gpu_exact.py tests/test_gpu_bad_entry.py tests/test_gpu_spill.py -x -q --timeout 120 --timeout-method thread > $OUT/tp.log 2>&1 || { tail -40 $OUT/tp.log; exit 1; }
+tail -2 $OUT/tp.log
+timeout -k 10 300 python3 -u tools/abl_multi.py --rounds 5 c8b18cf full piped > $OUT/abl.jsonl 2> $OUT/abl.err || { tail -20 $OUT/abl.err; exit 1; }
+cat $OUT/abl.jsonl
+timeout -k 10 300 python3 -u tools/abl_multi.py --rounds 5 --config zipf c8b18cf full piped > $OUT/abl_zipf.jsonl 2> $OUT/abl_zipf.err || { tail -20 $OUT/abl_zipf.err; exit 1; }
+cat $OUT/abl_zipf.jsonl

@@ -65,8 +65,9 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
                                                uint8_t* __restrict__ meta, u64 nchunks) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 * 4096];
   const u32 lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const u64 W = (u64)gridDim.x * 16;
-  u64 c = (u64)blockIdx.x * 16 + wv;
+  const u32 wpg = blockDim.x >> 6;
+  const u64 W = (u64)gridDim.x * wpg;
+  u64 c = (u64)blockIdx.x * wpg + wv;
   uint8_t* win = lds + wv * 4096;
   uint4 v[4];
   auto load = [&](u64 cc) {
@@ -124,6 +125,80 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
     }
     c = cn;
   } while (c < nchunks);
+}
+
+// 4 KiB chunks with the piece loads and stores interleaved: piece q of chunk c is stored, then
+// piece q of the next chunk loaded (each load has a whole iteration to arrive)
+__global__ __launch_bounds__(1024) void pipeil_k(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, u64 nchunks) {
+  const u32 lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 W = (u64)gridDim.x * 16;
+  u64 c = (u64)blockIdx.x * 16 + wv;
+  if (c >= nchunks) return;
+  uint4 v[4];
+  auto ld = [&](u64 cc, int q) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(s + (cc < nchunks ? cc : 0) * 4096, cc < nchunks ? 4096 : 0);
+    v[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, q * 1024 + lane * 16, 0, 0));
+  };
+#pragma unroll
+  for (int q = 0; q < 4; q++) ld(c, q);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; q++) __builtin_amdgcn_raw_buffer_store_b32(0u, rsrc(d, 0), q * 256, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  do {
+    const u64 cn = c + W;
+    const __amdgpu_buffer_rsrc_t rd = rsrc(d + c * 4096, 4096);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 o = v[q];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rd, q * 1024 + lane * 16, 0, 0);
+      ld(cn, q);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    c = cn;
+  } while (c < nchunks);
+}
+
+// pipe_lds with the workgroup's rows of 16 chunks claimed from one global counter (one atomic
+// per row, its chunks handed to the waves through LDS): every workgroup works near the others,
+// the chunks in flight stay within a narrow window of the buffer
+__global__ __launch_bounds__(1024) void pipedyn_k(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
+                                                  u32* ctr, u64 nchunks) {
+  __shared__ u32 row_of[2];
+  __shared__ u32 taken;
+  const u32 lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const u64 nrows = (nchunks + 15) / 16;
+  // every wave takes chunk wv of row r (one row per workgroup iteration): a workgroup barrier per
+  // row hands the next row's index to all waves
+  if (threadIdx.x == 0) row_of[0] = atomicAdd(ctr, 1u);
+  __syncthreads();
+  u64 r = row_of[0];
+  uint4 v[4];
+  auto load = [&](u64 cc) {
+    const __amdgpu_buffer_rsrc_t rr = rsrc(s + (cc < nchunks ? cc : 0) * 4096, cc < nchunks ? 4096 : 0);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      v[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, q * 1024 + lane * 16, 0, 0));
+  };
+  load(r * 16 + wv);
+  int flip = 0;
+  while (r < nrows) {
+    if (threadIdx.x == 0) row_of[flip ^ 1] = atomicAdd(ctr, 1u);
+    __syncthreads();
+    const u64 rn = row_of[flip ^ 1];
+    flip ^= 1;
+    uint4 o[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) o[q] = v[q];
+    load(rn * 16 + wv);
+    const u64 c = r * 16 + wv;
+    const __amdgpu_buffer_rsrc_t rd = rsrc(d + (c < nchunks ? c : 0) * 4096, c < nchunks ? 4096 : 0);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o[q]), rd, q * 1024 + lane * 16, 0, 0);
+    r = rn;
+  }
+  (void)taken;
 }
 
 // 1 KiB pieces: each iteration one 16-byte load and one store per lane (wave w of workgroup x
@@ -199,7 +274,8 @@ int main(int argc, char** argv) {
   std::vector<std::string> vars;
   for (int i = 1; i < argc; i++) vars.push_back(argv[i]);
   if (vars.empty()) vars = {"flat", "w4k", "pipe", "pipe_lds", "pipe_meta", "pipe_w0", "pipe2", "pipe_nt", "pipe_rd",
-                            "pipe32", "pipe1k", "pipe1k32", "pipe_512", "flat", "pipe_lds"};
+                            "pipe32", "pipe1k", "pipe1k32", "pipe_512", "pipe_il", "pipe8", "pipe_dyn", "flat",
+                            "pipe_lds"};
   const u64 N = 4356833280ull;   // the 4k config's input bytes
   const u64 nch = N / 4096;
   uint8_t *a, *b, *m;
@@ -224,6 +300,9 @@ int main(int argc, char** argv) {
       else if (v == "pipe_w0") pipe_k<3><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe2") pipe2_k<<<cus, 1024>>>(a, b, nch);
       else if (v == "pipe_nt") pipe_k<4><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_il") pipeil_k<<<cus, 1024>>>(a, b, nch);
+      else if (v == "pipe8") pipe_k<1><<<cus, 512>>>(a, b, m, nch);
+      else if (v == "pipe_dyn") { (void)hipMemsetAsync(m, 0, 4); pipedyn_k<<<cus, 1024>>>(a, b, (u32*)m, nch); }
       else if (v == "pipe_rd") pipe_k<5><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe32") pipe_k<1><<<2 * cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe1k") pipe1k_k<<<cus, 1024>>>(a, b, N / 1024);

@@ -52,6 +52,8 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 // per launch (launch_decode); TPZ_WAVE_CHUNK forces one (diagnostic builds).
 static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
 constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
+// wave path: a workgroup's rows are claimed kRowAhead row slots ahead, into a ring of kRowRing
+constexpr u32 kRowAhead = 4, kRowRing = 8;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
@@ -742,6 +744,80 @@ __device__ __forceinline__ void copy_stream(const S& src, const Col& col, const 
   for (u32 w = 0; w < nw; w++) carry = copy_window(src, col, map, nk, tot, dst, map_len, w, carry);
 }
 
+// The wave path defers a block's CRC combine and status write into the next block's decode
+// (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
+// and parse round trips instead of ending the block's dependent chain.
+struct PendingCrc {
+  u32 live;            // (uniform) a block's combine is pending
+  u32 b, st, cnt, stored, k;
+  u32 lc;              // per lane: the raw CRC of the lane's 80-byte run
+  u32 early;           // (uniform) run it behind the next block's header reads (the block took
+                       // the short-segment copy, whose windows leave the combine no room)
+};
+
+// (Every decode_block exit that does not hand the pending combine to copy_crc_piped runs it.)
+__device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
+  if (!pd.live) return;
+  const u32 R = crc_combine(tab, pd.lc);
+  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
+                                                                   : ~crc_unshift_small(tab, R, pd.k);
+  const bool ok = crc == pd.stored;                                            // checksum.rs:17
+  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
+  pd.live = 0;
+}
+
+struct FinishAtExit {
+  const u32* tab;
+  const Out& o;
+  PendingCrc& pd;
+  bool on;
+  __device__ __forceinline__ ~FinishAtExit() {
+    if (on) finish_pending(tab, o, pd);
+  }
+};
+
+// The previous block's CRC combine (PendingCrc, crc_combine's six tree levels) split into steps
+// that the copy + CRC of the next block interleaves with its own: level J's lookups are issued
+// in one step and used (XOR, DPP hand-down) in the next, so its six dependent LDS round trips
+// overlap the copy's and the CRC's.
+template <int J>
+__device__ __forceinline__ bool comb_lane(u32 lane) {
+  return J == 0 ? (lane & 1u) == 1u : J == 1 ? (lane & 3u) == 2u : J == 2 ? (lane & 7u) == 4u
+       : J == 3 ? (lane & 15u) == 8u : J == 4 ? (lane & 31u) == 16u : (lane & 47u) == 32u;
+}
+struct CombLv {
+  u32 r0, r1, r2, r3;
+};
+template <int J>
+__device__ __forceinline__ CombLv comb_issue(const u32* tab, u32 A) {
+  CombLv c{0u, 0u, 0u, 0u};
+  if (comb_lane<J>(lane_id())) {        // exec-masked: fewer lanes touch LDS at each level
+    constexpr int b0 = 16 + 4 * J;
+    c.r0 = tlook(tab, b0, A & 0xFF);
+    c.r1 = tlook(tab, b0 + 1, (A >> 8) & 0xFF);
+    c.r2 = tlook(tab, b0 + 2, (A >> 16) & 0xFF);
+    c.r3 = tlook(tab, b0 + 3, A >> 24);
+  }
+  return c;
+}
+template <int J>
+__device__ __forceinline__ u32 comb_use(u32 A, const CombLv& c) {
+  if (comb_lane<J>(lane_id())) A = xor3(c.r0, c.r1, c.r2) ^ c.r3;
+  if (J < 4) A ^= dpp<kRowShl + (1 << (J < 4 ? J : 0))>(A);
+  return A;
+}
+
+// The previous block's status, count and CRC from its combined value (finish_pending's tail).
+__device__ __forceinline__ void comb_finish(const u32* tab, const Out& o, PendingCrc& pd, u32 cA,
+                                            u32 want) {
+  if (!pd.live) return;
+  const u32 R = readlane(cA, 0) ^ readlane(cA, 16) ^ readlane(cA, 32) ^ readlane(cA, 48);
+  const u32 crc = R == want ? pd.stored : ~crc_unshift_small(tab, R, pd.k);
+  const bool ok = crc == pd.stored;                                            // checksum.rs:17
+  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
+  pd.live = 0;
+}
+
 // ------------------------------------------------------------------ fused copy + CRC (wave path)
 // A wave-path block has at most 5 copy windows (stream <= len + 2 <= 4338 B) and its CRC at most
 // five 80-byte slice-by-16 steps per lane (P + k <= 4351 B). The copy's LDS round trips (map ->
@@ -859,7 +935,8 @@ template <bool SHORT, bool FLAT, class S>
 __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
-                                              u32 kshift, Stamps& St, u32 w3 = 5) {
+                                              u32 kshift, Stamps& St, u32 w3, const Out& o,
+                                              PendingCrc& pd) {
   // SHORT: windows t < w3 can hold chunks that span three segments (copy_fast3); the others
   // take copy_fast (a chunk it cannot do sends its window to copy_window, so either is exact)
   const u32 lane = lane_id();
@@ -876,18 +953,37 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   L.act = L.seg + kCrcLaneBytes > 0;
   L.c = 0;
   u32 carry = 0, rare = 0, cw[5];
+  // the previous block's combine (if still pending), two tree levels per window (comb_issue)
+  const bool pl = pd.live != 0;
+  u32 cA = pd.lc, want = 0;
+  CombLv cl{0u, 0u, 0u, 0u};
+  if (pl) {
+    cl = comb_issue<0>(tab, cA);
+    want = crc_shift_small(tab, ~pd.stored, pd.k);
+  }
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     cw[t] = carry;
     crc_step(tab, win, pb, L, t);
     carry = (SHORT && (u32)t < w3) ? copy_fast3<FLAT>(src, col, map, F, D, (u32)t, carry, rare)
                                    : copy_fast<FLAT>(src, col, map, F, D, (u32)t, carry, rare);
+    if (pl) {
+      if (t == 0) { cA = comb_use<0>(cA, cl); cl = comb_issue<1>(tab, cA); }
+      if (t == 1) { cA = comb_use<1>(cA, cl); cl = comb_issue<2>(tab, cA); }
+      if (t == 2) { cA = comb_use<2>(cA, cl); cl = comb_issue<3>(tab, cA); }
+      if (t == 3) { cA = comb_use<3>(cA, cl); cl = comb_issue<4>(tab, cA); }
+    }
   }
   cw[4] = carry;
   crc_step(tab, win, pb, L, 4);
+  if (pl) {
+    cA = comb_use<4>(cA, cl);
+    cl = comb_issue<5>(tab, cA);
+  }
   if (nw > 4)
     carry = (SHORT && 4u < w3) ? copy_fast3<FLAT>(src, col, map, F, D, 4u, carry, rare)
                                : copy_fast<FLAT>(src, col, map, F, D, 4u, carry, rare);
+  if (pl) comb_finish(tab, o, pd, comb_use<5>(cA, cl), want);
   TPZ_STAMP(St, 4);
 #ifdef TPZ_ABL_STAMPS
   St.rare += __builtin_popcount(rare);
@@ -903,36 +999,6 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
   }
   return crc_lane_value(tab, L);   // the lane's raw run CRC: crc_combine gives R0 of the range
 }
-
-// The wave path defers a block's CRC combine and status write into the next block's decode
-// (PendingCrc): the combine's six dependent LDS round trips then overlap the next block's header
-// and parse round trips instead of ending the block's dependent chain.
-struct PendingCrc {
-  u32 live;            // (uniform) a block's combine is pending
-  u32 b, st, cnt, stored, k;
-  u32 lc;              // per lane: the raw CRC of the lane's 80-byte run
-};
-
-// (Every decode_block exit that does not hand the pending combine to copy_crc_piped runs it.)
-__device__ __forceinline__ void finish_pending(const u32* tab, const Out& o, PendingCrc& pd) {
-  if (!pd.live) return;
-  const u32 R = crc_combine(tab, pd.lc);
-  const u32 crc = (R == crc_shift_small(tab, ~pd.stored, pd.k)) ? pd.stored
-                                                                   : ~crc_unshift_small(tab, R, pd.k);
-  const bool ok = crc == pd.stored;                                            // checksum.rs:17
-  put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc);
-  pd.live = 0;
-}
-
-struct FinishAtExit {
-  const u32* tab;
-  const Out& o;
-  PendingCrc& pd;
-  bool on;
-  __device__ __forceinline__ ~FinishAtExit() {
-    if (on) finish_pending(tab, o, pd);
-  }
-};
 
 // ------------------------------------------------------------------ pipelined copy + CRC
 // LDS reads return in issue order and `s_waitcnt lgkmcnt(N)` waits for all but the N youngest,
@@ -1011,36 +1077,6 @@ struct PWin {
   bool act, cross;
   Gath ga, gn;
 };
-
-// The previous block's CRC combine (PendingCrc, crc_combine's six tree levels) runs between the
-// stages too, one level per stage: level J's lookups are issued in one stage and used (XOR, DPP
-// hand-down) in the next, so its six dependent LDS round trips overlap the copy's and the CRC's.
-template <int J>
-__device__ __forceinline__ bool comb_lane(u32 lane) {
-  return J == 0 ? (lane & 1u) == 1u : J == 1 ? (lane & 3u) == 2u : J == 2 ? (lane & 7u) == 4u
-       : J == 3 ? (lane & 15u) == 8u : J == 4 ? (lane & 31u) == 16u : (lane & 47u) == 32u;
-}
-struct CombLv {
-  u32 r0, r1, r2, r3;
-};
-template <int J>
-__device__ __forceinline__ CombLv comb_issue(const u32* tab, u32 A) {
-  CombLv c{0u, 0u, 0u, 0u};
-  if (comb_lane<J>(lane_id())) {        // exec-masked: fewer lanes touch LDS at each level
-    constexpr int b0 = 16 + 4 * J;
-    c.r0 = tlook(tab, b0, A & 0xFF);
-    c.r1 = tlook(tab, b0 + 1, (A >> 8) & 0xFF);
-    c.r2 = tlook(tab, b0 + 2, (A >> 16) & 0xFF);
-    c.r3 = tlook(tab, b0 + 3, A >> 24);
-  }
-  return c;
-}
-template <int J>
-__device__ __forceinline__ u32 comb_use(u32 A, const CombLv& c) {
-  if (comb_lane<J>(lane_id())) A = xor3(c.r0, c.r1, c.r2) ^ c.r3;
-  if (J < 4) A ^= dpp<kRowShl + (1 << (J < 4 ? J : 0))>(A);
-  return A;
-}
 
 template <bool FLAT>
 __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& col,
@@ -1140,13 +1176,7 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   LK = look_issue(tab, dA, crc);
   dB = dread(3);
   cA = comb_use<5>(cA, cl);
-  if (pd.live) {   // the previous block's status, count and CRC (finish_pending)
-    const u32 R = readlane(cA, 0) ^ readlane(cA, 16) ^ readlane(cA, 32) ^ readlane(cA, 48);
-    const u32 crc_prev = R == want ? pd.stored : ~crc_unshift_small(tab, R, pd.k);
-    const bool ok = crc_prev == pd.stored;                                     // checksum.rs:17
-    put_meta(o, pd.b, ok ? pd.st : TPZ_BLOCK_CHECKSUM_MISMATCH, ok ? pd.cnt : 0u, crc_prev);
-    pd.live = 0;
-  }
+  comb_finish(tab, o, pd, cA, want);
   TPZ_SB();
   finish(W[1], 1);
   gissue(W[2], 2);
@@ -1209,8 +1239,11 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     e_ok = len >= 7 && lane < n && Pn >= 2 + 2 * n && e_off + 2 <= Pn - 2 - 2 * n;
     e_kl = lds_be16(win, e_ok ? db0 + e_off : a0);
   }
-  // The previous block's combine: copy_crc_piped runs it level by level between its own stages;
-  // every other exit of this block runs it whole (FinishAtExit).
+  // The previous block's combine: after a short-segment block it runs here, behind this block's
+  // header reads (whose round trips it overlaps); otherwise this block's copy runs it level by
+  // level between its own steps (copy_crc_piped / copy_crc_fused), and every other exit of this
+  // block runs it whole (FinishAtExit).
+  if (pd.early) finish_pending(tab, o, pd);
   FinishAtExit fin{tab, o, pd, true};
   if (len == 0) { put_meta(o, b, TPZ_BLOCK_EMPTY, 0, 0); return; }           // compress.rs:96
   if (tag == 0 || tag > 3) { put_meta(o, b, TPZ_BLOCK_BAD_TAG, 0, 0); return; } // :44-53,102
@@ -1396,7 +1429,7 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     if (!BIG && fuse) {
       u32 lc;
       fin.on = false;      // the previous block's combine runs here, before pd is reused
-#ifdef TPZ_ABL_PIPED
+#ifndef TPZ_ABL_FUSED
       if (!f_short) {
         lc = copy_crc_piped<FLAT>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                   reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, fo,
@@ -1404,16 +1437,15 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       } else
 #endif
       {
-        finish_pending(tab, o, pd);
         lc = f_short
           ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
-                                       fo, win, pb, P + k, kshift, S, f_w3)
+                                       fo, win, pb, P + k, kshift, S, f_w3, o, pd)
           : copy_crc_fused<false, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
                                         reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
-                                        fo, win, pb, P + k, kshift, S);
+                                        fo, win, pb, P + k, kshift, S, 5u, o, pd);
       }
-      pd = PendingCrc{1u, b, st, cnt, stored, k, lc};   // combined during the next block
+      pd = PendingCrc{1u, b, st, cnt, stored, k, lc, f_short ? 1u : 0u};   // combined during the next block
       return;
     } else {
         R = wave_crc(tab, win, pb, P + k);
@@ -1489,6 +1521,8 @@ struct Params {
   u32 xp[kBigSuper];  // big path: x^(8 * 5120 r) mod P, the shift of CRC super-round r
   u32 lane_shift[64]; // wave path: x^(8 * 80 l) mod P, lane l's CRC run to the range end
   u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
+  u32* row_ctr;       // wave path: the rows of 16 blocks claimed so far (tail + kTailRow)
+  u32* err;           // sticky error word (tail + kTailError)
 };
 
 
@@ -1508,6 +1542,15 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   u32* tab = reinterpret_cast<u32*>(lds);
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   __shared__ Out out_lds;             // the worklist pointers for the rare paths (see above)
+  // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
+  // row_slot[s % kRowRing] == s (see claim_chunk)
+  __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
+  if (threadIdx.x < kRowAhead) {      // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
+    row_val[threadIdx.x] = atomicAdd(p.row_ctr, 1u);
+    row_slot[threadIdx.x] = threadIdx.x;
+  } else if (threadIdx.x < kRowRing) {
+    row_slot[threadIdx.x] = ~0u;
+  }
   if (threadIdx.x == 0) {             // (load_tables' barrier publishes both)
     chunk_next = 0;
     out_lds = p.out;
@@ -1534,30 +1577,71 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   S.last = stamp_now();
 #endif
 
-  // The workgroup's blocks are the rows q nw + kWavesPerWG blockIdx.x + [0, kWavesPerWG), in
-  // chunks of kChunk consecutive blocks. A wave takes the next chunk from an LDS counter when it
-  // finishes one: the waves of a CU do not run at one speed (with a fixed block per wave, the
-  // first four waves of each workgroup finished at 1.66 ms and the last four at 2.21 ms of a
-  // 2.26 ms launch, tools/wave_ends.py), so a fixed split left the fast waves idle while the slow
-  // ones finished. Lane l of a chunk's extent group holds ext[] of the chunk's block l (loaded
-  // one chunk ahead, so a block's extent is two readlanes instead of a memory round trip).
+  // Rows of 16 consecutive blocks, claimed by the workgroups from one global counter, so that
+  // every workgroup works near the others and the batch is read and written through a narrow
+  // moving window (static rows, r * grid + blockIdx.x, let the workgroups drift apart and spread
+  // the accesses in flight over the buffer: a persistent 4 KiB-chunk copy ran at 5.75 TB/s with
+  // static rows and 6.24 TB/s with claimed rows, the one-shot copy's rate; tools/ubench_pipe.hip,
+  // profiles/r5/). Within a workgroup the rows fill row slots 0, 1, 2, ...; a wave takes the
+  // next chunk of kChunk consecutive blocks from an LDS counter when it finishes one: the waves
+  // of a CU do not run at one speed (with a fixed block per wave, the first four waves of each
+  // workgroup finished at 1.66 ms and the last four at 2.21 ms of a 2.26 ms launch,
+  // tools/wave_ends.py), so a fixed split left the fast waves idle while the slow ones finished.
+  // Lane l of a chunk's extent group holds ext[] of the chunk's block l (loaded one chunk ahead,
+  // so a block's extent is two readlanes instead of a memory round trip).
 #ifdef TPZ_WAVE_CHUNK
   const u32 cshift = __builtin_ctz((u32)TPZ_WAVE_CHUNK);
 #else
   const u32 cshift = uni(p.chunk_shift);
 #endif
   const u32 kChunk = 1u << cshift, rshift = kRowShift - cshift;   // chunks per row: 2^rshift
-  // (saturated at n_blocks: a chunk past the batch is empty)
-  const u32 row0 = blockIdx.x * kWavesPerWG;
-  auto chunk_first = [&](u32 q) -> u32 {
-    const u64 f = (u64)(q >> rshift) * nw + row0 + ((q & ((1u << rshift) - 1u)) << cshift);
-    return f < p.n_blocks ? (u32)f : p.n_blocks;
+  // claim_chunk returns the chunk's first block (saturated at n_blocks: a chunk past the batch
+  // is empty). The wave that takes the first chunk of row slot s claims the row of slot
+  // s + kRowAhead from the global counter and publishes it at its next claim (the atomic's value
+  // has arrived by then: the prefetch wait at the top of the loop covers it), long before any
+  // wave reaches that slot (kRowAhead - 1 rows of claims later); a reader that gets there first
+  // waits for it (bounded; a timeout sets the sticky error word, tpz_decode_check).
+  u32 pend_slot = ~0u, pend_row = 0;   // (uniform / lane 0) a claimed row not yet published
+  auto publish = [&]() {
+    if (pend_slot != ~0u) {
+      if (lane == 0) {
+        row_val[pend_slot % kRowRing] = pend_row;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __hip_atomic_store(&row_slot[pend_slot % kRowRing], pend_slot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      pend_slot = ~0u;
+    }
   };
   auto claim_chunk = [&]() -> u32 {
+    publish();
     u32 q = 0;
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
-    return uni(q);
+    q = uni(q);
+    const u32 slot_q = q >> rshift;
+    if ((q & ((1u << rshift) - 1u)) == 0) {
+      pend_slot = slot_q + kRowAhead;
+      if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
+    }
+    u32 row = 0;
+    if (lane == 0) {
+      u32 spins = 0;
+      while (__hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP) != slot_q) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins == (1u << 22)) {   // never expected: report it, and end this wave's work
+          atomicOr(p.err, 2u);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      row = spins == (1u << 22) ? 0xFFFFFFFFu : row_val[slot_q % kRowRing];
+    }
+    row = uni(row);
+    const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
+    return f < p.n_blocks ? (u32)f : p.n_blocks;
   };
+  auto chunk_first = [](u32 f) -> u32 { return f; };
   // Lane l <= kChunk holds ext[first + l]: block j of the chunk spans lanes j and j + 1 (one
   // u64 per lane per chunk in flight; two extents per lane cost the loop VGPRs it spilled)
   u64 gs_cur, gs_nxt;
@@ -1694,6 +1778,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
   }
+  publish();                         // (a wave waiting for this slot's row reads past the end)
   finish_pending(tab, p.out, pd);    // the wave's last block
 #ifdef TPZ_ABL_WAVEENDS
   {
@@ -2164,6 +2249,8 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // 2.20 with 4, 2.78 with 1; profiles/r3/wave_chunks.jsonl).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
   p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
+  p.row_ctr = a.tail + kTailRow;
+  p.err = a.tail + kTailError;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;

@@ -123,6 +123,7 @@ enum TailCounter : int {
   kTailBigDone,        // big blocks finished
   kTailSpillTicket,    // spill blocks claimed
   kTailExit,           // tail-kernel workgroups finished
+  kTailRow,            // wave path: rows of 16 blocks claimed (decode_wave_kernel)
   kTailCounters,
   // Sticky, past the counters the tail kernel zeroes: set when a tail workgroup's wait for the
   // big phase timed out (tpz_decode_check reports it and clears it)
