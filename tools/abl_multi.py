@@ -68,18 +68,29 @@ def main():
         for _ in range(n):
             assert L.tpz_decode_blocks(h, C.byref(b), C.byref(c), C.c_void_p(stream.cuda_stream)) == 0
 
+    def digest(t):
+        """Position-weighted sums of a tensor's bytes in 256 MiB pieces (the outputs of large
+        configs do not fit twice in HBM)."""
+        u = t.view(torch.uint8).reshape(-1)
+        w = (torch.arange(1 << 28, device=u.device, dtype=torch.int64) % 251) + 1
+        out = []
+        for i in range(0, u.numel(), 1 << 28):
+            x = u[i:i + (1 << 28)].to(torch.int64)
+            out.append(int((x * w[:x.numel()]).sum()))
+        return out
+
     ref = None
     if "full" in libs:
         run("full", 1)
         torch.cuda.synchronize()
-        ref = [t.clone() for t in (cols.status, cols.count, cols.crc, cols.ends, cols.data)]
+        ref = [digest(t) for t in (cols.status, cols.count, cols.crc, cols.ends, cols.data)]
     same = {}
     for v in a.variants:
         run(v, 1)
         torch.cuda.synchronize()
         if ref is not None:
-            got = (cols.status, cols.count, cols.crc, cols.ends, cols.data)
-            same[v] = all(torch.equal(x, y) for x, y in zip(got, ref))
+            got = [digest(t) for t in (cols.status, cols.count, cols.crc, cols.ends, cols.data)]
+            same[v] = got == ref
     times = {v: [] for v in a.variants}
     for _ in range(a.rounds):
         for v in a.variants:

@@ -153,10 +153,13 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
-        L.tpz_verify_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
-                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                             C.c_uint64, C.c_void_p, C.c_uint32]
-        L.tpz_verify_blocks_host.restype = C.c_int
+        try:   # (absent from diagnostic builds of earlier commits, TPZ_LIB_PATH)
+            L.tpz_verify_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_uint64, C.c_void_p, C.c_uint32]
+            L.tpz_verify_blocks_host.restype = C.c_int
+        except AttributeError:
+            pass
         L.tpz_host_decoded_bound.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(C.c_uint64)]
         L.tpz_host_decoded_bound.restype = C.c_int

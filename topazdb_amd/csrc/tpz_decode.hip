@@ -1545,7 +1545,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
   // row_slot[s % kRowRing] == s (see claim_chunk)
   __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
-  if (threadIdx.x < kRowAhead) {      // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
+  if (threadIdx.x < kRowAhead && p.chunk_shift < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
     row_val[threadIdx.x] = atomicAdd(p.row_ctr, 1u);
     row_slot[threadIdx.x] = threadIdx.x;
   } else if (threadIdx.x < kRowRing) {
@@ -1613,11 +1613,19 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       pend_slot = ~0u;
     }
   };
+  // (Batches of long blocks claim whole rows, kChunk = 16: there the wave path only routes
+  // blocks, a window of claimed rows buys nothing, and a row per claim would be a global atomic
+  // per 16 blocks waited for by the next 16 waves; their rows stay static, r * grid + blockIdx.x.)
+  const bool dyn_rows = rshift != 0;
   auto claim_chunk = [&]() -> u32 {
     publish();
     u32 q = 0;
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     q = uni(q);
+    if (!dyn_rows) {
+      const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
+      return f < p.n_blocks ? (u32)f : p.n_blocks;
+    }
     const u32 slot_q = q >> rshift;
     if ((q & ((1u << rshift) - 1u)) == 0) {
       pend_slot = slot_q + kRowAhead;
