@@ -15,6 +15,15 @@
 //   pipe_w0   pipe_lds with a full drain (vmcnt(0)) at the top: the previous chunk's stores are
 //             waited for (the decode's loop today)
 //   pipe2     pipe_lds with two chunks in flight (loads two iterations ahead, ping-pong buffers)
+//   pipe_meta3   pipe_lds plus the three per-chunk status / count / crc stores (lane 0, the other
+//                lanes' offsets past the descriptor), no ends store
+//   pipe_meta3x  the same three stores exec-masked to lane 0
+//   pipe_meta1   one store instruction, lanes 0-2 to the three arrays
+//   pipe_metarow the three arrays written per row of 16 chunks (wave 0, lanes 0-15)
+//   (profiles/r5/ubench_meta.jsonl: 1.59 / 1.77 / 1.77 / 1.81 / 1.66 ms for pipe_lds / meta3 /
+//   meta3x / meta1 / metarow: each small store is a write request of its own whatever its lane
+//   count; batching per row recovers two thirds in this kernel, but not in the decode,
+//   profiles/r5/meta_rows_ab.jsonl)
 //
 //     hipcc -O3 --offload-arch=gfx950 -o tools/ubench_pipe tools/ubench_pipe.hip
 //     tools/ubench_pipe [variant ...]
@@ -86,7 +95,7 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
   {
     const __amdgpu_buffer_rsrc_t rz = rsrc(d, 0);
 #pragma unroll
-    for (int q = 0; q < (MODE == 2 ? 8 : 4); q++)
+    for (int q = 0; q < (MODE == 2 ? 8 : MODE == 6 ? 7 : MODE == 7 ? 5 : MODE == 8 ? 7 : MODE == 9 ? 5 : 4); q++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, q * 256, 0, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -113,15 +122,38 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
     for (int q = 0; q < 4; q++)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o[q]), rd, q * 1024 + lane * 16, 0,
                                              MODE == 4 ? 2 : 0);
-    if (MODE == 2) {
+    if (MODE == 2 || MODE == 6) {
       const __amdgpu_buffer_rsrc_t rm = rsrc(meta, 0x7FFFFFF0ull);
       const bool l0 = lane == 0;
-      // status u8, count u32, crc u32 (three arrays), one 512-B ends store
+      // status u8, count u32, crc u32 (three arrays, one entry per chunk)
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, rm, l0 ? (u32)c : 0x7FFFFFF8u, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32((u32)c, rm, l0 ? (u32)(0x200000 + 4 * c) : 0x7FFFFFF8u, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32((u32)c, rm, l0 ? (u32)(0x800000 + 4 * c) : 0x7FFFFFF8u, 0, 0);
+    }
+    if (MODE == 8 && lane == 0) {   // the three small stores from lane 0 alone (exec-masked)
+      const __amdgpu_buffer_rsrc_t rm = rsrc(meta, 0x7FFFFFF0ull);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, rm, (u32)c, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32((u32)c, rm, (u32)(0x200000 + 4 * c), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32((u32)c, rm, (u32)(0x800000 + 4 * c), 0, 0);
+    }
+    if (MODE == 9 && lane < 3) {    // one store instruction, lanes 0-2 to the three arrays
+      const __amdgpu_buffer_rsrc_t rm = rsrc(meta, 0x7FFFFFF0ull);
+      __builtin_amdgcn_raw_buffer_store_b32((u32)c, rm, lane == 0 ? (u32)(4 * c) : (u32)((lane == 1 ? 0x200000 : 0x800000) + 4 * c), 0, 0);
+    }
+    if (MODE == 10 && wv == 0) {   // a row's metadata at once: wave 0, lanes 0-15, 3 stores
+      const __amdgpu_buffer_rsrc_t rm = rsrc(meta, 0x7FFFFFF0ull);
+      const u32 i = (u32)c + lane;   // (wave 0's chunk is the row's first)
+      const bool on = lane < 16;
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)i, rm, on ? i : 0x7FFFFFF8u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(i, rm, on ? (u32)(0x200000 + 4 * i) : 0x7FFFFFF8u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(i, rm, on ? (u32)(0x800000 + 4 * i) : 0x7FFFFFF8u, 0, 0);
+    }
+    if (MODE == 2 || MODE == 7) {
+      // one 512-B ends store per chunk, into an ends region of its own (chunk c's at 512 c of d,
+      // past the copied data)
+      const __amdgpu_buffer_rsrc_t re = rsrc(d + nchunks * 4096 + c * 512, 512);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) u32, make_uint2(lane, (u32)c)),
-                                            rm, (u32)(0x1000000 + 512 * (c & 0xFFFF) + 8 * lane), 0, 0);
+                                            re, 8 * lane, 0, 0);
     }
     c = cn;
   } while (c < nchunks);
@@ -280,7 +312,7 @@ int main(int argc, char** argv) {
   const u64 nch = N / 4096;
   uint8_t *a, *b, *m;
   CHECK(hipMalloc(&a, N));
-  CHECK(hipMalloc(&b, N));
+  CHECK(hipMalloc(&b, N + (N / 4096) * 512));
   CHECK(hipMalloc(&m, 64u << 20));
   CHECK(hipMemset(a, 0x5A, N));
   CHECK(hipMemset(b, 0, N));
@@ -301,6 +333,11 @@ int main(int argc, char** argv) {
       else if (v == "pipe2") pipe2_k<<<cus, 1024>>>(a, b, nch);
       else if (v == "pipe_nt") pipe_k<4><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe_il") pipeil_k<<<cus, 1024>>>(a, b, nch);
+      else if (v == "pipe_meta3") pipe_k<6><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_ends") pipe_k<7><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_meta3x") pipe_k<8><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_meta1") pipe_k<9><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_metarow") pipe_k<10><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe8") pipe_k<1><<<cus, 512>>>(a, b, m, nch);
       else if (v == "pipe_dyn") { (void)hipMemsetAsync(m, 0, 4); pipedyn_k<<<cus, 1024>>>(a, b, (u32*)m, nch); }
       else if (v == "pipe_rd") pipe_k<5><<<cus, 1024>>>(a, b, m, nch);
