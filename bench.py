@@ -45,6 +45,7 @@ from topazdb_amd.batch import (DeviceBatch, FlatColumns, SlottedColumns, decode_
                                entry_first)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
+SETTLE_S = 0.3       # untimed decode steps before a timed region's warm-up (time_decode)
 GIB = float(1 << 30)
 
 
@@ -519,12 +520,11 @@ def file_crc_rate(ctx, batch: DeviceBatch, src: np.ndarray, dev, steps: int = 10
     got = crc.cpu().numpy().view(np.uint32)
     for i in (0, len(ext) - 2):  # spot check against zlib (the CRC oracle)
         assert got[i] == zlib.crc32(src[ext[i]:ext[i + 1]].tobytes()), "file CRC mismatch"
-    # the median of 5 timed rounds after 3 warm-up launches: right after the decode legs single
+    # the median of 5 timed rounds after a settle (the zlib spot check above idles the GPU): single
     # launches of this kernel ranged 0.76-1.06 ms (profiles/r2/closing2/kernel_stats_side.csv),
     # one timed round after one warm-up reported 0.955 ms where tools/crc_ab.py's interleaved
     # rounds measure 0.78 ms (profiles/r5/crc_ab.jsonl)
-    for _ in range(3):
-        run()
+    settle(run, dev)
     rounds = []
     for _ in range(5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -627,6 +627,7 @@ def codec_rate(ctx, dev, codec: str = "snappy", nb: int = 1 << 18, steps: int = 
                             out.src.data_ptr(), out.ext.data_ptr(), st.data_ptr(),
                             stream.cuda_stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    settle(lambda: (codec(), decode_batch(ctx, out, cols, stream)), dev)   # (after host work)
     codec()
     decode_batch(ctx, out, cols, stream)
     ev[0].record(stream)
@@ -701,6 +702,7 @@ def encode_rate(ctx, src: np.ndarray, ext: np.ndarray, gen, n_ent: np.ndarray, b
     ms_plan = min(pts) * 1e3
     ms_plan_median = sorted(pts)[len(pts) // 2] * 1e3
     stream = torch.cuda.current_stream(dev)
+    settle(lambda: encode_blocks(ctx, ent, first, dext, nb, out=out), dev)   # (after the checks)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(steps):
@@ -886,10 +888,27 @@ def validate_replicas(cols: SlottedColumns, ext: np.ndarray, nb: int, full: int,
                                 cols.data[sb0 + ln - int(ends0[-1]):sb0 + ln]), f"replica {c} data"
 
 
+def settle(fn, dev, seconds: float = SETTLE_S) -> None:
+    """Untimed launches of fn for `seconds` before a timed region: after host-side work (data
+    generation, uploads, checks) the shader clock is down and the first launches run slow
+    (time_decode)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize(dev)
+
+
 def time_decode(ctx, batch: DeviceBatch, cols: SlottedColumns, stream, steps: int, warmup: int,
                 dist, dev) -> tuple[float, float]:
     """W untimed + K timed decode steps bracketed by a barrier and a device sync on both sides;
-    returns (wall seconds, HIP-event ms per step on the decode stream), max over ranks."""
+    returns (wall seconds, HIP-event ms per step on the decode stream), max over ranks.
+
+    Before the W warm-up steps the GPU runs untimed decode steps for SETTLE_S seconds: after the
+    host-side shard generation and upload the shader clock is down, and a short warm-up left the
+    timed steps 5 % slow (2.01 ms against 1.915 ms for every later round on one box; after a
+    50 ms host sleep 2.20 ms: tools/decode_timing.py, profiles/r5/decode_timing.jsonl)."""
+    settle(lambda: decode_batch(ctx, batch, cols, stream), dev)
     for _ in range(warmup):
         decode_batch(ctx, batch, cols, stream)
     torch.cuda.synchronize(dev)
@@ -1020,6 +1039,7 @@ def flat_rate(ctx, batch: DeviceBatch, n_ent, gen, alg: int, dev, steps: int, wa
     args = (batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks, batch.src_bytes)
 
     def timed(fn):
+        settle(fn, dev)
         for _ in range(warmup):
             fn()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1310,6 +1330,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_s": SETTLE_S,   # untimed decode steps before the warm-up (time_decode)
             "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
