@@ -1218,7 +1218,8 @@ template <class Col, class MapT, int kMapLen, bool BIG, bool FLAT = false>
 __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const Col& col,
                                              MapT* map, u32 a0, u32 len, u32 b, u64 ext_b,
                                              const Out& o, u32 kshift, Stamps& S, PendingCrc& pd,
-                                             u64 kf = 0, u64 vf = 0, const Out* o_lds = nullptr) {
+                                             u64 kf = 0, u64 vf = 0, u64 ef = 0,
+                                             const Out* o_lds = nullptr) {
   const u32 lane = lane_id();
   // the header reads are issued together (one LDS round trip); the checks keep the reference's
   // order
@@ -1276,7 +1277,8 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     const u32 dl = P - 2 - 2 * n;
     // (flat: the exact ends, n pairs reserved for every block by tpz_flat_layout)
     const bool slots_fit = FLAT || 6u * n <= len;
-    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
+    // (flat: ef = efirst[b], loaded with the block's prefetch)
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + (FLAT ? ef : ends_base(o.efirst, ext_b, b));
     // whole 128-byte lines of {kend, vend} in the slotted layout; exactly n in the exact one
     const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
     {
@@ -1526,6 +1528,13 @@ struct Params {
 };
 
 
+// A load through the constant address space: a scalar load for a uniform index (memory no
+// kernel of the launch writes).
+template <class T>
+__device__ __forceinline__ T const_load(const T* base, u64 i) {
+  return reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(base))[i];
+}
+
 // ------------------------------------------------------------------ wave path kernel
 #ifdef TPZ_ABL_ONCHIP
 // diagnostic (timing only): every wave decodes blocks 0..4095 over and over, so loads and stores
@@ -1703,12 +1712,14 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // prefetch state for block b
   uint4 v[kWinRounds];
   u64 s_cur = 0, e_cur = 0;
-  u64 kf_cur = 0, vf_cur = 0;     // flat: the block's column starts, loaded one block ahead
+  u64 kf_cur = 0, vf_cur = 0, ef_cur = 0;   // flat: the block's column and ends starts, loaded
+                                             // one block ahead
   auto issue = [&](u32 bb, u32 jj, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
-    if (FLAT) {
-      kf_cur = p.out.kfirst[bb];
-      vf_cur = p.out.vfirst[bb];
+    if (FLAT) {   // (scalar loads: uniform, and no VGPRs held across the block)
+      kf_cur = const_load(p.out.kfirst, bb);
+      vf_cur = const_load(p.out.vfirst, bb);
+      ef_cur = const_load(p.out.efirst, bb);
     }
     s = lane64(gs_cur, jj);
     e = lane64(gs_cur, jj + 1);
@@ -1743,7 +1754,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 
   while (b < p.n_blocks) {
     const u64 s = s_cur, e = e_cur;
-    const u64 kf = kf_cur, vf = vf_cur;
+    const u64 kf = kf_cur, vf = vf_cur, ef = ef_cur;
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
     const bool fits = (e - s) <= kWaveMaxLen;
     if (fits) {
@@ -1781,7 +1792,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false, FLAT>(tab, win, col, map, (u32)(s & 15u),
                                                            len64, bdec, s, p.out, kshift, S, pd, kf, vf,
-                                                           &out_lds);
+                                                           ef, &out_lds);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
