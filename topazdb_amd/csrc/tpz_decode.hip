@@ -135,7 +135,7 @@ __device__ __forceinline__ u32 bswap32(u32 w) { return __builtin_bswap32(w); }
 // 16 bytes starting at LDS byte offset x (relative to base, base 16-aligned). Default: three
 // 8-byte-aligned ds_read_b64 + a one-bit dword select + alignbyte (9 VALU). Diagnostic variants:
 // one ds_read_b128 at the byte address (TPZ_ABL_U128; gfx950 replays it: 64 LDS cycles), two
-// aligned ds_read_b128 + a two-bit select (TPZ_ABL_FUNNEL, 16 VALU).
+// aligned ds_read_b128 + a two-bit select (16 VALU).
 __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
        // unaligned ds_read_b128 replay) + a one-bit dword select + alignbyte
   typedef u32 u32x2 __attribute__((ext_vector_type(2)));
@@ -153,19 +153,7 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
 // ------------------------------------------------------------------ CRC-32 (table driven)
 // tab = kNumCrcTables x 256 u32 in LDS. T_k[b] = R0(b || 0^k): raw CRC (init 0, no xorout).
 // ids 0..15: T_0..T_15 (slice-by-16); ids 16+4j+i: T_{n_j-1-i}, n_j = kCrcShiftBytes[j].
-#if defined(TPZ_ABL_NOCF)
-// diagnostic (timing only, wrong CRCs): the same lookups, made bank-conflict-free
-__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
-  return tab[id * 256 + ((byte & 0x20u) | (threadIdx.x & 31u))];
-}
-#elif defined(TPZ_ABL_LUTVALU)
-// diagnostic (timing only, wrong CRCs): no LDS lookup, one VALU op in its place
-__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
-  return __builtin_amdgcn_alignbyte(byte, byte ^ (u32)id, 1);
-}
-#else
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
-#endif
 
 // a ^ b ^ c in one v_bitop3_b32.
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -508,23 +496,9 @@ __device__ __forceinline__ void put_meta(const Out& o, u32 b, u32 st, u32 n, u32
   __builtin_amdgcn_raw_buffer_store_b32(n, whole_rsrc(o.count), l0 ? 4 * b : kOob, 0, 0);
   __builtin_amdgcn_raw_buffer_store_b32(crc, whole_rsrc(o.crc), l0 ? 4 * b : kOob, 0, 0);
 }
-// K VMEM ops that touch nothing (a zero-length descriptor), issued right behind the next
-// block's prefetch loads (diagnostic builds, TPZ_VMPAD=K): they make the compiler's wait for
-// those loads vmcnt(>= K) on every path. The shipped build issues none: the branch-free
-// meta/ends stores alone gave the gain (2.05 -> 1.96 ms per
-// 2^20 blocks) although the wait stays vmcnt(0), and padding on top measured slower
-// (profiles/r1/ablations_vmpad.jsonl).
-#ifndef TPZ_VMPAD
-#define TPZ_VMPAD 0                   // measured: 7/12/20 pads were 0.5-1.5 % slower than none
-#endif
-constexpr int kVmAfter = TPZ_VMPAD;
-template <int K>
-__device__ __forceinline__ void vm_pad(const Out& o) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)o.status, (short)0, 0, 0x00020000);
-#pragma unroll
-  // distinct, non-adjacent offsets: neither merged nor vectorized into fewer instructions
-  for (int i = 0; i < K; i++) __builtin_amdgcn_raw_buffer_store_b32(0u, r, 256 * i, 0, 0);
-}
+// (Zero-length stores issued after the prefetch loads, so that the compiler's wait for them
+// became vmcnt(>= K) on every path, measured 0.5-1.5 % slower than none: profiles/r1/
+// ablations_vmpad.jsonl, profiles/r4/vmpad/.)
 
 // Bytes [lo, hi) of the 4-byte word d (lo, hi in 0..16, relative to the chunk start).
 __device__ __forceinline__ u32 byte_mask(int lo, int hi, int d) {
@@ -1431,13 +1405,11 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     if (!BIG && fuse) {
       u32 lc;
       fin.on = false;      // the previous block's combine runs here, before pd is reused
-#ifndef TPZ_ABL_FUSED
       if (!f_short) {
         lc = copy_crc_piped<FLAT>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                   reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst, fo,
                                   win, pb, P + k, o, pd);
       } else
-#endif
       {
         lc = f_short
           ? copy_crc_fused<true, FLAT>(tab, Src16{win}, *reinterpret_cast<const ColSmall*>(&col),
@@ -1456,10 +1428,6 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
     else
       crc = (R == crc_shift_small(tab, ~stored, k)) ? stored : ~crc_unshift_small(tab, R, k);
-#if defined(TPZ_ABL_NOCF) || defined(TPZ_ABL_LUTVALU)
-    asm volatile("" ::"v"(R));   // keep the CRC work, report a match (timing builds only)
-    crc = stored;
-#endif
 #endif
   } else {
     u32 c = 0xFFFFFFFFu;
@@ -1541,10 +1509,6 @@ __device__ __forceinline__ T const_load(const T* base, u64 i) {
 // stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
 constexpr u32 kOnchipMask = 4095;
 #endif
-#ifdef TPZ_ABL_WAVEENDS
-// diagnostic: each wave's start and end time (s_memrealtime, 100 MHz) and block count
-__device__ unsigned long long g_wave_ends[3 * 8192];
-#endif
 template <bool FLAT>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
@@ -1565,9 +1529,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     out_lds = p.out;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
-#ifdef TPZ_ABL_WAVEENDS
-  const unsigned long long we_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
   load_tables(tab, p.crc_tables);
 
   const u32 wid = uni(threadIdx.x >> 6);
@@ -1595,7 +1556,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // next chunk of kChunk consecutive blocks from an LDS counter when it finishes one: the waves
   // of a CU do not run at one speed (with a fixed block per wave, the first four waves of each
   // workgroup finished at 1.66 ms and the last four at 2.21 ms of a 2.26 ms launch,
-  // tools/wave_ends.py), so a fixed split left the fast waves idle while the slow ones finished.
+  // a round-3 per-wave timing build), so a fixed split left the fast waves idle while the slow
+  // ones finished.
   // Lane l of a chunk's extent group holds ext[] of the chunk's block l (loaded one chunk ahead,
   // so a block's extent is two readlanes instead of a memory round trip).
 #ifdef TPZ_WAVE_CHUNK
@@ -1745,12 +1707,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
         if ((u32)r < rounds) fix_tail(v[r], p.src, ws + r * 1024 + lane * 16, p.src_bytes);
     }
   };
-#ifdef TPZ_ABL_WAVEENDS
-  u32 k = 0;  // this wave's block counter
-#endif
   PendingCrc pd{0u, 0u, 0u, 0u, 0u, 0u, 0u};
   issue(b, 0, s_cur, e_cur);
-  vm_pad<kVmAfter>(p.out);
 
   while (b < p.n_blocks) {
     const u64 s = s_cur, e = e_cur;
@@ -1767,9 +1725,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     }
     TPZ_STAMP(S, 0);
     const u32 bcur = b;
-#ifdef TPZ_ABL_WAVEENDS
-    k++;
-#endif
     if (++j == kChunk) {              // next chunk (its extent loads completed long ago)
       j = 0;
       q_cur = q_nxt;
@@ -1781,7 +1736,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     b = chunk_first(q_cur) + j;
     b = b < p.n_blocks ? b : p.n_blocks;
     issue(b, j, s_cur, e_cur);       // next block's loads fly while this one decodes
-    vm_pad<kVmAfter>(p.out);
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
     if (fits) {
@@ -1799,17 +1753,6 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   }
   publish();                         // (a wave waiting for this slot's row reads past the end)
   finish_pending(tab, p.out, pd);    // the wave's last block
-#ifdef TPZ_ABL_WAVEENDS
-  {
-    const u32 gw = blockIdx.x * kWavesPerWG + wid;
-    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && gw < 8192) {
-      g_wave_ends[3 * gw] = we_t0;
-      g_wave_ends[3 * gw + 1] = t1;
-      g_wave_ends[3 * gw + 2] = k;
-    }
-  }
-#endif
 #ifdef TPZ_ABL_STAMPS
   const u32 gw = blockIdx.x * kWavesPerWG + wid;
   if (lane == 0 && gw < (u32)kStampWaves)
@@ -2292,12 +2235,6 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
 
 }  // namespace tpz
 
-#ifdef TPZ_ABL_WAVEENDS
-extern "C" int tpz_debug_wave_ends(unsigned long long* host, int n_waves) {
-  if (n_waves > 8192) n_waves = 8192;
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tpz::g_wave_ends), (size_t)n_waves * 3 * 8);
-}
-#endif
 #ifdef TPZ_ABL_STAMPS
 // Diagnostic build only: copies the per-wave phase sums (8 u64 per wave, 6 used) to the host.
 extern "C" int tpz_debug_stamps(unsigned long long* host, int n_waves) {
