@@ -4,7 +4,7 @@ weak #10 / next #7.
 
 A DPP read of a lane that the surrounding control flow has switched off returns 0 (bound_ctrl)
 or `old`, not the lane's value: the wave path once lost a block that way when a select became
-a branch (adc06ae). DESIGN.md §4f lists every update_dpp of the two kernels and the wave-uniform
+a branch (adc06ae). DESIGN.md §4e lists every update_dpp of the two kernels and the wave-uniform
 control flow it sits in. These tests drive each shift with partial lane sets:
   * bigwave: every entry count 1..63 (the parse's lanes >= n are off in the `act` branch and
     carry kl = vl = 0 into scan_incl), keys of 1..40 B and empty values (so segment ends skip
