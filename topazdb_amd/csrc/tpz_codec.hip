@@ -337,6 +337,34 @@ struct Lz4LaneSrc {
     return (u32)(cv >> (8 * (a - cpos))) & 0xFFu;
   }
 };
+// the sizes pass's source: the lane's own 128-byte window in LDS, refilled at a 16-byte boundary
+// with eight 16-byte loads. The walk is a chain of dependent loads: in the compressible 4 KiB
+// shape a sequence is a ~70-byte literal and a match, so a 16-byte register window needed a
+// load per sequence, while the next header after a literal of up to ~110 bytes is still in the
+// 128-byte window (the byte reads become LDS round trips). 32 KiB per 256-thread workgroup, so
+// five workgroups (20 waves) share a CU, as many as the kernel's VGPRs allow.
+constexpr u32 kLz4WinStride = 128;
+struct Lz4LaneWinSrc {
+  const uint8_t* src;
+  u64 src_bytes, base;          // in[0] is src[base]
+  mutable u64 cpos;             // the window's first byte (starts 2^62 before base: no window)
+  uint8_t* win;                 // this lane's window (LDS)
+  __device__ u32 byte(int64_t i) const {
+    const u64 a = base + (u64)i;
+    if (a - cpos >= 128) {
+      cpos = a & ~15ull;
+      u128 v[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) v[t] = ld16c(src, src_bytes, cpos + 16 * t);
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        reinterpret_cast<uint64_t*>(win)[2 * t] = (uint64_t)v[t];
+        reinterpret_cast<uint64_t*>(win)[2 * t + 1] = (uint64_t)(v[t] >> 64);
+      }
+    }
+    return win[a - cpos];
+  }
+};
 template <class Src, class Out>
 __device__ int64_t lz4_walk(const Src& in, int64_t iend, const Out& out, int64_t oend) {
   if (oend == 0) return (iend == 1 && in.byte(0) == 0) ? 0 : -1;
@@ -551,6 +579,13 @@ __device__ __forceinline__ int64_t lz4_block_length(const uint8_t* src, u64 src_
   return lz4_walk(Lz4LaneSrc{src, src_bytes, s + 4, s + 4 - (1ull << 62), 0}, (int64_t)len - 5, Lz4NoOut{}, size);
 }
 
+__device__ __forceinline__ int64_t lz4_block_length_lds(const uint8_t* src, u64 src_bytes, u64 s, u64 len,
+                                                        uint8_t* win) {
+  const int64_t size = lz4_prefix(src + s, len - 1);
+  if (size < 0) return -1;
+  return lz4_walk(Lz4LaneWinSrc{src, src_bytes, s + 4, s + 4 - (1ull << 62), win}, (int64_t)len - 5, Lz4NoOut{}, size);
+}
+
 __device__ __forceinline__ int64_t lz4_block_length_bytes(const uint8_t* blk, u64 len) {
   const int64_t size = lz4_prefix(blk, len - 1);
   if (size < 0) return -1;
@@ -559,6 +594,7 @@ __device__ __forceinline__ int64_t lz4_block_length_bytes(const uint8_t* blk, u6
 
 // ------------------------------------------------------------------ sizes
 __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kLz4WinStride];
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_blocks) return;
   const u64 s = p.ext[i], e = p.ext[i + 1], len = e - s;
@@ -566,8 +602,9 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
   if (tag == 3) {
     // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err
     // leaves a lone tag byte
-    const int64_t r = p.src_bytes >= 16 ? lz4_block_length(p.src, p.src_bytes, s, len)
-                                        : lz4_block_length_bytes(p.src + s, len);
+    const int64_t r = p.src_bytes >= 16
+        ? lz4_block_length_lds(p.src, p.src_bytes, s, len, wins + threadIdx.x * kLz4WinStride)
+        : lz4_block_length_bytes(p.src + s, len);
     p.size[i] = r < 0 ? 1 : (u64)r + 1;
     return;
   }
