@@ -2203,14 +2203,17 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   for (int r = 0; r < kBigSuper; r++) p.xp[r] = xp[r];
   const u32* ls = lane_run_shifts();
   for (int l = 0; l < 64; l++) p.lane_shift[l] = ls[l];
-  // Blocks claimed at a time by a wave of the wave path: single blocks balance the waves of a CU
-  // best (the first waves issue first; same box, 4k: 1.875 ms with 1, 1.89 with 2 or 4, 1.95
-  // with 16, 2.10 with a fixed split; zipf 2.04 against 2.28). A batch of long blocks (the 64k
-  // config, where the wave path only routes blocks to the bigwave kernel) takes whole rows: its
+  // Blocks claimed at a time by a wave of the wave path. Claims of single blocks balanced the
+  // waves of a CU best with static rows (the first waves issue first; same box, 4k: 1.875 ms with
+  // 1, 1.89 with 2 or 4, 1.95 with 16, 2.10 with a fixed split; zipf 2.04 against 2.28;
+  // profiles/r3/wave_chunks.jsonl); with rows claimed from the global counter, pairs are better
+  // (4k 1.872-1.877 against 1.881-1.890 ms, zipf 1.986 against 2.010, each in both orders; 4
+  // blocks 1.920 / 2.045: profiles/r5/chunk_ab.jsonl). A batch of long blocks (the 64k config,
+  // where the wave path only routes blocks to the bigwave kernel) takes whole rows: its
   // per-chunk extent and header round trips are not hidden by any decode (64k: 2.07 ms with 16,
-  // 2.20 with 4, 2.78 with 1; profiles/r3/wave_chunks.jsonl).
+  // 2.20 with 4, 2.78 with 1).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
-  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
+  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 1u;
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
