@@ -341,19 +341,6 @@ typedef struct {
 tpz_err tpz_decode_blocks_flat(tpz_ctx* ctx, const tpz_batch* batch, const tpz_flat_columns* out,
                                void* stream);
 
-/* tpz_decode_blocks_flat_scan: tpz_flat_layout and tpz_decode_blocks_flat in one pass over the
- * batch: the decode computes the layout itself (a decoupled look-back over rows of 16 blocks)
- * and writes it to d_first (3 * (n_blocks + 1) u64, as tpz_flat_layout; out->d_first is
- * ignored). The columns are sized by the caller: d_keys holds key_cap bytes, d_values
- * value_cap, d_ends 2 * pair_cap u32. A block whose reservation does not fit them is not
- * decoded and reports TPZ_BLOCK_SPILL_FULL; d_first is exact whatever the capacities (its
- * totals say what the batch needs). Otherwise every output equals tpz_flat_layout +
- * tpz_decode_blocks_flat's. Asynchronous on `stream`; uses the stream's workspace. */
-tpz_err tpz_decode_blocks_flat_scan(tpz_ctx* ctx, const tpz_batch* batch,
-                                    const tpz_flat_columns* out, uint64_t* d_first,
-                                    uint64_t key_cap, uint64_t value_cap, uint64_t pair_cap,
-                                    void* stream);
-
 /* ---- the host pipeline -------------------------------------------------------------------
  * SsTable::read_block for a whole run of blocks that sit in HOST memory (src/table.rs:154-164;
  * the bytes FileObject::read's pread returns, src/table/file_object.rs:23-27): the library

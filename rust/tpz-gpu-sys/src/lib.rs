@@ -167,10 +167,6 @@ extern "C" {
                            stream: *mut c_void) -> TpzErr;
     pub fn tpz_decode_blocks_flat(ctx: *mut TpzCtx, batch: *const TpzBatch,
                                   out: *const TpzFlatColumns, stream: *mut c_void) -> TpzErr;
-    pub fn tpz_decode_blocks_flat_scan(ctx: *mut TpzCtx, batch: *const TpzBatch,
-                                       out: *const TpzFlatColumns, d_first: *mut u64,
-                                       key_cap: u64, value_cap: u64, pair_cap: u64,
-                                       stream: *mut c_void) -> TpzErr;
     pub fn tpz_host_decoded_bound(h_src: *const u8, h_ext: *const u64, n_blocks: u32,
                                   bound: *mut u64) -> TpzErr;
     pub fn tpz_decode_blocks_host(ctx: *mut TpzCtx, h_src: *const u8, h_ext: *const u64,

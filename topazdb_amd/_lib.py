@@ -150,11 +150,6 @@ def lib() -> C.CDLL:
         L.tpz_decode_blocks_flat.argtypes = [C.c_void_p, C.POINTER(Batch), C.POINTER(FlatColumns),
                                              C.c_void_p]
         L.tpz_decode_blocks_flat.restype = C.c_int
-        if hasattr(L, "tpz_decode_blocks_flat_scan"):   # (diagnostic builds of older trees lack it)
-            L.tpz_decode_blocks_flat_scan.argtypes = [C.c_void_p, C.POINTER(Batch),
-                                                      C.POINTER(FlatColumns), C.c_void_p,
-                                                      C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]
-            L.tpz_decode_blocks_flat_scan.restype = C.c_int
         L.tpz_decode_blocks_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                              C.POINTER(HostColumns), C.c_uint32]
         L.tpz_decode_blocks_host.restype = C.c_int
@@ -314,17 +309,6 @@ class Context:
         c = FlatColumns(*[cols[f] for f in FLAT_FIELDS])
         check(lib().tpz_decode_blocks_flat(self.handle, C.byref(b), C.byref(c), C.c_void_p(stream)),
               "tpz_decode_blocks_flat")
-
-    def decode_flat_scan_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
-                              cols: dict, d_first: int, key_cap: int, value_cap: int,
-                              pair_cap: int, stream: int = 0) -> None:
-        """tpz_decode_blocks_flat_scan: the flat layout and the decode in one pass; d_first
-        receives the layout (cols["first"] is not read)."""
-        b = Batch(d_src, d_ext, n_blocks, src_bytes)
-        c = FlatColumns(*[cols[f] for f in FLAT_FIELDS])
-        check(lib().tpz_decode_blocks_flat_scan(self.handle, C.byref(b), C.byref(c),
-                                                C.c_void_p(d_first), key_cap, value_cap, pair_cap,
-                                                C.c_void_p(stream)), "tpz_decode_blocks_flat_scan")
 
     def decode_host_ptrs(self, h_src: int, h_ext: int, n_blocks: int, cols: HostColumns,
                          chunk_blocks: int = 0) -> int:

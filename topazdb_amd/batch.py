@@ -72,11 +72,6 @@ class SlottedColumns:
         self.n_blocks = n_blocks
         self._decoded = None   # (ctx, batch, stream) of the last decode_batch into these columns
 
-    def _columns(self, dev) -> None:
-        self.keys = torch.empty(max(self.key_bytes, 16), dtype=torch.uint8, device=dev)
-        self.values = torch.empty(max(self.value_bytes, 16), dtype=torch.uint8, device=dev)
-        self.ends = torch.empty(2 * max(self.n_pairs, 1), dtype=torch.int32, device=dev)
-
     def set_spill_cap(self, spill_cap: int) -> None:
         self.spill_cap = int(spill_cap)
         self.spill = (torch.empty(self.spill_cap, dtype=torch.uint8, device=_dev(self.device))
@@ -287,24 +282,16 @@ class FlatColumns:
     the whole batch, in SsTableIterator order, plus exact {kend, vend} pairs per block."""
 
     def __init__(self, ctx: Context, batch: DeviceBatch, spill_cap: int = 0,
-                 stream: torch.cuda.Stream | None = None, caps: tuple | None = None):
-        """caps = (pairs, key bytes, value bytes): the one-pass decode's columns (decode_flat_scan;
-        the layout is then its output). None: run tpz_flat_layout and size them exactly."""
+                 stream: torch.cuda.Stream | None = None):
         dev = _dev(ctx.device)
         self.device = ctx.device
-        self.scan = caps is not None
-        if self.scan:
-            s = stream if stream is not None else torch.cuda.current_stream(dev)
-            with torch.cuda.stream(s):
-                self.first = torch.empty(3 * (batch.n_blocks + 1), dtype=torch.int64,
-                                         device=dev).view(3, batch.n_blocks + 1)
-            self.n_pairs, self.key_bytes, self.value_bytes = (int(x) for x in caps)
-        else:
-            self.first = flat_layout(ctx, batch, stream)
-            tot = self.first[:, batch.n_blocks].cpu().numpy()      # one sync: the column sizes
-            self.n_pairs, self.key_bytes, self.value_bytes = (int(x) for x in tot)
-        self._columns(dev)
+        self.first = flat_layout(ctx, batch, stream)
+        tot = self.first[:, batch.n_blocks].cpu().numpy()      # one sync: the column sizes
+        self.n_pairs, self.key_bytes, self.value_bytes = (int(x) for x in tot)
         nb = max(batch.n_blocks, 1)
+        self.keys = torch.empty(max(self.key_bytes, 16), dtype=torch.uint8, device=dev)
+        self.values = torch.empty(max(self.value_bytes, 16), dtype=torch.uint8, device=dev)
+        self.ends = torch.empty(2 * max(self.n_pairs, 1), dtype=torch.int32, device=dev)
         self.count = torch.empty(nb, dtype=torch.int32, device=dev)
         self.status = torch.empty(nb, dtype=torch.uint8, device=dev)
         self.crc = torch.empty(nb, dtype=torch.int32, device=dev)
@@ -313,11 +300,6 @@ class FlatColumns:
         self.set_spill_cap(spill_cap)
         self.n_blocks = batch.n_blocks
         self._decoded = None
-
-    def _columns(self, dev) -> None:
-        self.keys = torch.empty(max(self.key_bytes, 16), dtype=torch.uint8, device=dev)
-        self.values = torch.empty(max(self.value_bytes, 16), dtype=torch.uint8, device=dev)
-        self.ends = torch.empty(2 * max(self.n_pairs, 1), dtype=torch.int32, device=dev)
 
     def set_spill_cap(self, spill_cap: int) -> None:
         self.spill_cap = int(spill_cap)
@@ -339,22 +321,9 @@ class FlatColumns:
             ctx, batch, stream = self._decoded
             sid = _stream_id(ctx, stream)
             ctx.decode_check(sid)
-            again = False
-            if self.scan:
-                # the one-pass decode: its layout's totals against the caps it ran with (blocks
-                # past them reported SPILL_FULL and wrote nothing)
-                self.scan = False
-                tot = [int(x) for x in self.first[:, self.n_blocks].cpu().numpy()]
-                caps = (self.n_pairs, self.key_bytes, self.value_bytes)
-                self.n_pairs, self.key_bytes, self.value_bytes = tot
-                if any(t > c for t, c in zip(tot, caps)):
-                    self._columns(_dev(self.device))
-                    again = True
             used = int(self.spill_used.cpu()[0])
             if used > self.spill_cap:
                 self.set_spill_cap(used)
-                again = True
-            if again:       # the two-pass decode over the layout the first decode wrote
                 decode_flat(ctx, batch, self, stream)
                 torch.cuda.synchronize(_dev(self.device))
                 ctx.decode_check(sid)
@@ -406,26 +375,6 @@ def decode_flat(ctx: Context, batch: DeviceBatch, cols: FlatColumns | None = Non
     s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
     ctx.decode_flat_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
                          batch.src_bytes, cols.ptrs(), s.cuda_stream)
-    cols._decoded = (ctx, batch, stream)
-    return cols
-
-
-def decode_flat_scan(ctx: Context, batch: DeviceBatch, caps: tuple | None = None,
-                     stream: torch.cuda.Stream | None = None, spill_cap: int = 0) -> FlatColumns:
-    """tpz_decode_blocks_flat_scan: the flat layout and the decode in one pass, with no host sync
-    before the decode. caps = (pairs, key bytes, value bytes) the columns hold; the default is
-    what a batch whose entries do not overlap can need (keys and values are bytes of the blocks:
-    src_bytes each; pairs: the slotted layout's entry capacity). cols.complete() (dense() calls
-    it) reads the layout's totals back and, when the batch needed more, sizes the columns exactly
-    and decodes again (tpz_decode_blocks_flat over the layout the first pass wrote)."""
-    if caps is None:
-        caps = (_lib.entry_capacity(batch.src_bytes, batch.n_blocks), batch.src_bytes,
-                batch.src_bytes)
-    cols = FlatColumns(ctx, batch, spill_cap, stream, caps=caps)
-    s = stream if stream is not None else torch.cuda.current_stream(_dev(ctx.device))
-    ctx.decode_flat_scan_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
-                              batch.src_bytes, cols.ptrs(), cols.first.data_ptr(), cols.key_bytes,
-                              cols.value_bytes, cols.n_pairs, s.cuda_stream)
     cols._decoded = (ctx, batch, stream)
     return cols
 

@@ -136,8 +136,6 @@ struct tpz_workspace {
   size_t bloom_cap = 0;
   void* d_comp = nullptr;       // tpz_compress_blocks: the per-block scratch slots + scan parts
   size_t comp_cap = 0;
-  void* d_scan = nullptr;       // tpz_decode_blocks_flat_scan: the row descriptors
-  size_t scan_cap = 0;
   uint32_t* h_info = nullptr;   // pinned: tpz_plan_blocks' read-back of its 16-byte info
 };
 
@@ -164,7 +162,6 @@ void free_workspace(tpz_workspace& w) {
   if (w.d_plan1) (void)hipFree(w.d_plan1);
   if (w.d_bloom) (void)hipFree(w.d_bloom);
   if (w.d_comp) (void)hipFree(w.d_comp);
-  if (w.d_scan) (void)hipFree(w.d_scan);
   if (w.h_info) (void)hipHostFree(w.h_info);
   w = tpz_workspace{};
 }
@@ -559,74 +556,6 @@ tpz_err tpz_decode_blocks_flat(tpz_ctx* c, const tpz_batch* b, const tpz_flat_co
   a.vals = o->d_values;
   a.kfirst = o->d_first + st;
   a.vfirst = o->d_first + 2 * st;
-  tpz::launch_decode(a, (hipStream_t)stream);
-  TPZ_HIP(hipGetLastError());
-  return TPZ_SUCCESS;
-}
-
-tpz_err tpz_decode_blocks_flat_scan(tpz_ctx* c, const tpz_batch* b, const tpz_flat_columns* o,
-                                    uint64_t* d_first, uint64_t key_cap, uint64_t value_cap,
-                                    uint64_t pair_cap, void* stream) {
-  if (!c || !b || !o || !d_first) return TPZ_ERR_INVALID_ARG;
-  TPZ_HIP(hipSetDevice(c->device));
-  if (b->n_blocks == 0) {
-    TPZ_HIP(hipMemsetAsync(d_first, 0, 3 * 8, (hipStream_t)stream));
-    if (o->d_spill_used) TPZ_HIP(hipMemsetAsync(o->d_spill_used, 0, 8, (hipStream_t)stream));
-    return TPZ_SUCCESS;
-  }
-  if (!b->d_src || !b->d_ext || !o->d_keys || !o->d_values || !o->d_ends || !o->d_count ||
-      !o->d_status || !o->d_crc || !o->d_spill_off || !o->d_spill_used ||
-      (o->spill_cap && !o->d_spill) || (reinterpret_cast<uintptr_t>(b->d_src) & 15u) ||
-      (reinterpret_cast<uintptr_t>(o->d_keys) & 15u) || (reinterpret_cast<uintptr_t>(o->d_values) & 15u))
-    return TPZ_ERR_INVALID_ARG;
-  tpz_workspace* w = nullptr;
-  const uint64_t rows = ((uint64_t)b->n_blocks + 15) / 16;
-  {
-    std::lock_guard<std::mutex> g(c->mu);
-    tpz_err r = get_workspace(c, stream, b->n_blocks, &w);
-    if (r != TPZ_SUCCESS) return r;
-    r = grow(stream, &w->d_scan, &w->scan_cap, rows * 64);
-    if (r != TPZ_SUCCESS) return r;
-  }
-  TPZ_HIP(hipMemsetAsync(w->d_scan, 0, rows * 64, (hipStream_t)stream));
-  uint32_t* tail = w->d_tail;
-  const uint64_t st = (uint64_t)b->n_blocks + 1;
-  tpz::LaunchArgs a{};
-  a.src = b->d_src;
-  a.ext = b->d_ext;
-  a.src_bytes = b->src_bytes;
-  a.n_blocks = b->n_blocks;
-  a.crc_tables = c->d_tables;
-  a.data = nullptr;
-  a.ends = o->d_ends;
-  a.count = o->d_count;
-  a.status = o->d_status;
-  a.crc = o->d_crc;
-  a.tail = tail;
-  a.defer_count = tail + tpz::kTailBig;
-  a.defer_list = w->d_defer + 4;
-  a.spill_count = tail + tpz::kTailSpill;
-  a.spill_list = w->d_defer + 4 + w->defer_cap;
-  a.bw_count = tail + tpz::kTailBw;
-  a.bw_list = nullptr;
-  a.rep = c->d_rep_tables;
-  a.spill = o->d_spill;
-  a.spill_cap = o->d_spill ? o->spill_cap : 0;
-  a.spill_off = o->d_spill_off;
-  a.spill_used = o->d_spill_used;
-  a.num_cus = c->num_cus;
-  a.big_scratch = w->d_big_scratch;
-  a.big_grid = c->num_cus;
-  a.efirst = d_first;
-  a.keys = o->d_keys;
-  a.vals = o->d_values;
-  a.kfirst = d_first + st;
-  a.vfirst = d_first + 2 * st;
-  a.scan_desc = static_cast<uint64_t*>(w->d_scan);
-  a.scan_first = d_first;
-  a.cap_e = pair_cap;
-  a.cap_k = key_cap;
-  a.cap_v = value_cap;
   tpz::launch_decode(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;

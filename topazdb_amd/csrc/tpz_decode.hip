@@ -53,7 +53,7 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
 constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
 // wave path: a workgroup's rows are claimed kRowAhead row slots ahead, into a ring of kRowRing
-constexpr u32 kRowAhead = 4, kRowRing = 16;
+constexpr u32 kRowAhead = 4, kRowRing = 8;
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
@@ -1493,12 +1493,6 @@ struct Params {
   u32 chunk_shift;    // wave path: blocks claimed at a time = 2^chunk_shift (<= the row)
   u32* row_ctr;       // wave path: the rows of 16 blocks claimed so far (tail + kTailRow)
   u32* err;           // sticky error word (tail + kTailError)
-  // flat layout in one pass (tpz_decode_blocks_flat_scan): the row descriptors (8 u64 per row
-  // of 16 blocks, zeroed before the launch), the layout out (3 x (n_blocks + 1) u64: out.efirst,
-  // out.kfirst and out.vfirst point into it) and the columns' capacities
-  u64* scan_desc;
-  u64* scan_first;
-  u64 cap_e, cap_k, cap_v;
 };
 
 
@@ -1509,267 +1503,22 @@ __device__ __forceinline__ T const_load(const T* base, u64 i) {
   return reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(base))[i];
 }
 
-// ------------------------------------------------------------------ flat layout in one pass
-// tpz_decode_blocks_flat_scan: the decode computes the flat layout itself instead of reading
-// tpz_flat_layout's. Each row of 16 blocks' reservations (tpz_flat.hip's rules: the entries,
-// key bytes and value bytes the block's decode yields when its CRC matches) are counted by one
-// wave of the row's workgroup, the layout wave (the last of the 16; the other 15 decode), which
-// runs kRowAhead row slots ahead of the decode waves: a block's predecessors are decoded at the
-// same time as the block itself, so a block cannot wait for their counts, but
-// a row can be counted as soon as its number is claimed. The layout wave reads the 16 blocks'
-// headers, offsets and key / value lengths with gathered loads (16 blocks per round, three
-// dependent rounds: the lines then sit in L2 / the Infinity Cache for the decode's own read),
-// publishes the row's aggregate, finds the row's exclusive prefix by a decoupled look-back over
-// the rows before it (64 rows per round, agent-scope words), publishes the row's inclusive
-// prefix, and hands every block its column starts through an LDS ring (and the layout out).
-constexpr u32 kInfoRing = kRowRing;           // row slots of layout info in LDS
-constexpr u32 kInfoStride = 52;               // u64 per slot: the tag, then 17 x {e, k, v} starts
-constexpr u32 kScanAhead = 6;                 // rows claimed ahead of the layout wave's counting
-constexpr u64 kDescValid = 1ull << 63;        // a descriptor word holds a value
-// The layout info of one row slot: tag (the slot, once written), then block j's entry, key and
-// value starts at words 1 + 3 j .. 3 + 3 j, j <= 16 (j = 16 or the row's block count: its ends).
-struct InfoRing {
-  u64* base;   // LDS: kInfoRing x kInfoStride u64
-  __device__ __forceinline__ u64* entry(u32 slot) const { return base + (slot % kInfoRing) * kInfoStride; }
-};
-static_assert(kGuard + kInfoRing * kInfoStride * 8 <= (u32)kSlotBytes && 1 + 3 * 17 <= kInfoStride &&
-              kGuard % 16 == 0,
-              "info ring in the layout wave's slot");
-
-__device__ __forceinline__ u64 desc_load(const u64* a) {
-  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void desc_store(u64* a, u64 v) {
-  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32 gbe16(const uint8_t* q) { return ((u32)q[0] << 8) | q[1]; }
-__device__ __forceinline__ u64 wave_sum64(u64 x) {
-  for (int o = 32; o >= 1; o >>= 1) {
-    const u32 lo = (u32)__shfl_xor((int)(u32)x, o), hi = (u32)__shfl_xor((int)(u32)(x >> 32), o);
-    x += ((u64)hi << 32) | lo;
-  }
-  return x;
-}
-
-// The layout wave's loop: row slots t = 0, 1, ... of this workgroup until a row past the batch.
-// The layout wave is also the workgroup's only row claimer, kScanAhead slots ahead of its own
-// counting: one claim at a time, so the workgroup's rows increase with its slots (the first row
-// past the batch ends the loop, and row_end tells the decode waves that every later slot is past
-// it too). Before it claims the row of slot t + kScanAhead it waits until the decode waves have
-// taken all 16 blocks of slot t + kScanAhead - kRowRing (info_done), the slot whose row entry
-// that claim overwrites (its info entry was slot t's, overwritten kScanAhead iterations later).
-// (No cycle: a decode wave waits for the row of slot s, claimed after slot s - kRowRing is
-// taken, only while it holds a block of that slot if all chunks in between were claimed. With
-// the claim blocked, slots s - kScanAhead .. s - 1 have no info yet, so their 8 kScanAhead = 48
-// chunks (pairs of blocks, launch_decode) could only be held, not decoded, and the 15 decode
-// waves hold at most 29 chunks besides the waiting one's current block.)
-static_assert(kScanAhead < kRowRing && 8 * kScanAhead > 2 * 14 + 1, "scan claim distance");
-__device__ __forceinline__ void scan_claim_row(const Params& p, u32* row_val, u32* row_slot, u32 s) {
-  if (lane_id() == 0) {
-    row_val[s % kRowRing] = atomicAdd(p.row_ctr, 1u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(&row_slot[s % kRowRing], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-__device__ __forceinline__ void layout_rows(const Params& p, u32* row_val, u32* row_slot,
-                                         u32* row_end, u32* info_done, InfoRing ring) {
-  const u32 lane = lane_id();
-  const u64 st = (u64)p.n_blocks + 1;
-  for (u32 s = 0; s < kScanAhead; s++) scan_claim_row(p, row_val, row_slot, s);
-  for (u32 t = 0;; t++) {
-    const u32 s_new = t + kScanAhead;
-    if (s_new >= kRowRing && lane == 0) {
-      u32* done = &info_done[(s_new - kRowRing) % kInfoRing];
-      u32 spins = 0;
-      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kWavesPerWG) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins == (1u << 22)) { atomicOr(p.err, 2u); break; }
-      }
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // the row of slot t (claimed kScanAhead iterations ago, by this wave)
-    const u32 r = uni(row_val[t % kRowRing]);
-    scan_claim_row(p, row_val, row_slot, s_new);
-    const u64 b0 = (u64)r * kWavesPerWG;
-    if (b0 >= p.n_blocks) {
-      if (lane == 0) __hip_atomic_store(row_end, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      break;
-    }
-    const u32 nb = (u32)min((u64)kWavesPerWG, (u64)p.n_blocks - b0);
-    // extents (lanes 0..nb), then each block's header: lane j < nb holds block j's
-    const u64 ex = p.ext[b0 + (lane <= nb ? lane : nb)];
-    const u64 sj = ex;
-    const u64 ej = ((u64)(u32)__shfl_down((int)(u32)(ex >> 32), 1) << 32) | (u32)__shfl_down((int)(u32)ex, 1);
-    u32 nj = 0, okj = 0;
-    if (lane < nb) {
-      const u64 len = ej - sj;
-      const u32 tag = len ? p.src[ej - 1] : 0u;
-      const u32 n = len >= 2 ? gbe16(p.src + sj) : 0u;
-      const u64 P = len >= 5 ? len - 5 : 0;
-      okj = len >= 5 && tag == 1 && P >= 2 && P >= 2 + 2 * (u64)n;               // tpz_flat.hip
-      nj = okj ? n : 0u;
-    }
-    u32 nmax = nj;
-    for (int o = 32; o >= 1; o >>= 1) nmax = max(nmax, (u32)__shfl_xor((int)nmax, o));
-    // the entries, 64 per group, all blocks of the row at once per round (lane = entry)
-    u64 kacc = 0, vacc = 0;   // lane j < nb: block j's key / value bytes
-    u64 sv = sj, ev = ej;
-    u32 nv = nj;
-    for (u32 g0 = 0; g0 < nmax; g0 += kWave) {
-      const u32 i = g0 + lane;
-      u32 off[kWavesPerWG], kl[kWavesPerWG];
-      // (each round reads the blocks' extents from the lanes again: held as scalars across the
-      // three rounds they spilled)
-      asm volatile("" : "+v"(sv), "+v"(ev), "+v"(nv));
-      const u64 sj = sv, ej = ev;
-      const u32 nj = nv;
-#pragma unroll
-      for (int j = 0; j < (int)kWavesPerWG; j++) {
-        const u64 s = (u64)readlane((u32)sj, j) | (u64)readlane((u32)(sj >> 32), j) << 32;
-        const u32 n = readlane(nj, j);
-        off[j] = ((u32)j < nb && i < n) ? gbe16(p.src + s + 2 + 2 * (u64)i) : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int j = 0; j < (int)kWavesPerWG; j++) {
-        const u64 s = (u64)readlane((u32)sj, j) | (u64)readlane((u32)(sj >> 32), j) << 32;
-        const u64 e = (u64)readlane((u32)ej, j) | (u64)readlane((u32)(ej >> 32), j) << 32;
-        const u32 n = readlane(nj, j);
-        const u64 db = 2 + 2 * (u64)n, dl = (e - s) - 5 - db;
-        kl[j] = (off[j] != 0xFFFFFFFFu && off[j] + 2 <= dl) ? gbe16(p.src + s + db + off[j]) : 0xFFFFFFFFu;
-      }
-      asm volatile("" : "+v"(sv), "+v"(ev), "+v"(nv));
-#pragma unroll
-      for (int j = 0; j < (int)kWavesPerWG; j++) {
-        const u64 s = (u64)readlane((u32)sv, j) | (u64)readlane((u32)(sv >> 32), j) << 32;
-        const u64 e = (u64)readlane((u32)ev, j) | (u64)readlane((u32)(ev >> 32), j) << 32;
-        const u32 n = readlane(nv, j);
-        const u64 db = 2 + 2 * (u64)n, dl = (e - s) - 5 - db;
-        u64 kc = 0, vc = 0;
-        if (kl[j] != 0xFFFFFFFFu) {
-          const u64 o = off[j], k = kl[j];
-          if (o + 2 + k <= dl) kc = k;                                             // iterator.rs:77-78
-          if (o + 4 + k <= dl) {
-            const u64 v = gbe16(p.src + s + db + o + 2 + k);                       // :80
-            if (o + 4 + k + v <= dl) vc = v;                                       // :81-82
-          }
-        }
-        const u64 K = wave_sum64(kc), V = wave_sum64(vc);
-        if (lane == (u32)j) {
-          kacc += K;
-          vacc += V;
-        }
-      }
-    }
-    // the row's prefixes: lanes j < nb, exclusive within the row
-    u64 e_in = lane < nb ? nj : 0, k_in = lane < nb ? kacc : 0, v_in = lane < nb ? vacc : 0;
-    u64 ei = e_in, ki = k_in, vi = v_in;   // inclusive scans over lanes 0..15
-    for (u32 o = 1; o < kWavesPerWG; o <<= 1) {
-      const u64 ea = ((u64)(u32)__shfl_up((int)(u32)(ei >> 32), o) << 32) | (u32)__shfl_up((int)(u32)ei, o);
-      const u64 ka = ((u64)(u32)__shfl_up((int)(u32)(ki >> 32), o) << 32) | (u32)__shfl_up((int)(u32)ki, o);
-      const u64 va = ((u64)(u32)__shfl_up((int)(u32)(vi >> 32), o) << 32) | (u32)__shfl_up((int)(u32)vi, o);
-      if (lane >= o) { ei += ea; ki += ka; vi += va; }
-    }
-    const u32 tl = kWavesPerWG - 1;
-    const u64 ER = (u64)readlane((u32)ei, tl) | (u64)readlane((u32)(ei >> 32), tl) << 32;
-    const u64 KR = (u64)readlane((u32)ki, tl) | (u64)readlane((u32)(ki >> 32), tl) << 32;
-    const u64 VR = (u64)readlane((u32)vi, tl) | (u64)readlane((u32)(vi >> 32), tl) << 32;
-    u64* d = p.scan_desc + 8 * (u64)r;
-    if (lane == 0) {
-      desc_store(d + 0, kDescValid | ER);
-      desc_store(d + 1, kDescValid | KR);
-      desc_store(d + 2, kDescValid | VR);
-    }
-    // look back over rows r - 1, r - 2, ...: lane l reads row base - l
-    u64 XE = 0, XK = 0, XV = 0;
-    int64_t base = (int64_t)r - 1;
-    u32 spins = 0;
-    while (base >= 0) {
-      const int64_t q = base - (int64_t)lane;
-      u64 a0 = 0, a1 = 0, a2 = 0, i0 = 0, i1 = 0, i2 = 0;
-      bool inc = q < 0, agg = q < 0;   // (before row 0: an inclusive prefix of 0)
-      if (q >= 0) {
-        const u64* dq = p.scan_desc + 8 * (u64)q;
-        i0 = desc_load(dq + 4); i1 = desc_load(dq + 5); i2 = desc_load(dq + 6);
-        a0 = desc_load(dq + 0); a1 = desc_load(dq + 1); a2 = desc_load(dq + 2);
-        inc = (i0 & i1 & i2 & kDescValid) != 0;
-        agg = (a0 & a1 & a2 & kDescValid) != 0;
-      }
-      const u64 mi = __ballot(inc);
-      const u32 f = mi ? (u32)__builtin_ctzll(mi) : 64u;      // the nearest row with an inclusive
-      const u64 below = f == 64 ? ~0ull : ((1ull << f) - 1);
-      if ((__ballot(agg) & below) != below) {                 // a row before it not counted yet
-        __builtin_amdgcn_s_sleep(4);
-        if (++spins == (1u << 20)) { if (lane == 0) atomicOr(p.err, 2u); break; }
-        continue;
-      }
-      const bool take_a = lane < f, take_i = lane == f;
-      const u64 ce = take_a ? (a0 & ~kDescValid) : take_i ? (i0 & ~kDescValid) : 0;
-      const u64 ck = take_a ? (a1 & ~kDescValid) : take_i ? (i1 & ~kDescValid) : 0;
-      const u64 cv = take_a ? (a2 & ~kDescValid) : take_i ? (i2 & ~kDescValid) : 0;
-      XE += wave_sum64(ce);
-      XK += wave_sum64(ck);
-      XV += wave_sum64(cv);
-      if (f < 64) break;
-      base -= 64;
-    }
-    if (lane == 0) {
-      desc_store(d + 4, kDescValid | (XE + ER));
-      desc_store(d + 5, kDescValid | (XK + KR));
-      desc_store(d + 6, kDescValid | (XV + VR));
-    }
-    // the blocks' starts (lane nb: the row's ends): to the decode waves (LDS), and to the
-    // layout out (the next row writes this row's ends as its starts, the last row the totals)
-    u64* en = ring.entry(t);
-    if (lane <= nb) {
-      const bool in = lane < nb;   // (lane 16's shuffled scan misses lane 0: the row's ends directly)
-      const u64 e0 = XE + (in ? ei - e_in : ER), k0 = XK + (in ? ki - k_in : KR), v0 = XV + (in ? vi - v_in : VR);
-      u64* w = en + 1 + 3 * lane;
-      w[0] = e0;
-      w[1] = k0;
-      w[2] = v0;
-      if (in) {
-        p.scan_first[b0 + lane] = e0;
-        p.scan_first[st + b0 + lane] = k0;
-        p.scan_first[2 * st + b0 + lane] = v0;
-      }
-    }
-    if (b0 + nb == p.n_blocks && lane == 0) {                 // the totals
-      p.scan_first[p.n_blocks] = XE + ER;
-      p.scan_first[st + p.n_blocks] = XK + KR;
-      p.scan_first[2 * st + p.n_blocks] = XV + VR;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(reinterpret_cast<u32*>(en), t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
 // ------------------------------------------------------------------ wave path kernel
 #ifdef TPZ_ABL_ONCHIP
 // diagnostic (timing only): every wave decodes blocks 0..4095 over and over, so loads and stores
 // stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
 constexpr u32 kOnchipMask = 4095;
 #endif
-template <bool FLAT, bool SCAN = false>
+template <bool FLAT>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
-  // (scan: the layout wave's slot holds the layout info ring, past the guard bytes every wave
-  // zeroes in its slot; tags ~0 = no slot written yet)
-  const InfoRing ring{reinterpret_cast<u64*>(lds + kWaveTabBytes + (kWavesPerWG - 1) * kSlotBytes + kGuard)};
-  if (SCAN && threadIdx.x < kInfoRing) ring.entry(threadIdx.x)[0] = ~0ull;
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   __shared__ Out out_lds;             // the worklist pointers for the rare paths (see above)
   // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
   // row_slot[s % kRowRing] == s (see claim_chunk)
   __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
-  // (scan: the layout wave claims every row; row_end is its first slot past the batch and
-  // info_done[s % kInfoRing] counts the blocks of slot s the decode waves have taken)
-  __shared__ u32 row_end, info_done[kInfoRing];
-  if (SCAN) {
-    if (threadIdx.x < kRowRing) row_slot[threadIdx.x] = ~0u;
-    if (threadIdx.x < kInfoRing) info_done[threadIdx.x] = 0;
-    if (threadIdx.x == 0) row_end = ~0u;
-  } else if (threadIdx.x < kRowAhead && p.chunk_shift < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
+  if (threadIdx.x < kRowAhead && p.chunk_shift < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
     row_val[threadIdx.x] = atomicAdd(p.row_ctr, 1u);
     row_slot[threadIdx.x] = threadIdx.x;
   } else if (threadIdx.x < kRowRing) {
@@ -1839,46 +1588,33 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // blocks, a window of claimed rows buys nothing, and a row per claim would be a global atomic
   // per 16 blocks waited for by the next 16 waves; their rows stay static, r * grid + blockIdx.x.)
   const bool dyn_rows = rshift != 0;
-  if (SCAN && wid == kWavesPerWG - 1) {   // the layout wave (after load_tables' barrier: none later)
-    layout_rows(p, row_val, row_slot, &row_end, info_done, ring);
-    return;
-  }
-  // (sl: the chunk's row slot, for the scan's layout info)
-  auto claim_chunk = [&](u32& sl) -> u32 {
+  auto claim_chunk = [&]() -> u32 {
     publish();
     u32 q = 0;
     if (lane == 0) q = atomicAdd(&chunk_next, 1u);
     q = uni(q);
-    if (!dyn_rows && !SCAN) {
-      sl = q;
+    if (!dyn_rows) {
       const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
       return f < p.n_blocks ? (u32)f : p.n_blocks;
     }
     const u32 slot_q = q >> rshift;
-    sl = slot_q;
-    if (!SCAN && (q & ((1u << rshift) - 1u)) == 0) {
+    if ((q & ((1u << rshift) - 1u)) == 0) {
       pend_slot = slot_q + kRowAhead;
       if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
     }
     u32 row = 0;
     if (lane == 0) {
       u32 spins = 0;
-      bool got = true;
       while (__hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP) != slot_q) {
-        if (SCAN && __hip_atomic_load(&row_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= slot_q) {
-          got = false;                 // (scan: a slot past the layout wave's last row)
-          break;
-        }
         __builtin_amdgcn_s_sleep(2);
         if (++spins == (1u << 22)) {   // never expected: report it, and end this wave's work
           atomicOr(p.err, 2u);
-          got = false;
           break;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      row = got ? row_val[slot_q % kRowRing] : 0xFFFFFFFFu;
+      row = spins == (1u << 22) ? 0xFFFFFFFFu : row_val[slot_q % kRowRing];
     }
     row = uni(row);
     const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
@@ -1917,7 +1653,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     const u64 ge = ((u64)ghi << 32) | glo;
     const u32 cf = chunk_first(q), bb = cf + lane;     // (lane < n_blocks - cf: no wrap)
     const bool lng = lane < kChunk && lane < p.n_blocks - cf && ge - gs > kWaveMaxLen;
-    if (SCAN || !__ballot(lng)) return;   // (scan: routed when current, after its layout info)
+    if (!__ballot(lng)) return;
     const Out& oc = out_lds;
     u32 nent = 0xFFFFu;
     if (lng) nent = ((u32)p.src[gs] << 8) | p.src[gs + 1];
@@ -1928,8 +1664,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     defer_lanes(oc.spill_list, oc.spill_count, to_spill, (u32)bb);
     defer_lanes(oc.defer_list, oc.defer_count, lng && !to_bw && !to_spill, (u32)bb);
   };
-  u32 sl_cur = 0, sl_nxt = 0;
-  u32 q_cur = claim_chunk(sl_cur), q_nxt = claim_chunk(sl_nxt);
+  u32 q_cur = claim_chunk(), q_nxt = claim_chunk();
   load_group(q_cur, gs_cur);
   load_group(q_nxt, gs_nxt);
   triage_group(q_cur, gs_cur);
@@ -1943,7 +1678,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
                                              // one block ahead
   auto issue = [&](u32 bb, u32 jj, u64& s, u64& e) {
     if (bb >= p.n_blocks) return;
-    if (FLAT && !SCAN) {   // (scalar loads: uniform, and no VGPRs held across the block)
+    if (FLAT) {   // (scalar loads: uniform, and no VGPRs held across the block)
       kf_cur = const_load(p.out.kfirst, bb);
       vf_cur = const_load(p.out.vfirst, bb);
       ef_cur = const_load(p.out.efirst, bb);
@@ -1989,13 +1724,12 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
           *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
     }
     TPZ_STAMP(S, 0);
-    const u32 bcur = b, slcur = sl_cur;
+    const u32 bcur = b;
     if (++j == kChunk) {              // next chunk (its extent loads completed long ago)
       j = 0;
       q_cur = q_nxt;
-      sl_cur = sl_nxt;
       gs_cur = gs_nxt;
-      q_nxt = claim_chunk(sl_nxt);
+      q_nxt = claim_chunk();
       load_group(q_nxt, gs_nxt);
       triage_group(q_cur, gs_cur);
     }
@@ -2004,43 +1738,15 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     issue(b, j, s_cur, e_cur);       // next block's loads fly while this one decodes
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
-    u64 kfs = kf, vfs = vf, efs = ef;
-    bool room = true;
-    if (SCAN) {
-      // the block's layout from the layout wave (a row slot or more ahead of this wave, so the
-      // wait is not expected to spin); blocks past the columns' capacities are not written
-      publish();
-      const u64* en = ring.entry(slcur);
-      {                                // (a wave-uniform wait: no divergent loop in the decode loop)
-        u32 spins = 0;
-        while (uni(__hip_atomic_load(reinterpret_cast<const u32*>(en), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != slcur) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins == (1u << 22)) {
-            if (lane == 0) atomicOr(p.err, 2u);
-            break;
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const u64* w = en + 1 + 3 * (bcur & (kWavesPerWG - 1));
-      efs = uni64(w[0]);               // (uniform: scalars, as the two-pass decode's starts)
-      kfs = uni64(w[1]);
-      vfs = uni64(w[2]);
-      room = uni64(w[3]) <= p.cap_e && uni64(w[4]) <= p.cap_k && uni64(w[5]) <= p.cap_v;   // (the next block's starts)
-      // taken (after the reads: a wave's LDS operations complete in order)
-      if (lane == 0) __hip_atomic_fetch_add(&info_done[slcur % kInfoRing], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (!room) put_meta(p.out, bcur, TPZ_BLOCK_SPILL_FULL, 0u, 0u);
-      else if (!fits) defer_to(out_lds.spill_list, out_lds.spill_count, bcur);   // (flat: every long block)
-    }
-    if (fits && room) {
+    if (fits) {
 #ifdef TPZ_ABL_ONCHIP
       const u32 bdec = bcur & kOnchipMask;
 #else
       const u32 bdec = bcur;
 #endif
       decode_block<ColSmall, uint16_t, kWaveMapLen, false, FLAT>(tab, win, col, map, (u32)(s & 15u),
-                                                           len64, bdec, s, p.out, kshift, S, pd, kfs, vfs,
-                                                           efs, &out_lds);
+                                                           len64, bdec, s, p.out, kshift, S, pd, kf, vf,
+                                                           ef, &out_lds);
     }                                // (long blocks went to their worklist in triage_group)
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 5);
@@ -2507,22 +2213,13 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // per-chunk extent and header round trips are not hidden by any decode (64k: 2.07 ms with 16,
   // 2.20 with 4, 2.78 with 1).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
-  // (The one-pass flat decode always claims pairs: its layout wave claims the rows, and its
-  // no-cycle bound counts 8 chunks per row, see layout_rows.)
-  p.chunk_shift = avg > kWaveMaxLen && !a.scan_desc ? kRowShift : 1u;
+  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 1u;
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
-  p.scan_desc = a.scan_desc;
-  p.scan_first = a.scan_first;
-  p.cap_e = a.cap_e;
-  p.cap_k = a.cap_k;
-  p.cap_v = a.cap_v;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
-  if (a.scan_desc)
-    hipLaunchKernelGGL((decode_wave_kernel<true, true>), dim3(grid), dim3(kWGThreads), 0, stream, p);
-  else if (a.keys)
+  if (a.keys)
     hipLaunchKernelGGL(decode_wave_kernel<true>, dim3(grid), dim3(kWGThreads), 0, stream, p);
   else
     hipLaunchKernelGGL(decode_wave_kernel<false>, dim3(grid), dim3(kWGThreads), 0, stream, p);

@@ -104,12 +104,6 @@ struct LaunchArgs {
   const uint64_t* vfirst;
   uint32_t* tail;         // workspace: kTailCounters, zero at the launch (the tail kernel
                           // leaves them zero)
-  // flat layout in one pass (tpz_decode_blocks_flat_scan): the row descriptors (workspace, 8
-  // u64 per row of 16 blocks, zeroed before the launch), the layout out (efirst / kfirst /
-  // vfirst point into it) and the columns' capacities; null: the layout is an input
-  uint64_t* scan_desc;
-  uint64_t* scan_first;
-  uint64_t cap_e, cap_k, cap_v;
 };
 // Pair index of block b's first {kend, vend}: the exact layout's d_entry_first[b], or the
 // slotted tpz_entry_base.
