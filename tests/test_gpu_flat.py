@@ -174,3 +174,34 @@ def test_flat_golden_sst(ctx, name):
     cols, g, o = flat_parity(ctx, src, ext, whole_columns=True)
     for i, eb in enumerate(exp["blocks"]):
         assert g.crc_actual[i] == eb["crc"] and g.count[i] == eb["n"]
+
+
+@pytest.mark.parametrize("kind", ["4k", "zipf"])
+def test_flat_full_size(ctx, kind):
+    """BASELINE.json's metric batch (2^20 blocks, 4.36 GB for 4k) into the flat columns: every
+    block OK with its count, the key and value columns equal to the generator's keys and values
+    back to back, every {kend, vend} pair exact (bench.validate_flat), and a 256-block sample at
+    a random position against the oracle's decode."""
+    from bench import make_shard, validate_flat
+    nb = 1 << 20
+    src, ext, gen, n_ent, _, _ = make_shard(kind, nb, 0)
+    batch = DeviceBatch(src, ext)
+    cols = decode_flat(ctx, batch).complete()
+    dev = torch.device("cuda", 0)
+    validate_flat(cols, n_ent, gen, dev)
+    del gen
+    rng = np.random.default_rng(11)
+    b0 = int(rng.integers(0, nb - 256))
+    b1 = b0 + 256
+    sub = np.ascontiguousarray(src[int(ext[b0]):int(ext[b1])])
+    o = O.decode_batch(sub, (ext[b0:b1 + 1] - ext[b0]).astype(np.uint64))
+    first = cols.first[:, [b0, b1]].cpu().numpy()
+    assert (o.status == O.OK).all()
+    assert cols.keys[int(first[1, 0]):int(first[1, 1])].cpu().numpy().tobytes() == o.keys.tobytes()
+    assert cols.values[int(first[2, 0]):int(first[2, 1])].cpu().numpy().tobytes() == o.vals.tobytes()
+    ends = cols.ends[2 * int(first[0, 0]):2 * int(first[0, 1])].cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(cols.count[b0:b1].cpu().numpy(), o.count)
+    ke = ends[0::2].astype(np.int64)
+    j = np.concatenate([np.arange(c) for c in o.count])
+    ks = np.where(j == 0, 0, np.roll(ke, 1))
+    np.testing.assert_array_equal(ke - ks, o.klen)
