@@ -50,8 +50,9 @@ extern "C" {
  *      the exact ends layout (tpz_columns.d_entry_first, tpz_table.d_entry_first)
  *   5  the flat layout: tpz_flat_layout + tpz_decode_blocks_flat (tpz_flat_columns); no
  *      existing struct or status changed
+ *   6  claimed LZ4 sizes: tpz_decompressed_sizes_claimed, tpz_decompress_check, TPZ_ERR_SIZES
  * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
-#define TPZ_ABI_VERSION 5
+#define TPZ_ABI_VERSION 6
 int tpz_abi_version(void);
 
 /* ---- API return codes ------------------------------------------------------------------- */
@@ -61,7 +62,8 @@ typedef enum {
   TPZ_ERR_HIP = -2,         /* a HIP runtime call failed (tpz_last_error has the text)        */
   TPZ_ERR_NO_DEVICE = -3,   /* no gfx950 device with that index                               */
   TPZ_ERR_NOMEM = -4,
-  TPZ_ERR_INTERNAL = -5     /* a device-side consistency check failed (tpz_decode_check)      */
+  TPZ_ERR_INTERNAL = -5,    /* a device-side consistency check failed (tpz_decode_check)      */
+  TPZ_ERR_SIZES = -6        /* claimed codec sizes were not exact (tpz_decompress_check)      */
 } tpz_err;
 
 /* ---- per-block outcome (written to columns.status[i]) ------------------------------------
@@ -457,6 +459,20 @@ tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
  * binds; restated in oracle/tpz_lz4.c and pinned against liblz4 in tests/test_lz4_oracle.py). */
 tpz_err tpz_decompressed_sizes(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_size,
                                void* stream);
+/* Step 1 without LZ4's walk: a tag-3 block reports its size prefix + 1 (what
+ * lz4::block::decompress allocates, compress.rs:108-111; the exact length of every stream
+ * lz4::block::compress writes) instead of the length its stream decodes to; the exact walk only
+ * where the prefix is invalid or larger than any stream of that length can decode to. Every other
+ * block as tpz_decompressed_sizes. A stream that then decodes to another length or fails sets a
+ * sticky word of the stream's workspace in tpz_decompress_blocks (that block's output is
+ * CODEC_ERROR, the layout is not the exact one): tpz_decompress_check reports it, and the caller
+ * sizes the batch with tpz_decompressed_sizes and decompresses it again. Asynchronous on
+ * `stream`. */
+tpz_err tpz_decompressed_sizes_claimed(tpz_ctx* ctx, const tpz_batch* batch, uint64_t* d_size,
+                                       void* stream);
+/* Synchronizes `stream`; TPZ_ERR_SIZES (and the word cleared) when a tpz_decompress_blocks on it
+ * since the previous check ran over claimed sizes that were not exact, TPZ_SUCCESS otherwise. */
+tpz_err tpz_decompress_check(tpz_ctx* ctx, void* stream);
 tpz_err tpz_decompress_blocks(tpz_ctx* ctx, const tpz_batch* batch, uint8_t* d_dst,
                               const uint64_t* d_dst_ext, uint8_t* d_status, void* stream);
 

@@ -17,6 +17,7 @@ pub const TPZ_ERR_HIP: TpzErr = -2;
 pub const TPZ_ERR_NO_DEVICE: TpzErr = -3;
 pub const TPZ_ERR_NOMEM: TpzErr = -4;
 pub const TPZ_ERR_INTERNAL: TpzErr = -5;
+pub const TPZ_ERR_SIZES: TpzErr = -6;
 
 /// `tpz_block_status`, one byte per block in `d_status` / `h_status`.
 pub const TPZ_BLOCK_OK: u8 = 0;
@@ -35,7 +36,7 @@ pub const TPZ_ENTRY_OK: u8 = 0;
 pub const TPZ_ENTRY_BAD_VALUE: u8 = 1;
 pub const TPZ_ENTRY_BAD_KEY: u8 = 2;
 
-pub const TPZ_ABI_VERSION: c_int = 5;
+pub const TPZ_ABI_VERSION: c_int = 6;
 pub const TPZ_LDS_BLOCK_BYTES: u32 = 94192;
 pub const TPZ_BIGWAVE_BLOCK_BYTES: u32 = 0x40000000;
 pub const TPZ_PLAN_ASYNC_MAX_BLOCK: u32 = 10242;
@@ -182,6 +183,9 @@ extern "C" {
                             d_status: *mut u8, stream: *mut c_void) -> TpzErr;
     pub fn tpz_decompressed_sizes(ctx: *mut TpzCtx, batch: *const TpzBatch, d_size: *mut u64,
                                   stream: *mut c_void) -> TpzErr;
+    pub fn tpz_decompressed_sizes_claimed(ctx: *mut TpzCtx, batch: *const TpzBatch,
+                                          d_size: *mut u64, stream: *mut c_void) -> TpzErr;
+    pub fn tpz_decompress_check(ctx: *mut TpzCtx, stream: *mut c_void) -> TpzErr;
     pub fn tpz_decompress_blocks(ctx: *mut TpzCtx, batch: *const TpzBatch, d_dst: *mut u8,
                                  d_dst_ext: *const u64, d_status: *mut u8,
                                  stream: *mut c_void) -> TpzErr;

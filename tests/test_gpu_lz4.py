@@ -134,3 +134,76 @@ def test_config_batch_lz4(ctx):
     src, ext = synth.make_region("4k", 5000)
     s2, e2 = synth.lz4_blocks(src, ext)
     assert_parity(ctx, s2, e2, expect_all_ok=True)
+
+
+def device_sizes(ctx, blocks, claimed):
+    import torch
+    from topazdb_amd.batch import DeviceBatch
+    src, ext = batch_of(blocks)
+    b = DeviceBatch(np.ascontiguousarray(src), ext)
+    size = torch.empty(len(blocks), dtype=torch.int64, device="cuda")
+    ctx.decompressed_sizes_ptrs(b.src.data_ptr(), b.ext.data_ptr(), b.n_blocks, b.src_bytes,
+                                size.data_ptr(), claimed=claimed)
+    torch.cuda.synchronize()
+    return size.cpu().numpy()
+
+
+def decompress_with_sizes(ctx, blocks, claimed):
+    """tpz_decompressed_sizes(_claimed) + prefix sum + tpz_decompress_blocks, then
+    tpz_decompress_check: (statuses, check result)."""
+    import torch
+    from topazdb_amd.batch import DeviceBatch
+    src, ext = batch_of(blocks)
+    b = DeviceBatch(np.ascontiguousarray(src), ext)
+    n = b.n_blocks
+    size = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx.decompressed_sizes_ptrs(b.src.data_ptr(), b.ext.data_ptr(), n, b.src_bytes, size.data_ptr(),
+                                claimed=claimed)
+    dext = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    torch.cumsum(size, 0, out=dext[1:])
+    dst = torch.empty(int(dext[-1]) + 16, dtype=torch.uint8, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.decompress_ptrs(b.src.data_ptr(), b.ext.data_ptr(), n, b.src_bytes, dst.data_ptr(),
+                        dext.data_ptr(), st.data_ptr())
+    ok = ctx.decompress_check()
+    return st.cpu().numpy(), ok
+
+
+def test_claimed_sizes(ctx):
+    """tpz_decompressed_sizes_claimed: an LZ4 block takes its size prefix. Streams the compressor
+    wrote: the claims are the exact sizes and tpz_decompress_check passes. A stream that decodes
+    to fewer bytes than its prefix (lz4::block::decompress keeps what LZ4_decompress_safe returns,
+    compress.rs:108-111) or fails: the check reports it, and decompress_batch's exact redo gives
+    the oracle's bytes and statuses. A prefix no stream of that length can reach: the sizes pass
+    walks that block (exact size, check passes)."""
+    rng = np.random.default_rng(21)
+    good = [b for b in lz4_random_blocks(rng, 200) if b and b[-1] == 3]
+    assert len(good) > 100
+    np.testing.assert_array_equal(device_sizes(ctx, good, True), device_sizes(ctx, good, False))
+    st, ok = decompress_with_sizes(ctx, good, True)
+    assert ok and (st == _lib.BLOCK_OK).all()
+    # a short stream: the prefix 10 bytes past what the stream decodes to
+    short = bytearray(good[7])
+    true = int.from_bytes(short[0:4], "little")
+    short[0:4] = (true + 10).to_bytes(4, "little")
+    # an Err stream (truncated), and an implausible claim on a short stream
+    bad = good[9][:len(good[9]) // 2] + b"\x03"
+    huge = (0x7E000000).to_bytes(4, "little") + good[11][4:]
+    mixed = good[:20] + [bytes(short)] + good[20:40] + [bad] + good[40:60] + [huge]
+    claimed, exact = device_sizes(ctx, mixed, True), device_sizes(ctx, mixed, False)
+    assert claimed[20] == true + 11 and exact[20] == true + 1
+    assert claimed[-1] == exact[-1]                        # walked: no stream reaches 0x7E000000
+    st, ok = decompress_with_sizes(ctx, mixed, True)
+    assert not ok                                          # the short and the Err stream
+    st, ok = decompress_with_sizes(ctx, mixed, False)
+    assert ok
+    outs, st = device_codec(ctx, mixed)                    # claimed, then the exact redo
+    for i, b in enumerate(mixed):
+        ost, ob = oracle_codec(b)
+        assert st[i] == ost, (i, st[i], ost)
+        if ost == O.OK:
+            assert outs[i] == ob, i
+    assert st[20] == _lib.BLOCK_OK and len(outs[20]) == true + 1
+    # the check reads and clears the word: a later clean batch passes
+    st, ok = decompress_with_sizes(ctx, good[:30], True)
+    assert ok

@@ -16,13 +16,14 @@ LIB_PATH = os.environ.get("TPZ_LIB_PATH") or os.path.join(HERE, "libtpz_gpu.so")
 HEADER = os.path.join(ROOT, "include", "tpz_gpu.h")
 
 # tpz_err
-SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM, ERR_INTERNAL = 0, -1, -2, -3, -4, -5
+SUCCESS, ERR_INVALID_ARG, ERR_HIP, ERR_NO_DEVICE, ERR_NOMEM, ERR_INTERNAL, ERR_SIZES = \
+    0, -1, -2, -3, -4, -5, -6
 # tpz_block_status
 (BLOCK_OK, BLOCK_EMPTY, BLOCK_BAD_TAG, BLOCK_UNSUPPORTED_CODEC, BLOCK_CHECKSUM_MISMATCH,
  BLOCK_MALFORMED, BLOCK_OK_SPILLED, BLOCK_SPILL_FULL, BLOCK_CODEC_ERROR, BLOCK_BAD_ENTRY) = range(10)
 # tpz_entry_class (BAD_ENTRY blocks)
 ENTRY_OK, ENTRY_BAD_VALUE, ENTRY_BAD_KEY = 0, 1, 2
-ABI_VERSION = 5           # TPZ_ABI_VERSION this binding was written against
+ABI_VERSION = 6           # TPZ_ABI_VERSION this binding was written against
 LDS_BLOCK_BYTES = 94192   # TPZ_LDS_BLOCK_BYTES: longer blocks with 64+ entries take the spill path
 BIGWAVE_BLOCK_BYTES = 0x40000000   # TPZ_BIGWAVE_BLOCK_BYTES
 
@@ -120,9 +121,11 @@ def lib() -> C.CDLL:
         L.tpz_verify_files.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
                                        C.c_void_p]
         L.tpz_verify_files.restype = C.c_int
-        L.tpz_decompressed_sizes.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p,
-                                             C.c_void_p]
-        L.tpz_decompressed_sizes.restype = C.c_int
+        for f in ("tpz_decompressed_sizes", "tpz_decompressed_sizes_claimed"):
+            getattr(L, f).argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
+            getattr(L, f).restype = C.c_int
+        L.tpz_decompress_check.argtypes = [C.c_void_p, C.c_void_p]
+        L.tpz_decompress_check.restype = C.c_int
         L.tpz_decompress_blocks.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p]
         L.tpz_decompress_blocks.restype = C.c_int
@@ -356,11 +359,24 @@ class Context:
         return status, crc, count, dext, plain[:int(dext[n])]
 
     def decompressed_sizes_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
-                                d_size: int, stream: int = 0) -> None:
-        """tpz_decompressed_sizes (compress::decode's codec step, compress.rs:95-113)."""
+                                d_size: int, stream: int = 0, claimed: bool = False) -> None:
+        """tpz_decompressed_sizes (compress::decode's codec step, compress.rs:95-113); claimed:
+        tpz_decompressed_sizes_claimed (LZ4 blocks take their size prefix, checked by
+        decompress_check after the decompress)."""
         b = Batch(d_src, d_ext, n_blocks, src_bytes)
-        check(lib().tpz_decompressed_sizes(self.handle, C.byref(b), C.c_void_p(d_size),
-                                           C.c_void_p(stream)), "tpz_decompressed_sizes")
+        name = "tpz_decompressed_sizes_claimed" if claimed else "tpz_decompressed_sizes"
+        check(getattr(lib(), name)(self.handle, C.byref(b), C.c_void_p(d_size), C.c_void_p(stream)),
+              name)
+
+    def decompress_check(self, stream: int = 0) -> bool:
+        """tpz_decompress_check: synchronizes the stream; False when a decompress on it since the
+        last check ran over claimed sizes that were not exact (the caller sizes the batch exactly
+        and decompresses it again), True otherwise."""
+        rc = lib().tpz_decompress_check(self.handle, C.c_void_p(stream))
+        if rc == ERR_SIZES:
+            return False
+        check(rc, "tpz_decompress_check")
+        return True
 
     def decompress_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int, d_dst: int,
                         d_dst_ext: int, d_status: int, stream: int = 0) -> None:

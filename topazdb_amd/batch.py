@@ -421,18 +421,21 @@ def verify_files(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | N
     return crc, st
 
 
-def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None):
+def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None,
+                     claimed: bool = True):
     """compress::decode's codec step (src/block/compress.rs:95-113) on the GPU: snappy (tag 2)
     and lz4 (tag 3) blocks become Uncompress blocks (tpz_decompressed_sizes, a device prefix sum
     of the sizes, tpz_decompress_blocks). Returns (DeviceBatch of the uncompressed blocks, codec status
     tensor); decode the former with decode_batch and take the codec status for blocks whose codec
-    step failed."""
+    step failed. claimed: LZ4 blocks sized by their size prefix (tpz_decompressed_sizes_claimed,
+    no acceptance walk); when tpz_decompress_check finds a block whose stream decoded to another
+    length or failed, the batch is sized exactly and decompressed again."""
     dev = _dev(ctx.device)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     nb = batch.n_blocks
     size = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
     ctx.decompressed_sizes_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
-                                size.data_ptr(), s.cuda_stream)
+                                size.data_ptr(), s.cuda_stream, claimed=claimed)
     with torch.cuda.stream(s):
         ext = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
         torch.cumsum(size[:nb], 0, out=ext[1:])
@@ -442,5 +445,7 @@ def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream
     st = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
     ctx.decompress_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
                         dst.data_ptr(), ext.data_ptr(), st.data_ptr(), s.cuda_stream)
+    if claimed and not ctx.decompress_check(s.cuda_stream):
+        return decompress_batch(ctx, batch, stream, claimed=False)
     out = DeviceBatch(dst, ext, ctx.device)
     return out, st

@@ -421,7 +421,8 @@ static tpz_err crc_ranges(tpz_ctx* c, const tpz_batch* r, uint32_t trailer, uint
   return TPZ_SUCCESS;
 }
 
-tpz_err tpz_decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size, void* stream) {
+static tpz_err decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size, void* stream,
+                                  bool claimed) {
   if (!c || !b || !d_size) return TPZ_ERR_INVALID_ARG;
   if (b->n_blocks == 0) return TPZ_SUCCESS;
   if (!b->d_src || !b->d_ext || (reinterpret_cast<uintptr_t>(b->d_src) & 15u))
@@ -433,9 +434,42 @@ tpz_err tpz_decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size,
   a.src_bytes = b->src_bytes;
   a.n_blocks = b->n_blocks;
   a.size = d_size;
+  a.claimed = claimed;
   tpz::launch_codec_sizes(a, (hipStream_t)stream);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;
+}
+
+tpz_err tpz_decompressed_sizes(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size, void* stream) {
+  return decompressed_sizes(c, b, d_size, stream, false);
+}
+
+tpz_err tpz_decompressed_sizes_claimed(tpz_ctx* c, const tpz_batch* b, uint64_t* d_size,
+                                       void* stream) {
+  return decompressed_sizes(c, b, d_size, stream, true);
+}
+
+tpz_err tpz_decompress_check(tpz_ctx* c, void* stream) {
+  if (!c) return TPZ_ERR_INVALID_ARG;
+  TPZ_HIP(hipSetDevice(c->device));
+  uint32_t* tail = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->ws.find(stream);
+    if (it != c->ws.end()) tail = it->second.d_tail;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (!tail) return hip_fail(hipStreamSynchronize(s), "tpz_decompress_check");
+  // read and clear the stream's word in stream order, as tpz_decode_check does
+  uint32_t flag = 0;
+  TPZ_HIP(hipMemcpyAsync(&flag, tail + tpz::kTailCodecInexact, 4, hipMemcpyDeviceToHost, s));
+  TPZ_HIP(hipMemsetAsync(tail + tpz::kTailCodecInexact, 0, 4, s));
+  TPZ_HIP(hipStreamSynchronize(s));
+  if (!flag) return TPZ_SUCCESS;
+  g_last_error = "tpz_decompress_blocks: an LZ4 block's claimed size was not its decoded length "
+                 "(an Err or a short stream); size the batch with tpz_decompressed_sizes and "
+                 "decompress it again";
+  return TPZ_ERR_SIZES;
 }
 
 tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
@@ -464,6 +498,7 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
   a.defer_count = w->d_defer;
   a.defer_list = w->d_defer + 4;
   a.num_cus = c->num_cus;
+  a.inexact = w->d_tail + tpz::kTailCodecInexact;
   tpz::launch_decompress(a, s);
   TPZ_HIP(hipGetLastError());
   return TPZ_SUCCESS;

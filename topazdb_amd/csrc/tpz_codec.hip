@@ -134,6 +134,8 @@ struct CodecParams {
   u32* defer_list;
   u32* defer_count;
   u32 group_pass;    // the lane kernels ran first (status 0xFF = left for the wave kernel)
+  u32 claimed;       // sizes kernel: LZ4 blocks take their size prefix (tpz_decompressed_sizes_claimed)
+  u32* inexact;      // decompress: sticky word, set when an LZ4 block's range is not its exact length
 };
 
 // ------------------------------------------------------------------ per-block work
@@ -600,6 +602,17 @@ __global__ __launch_bounds__(256) void codec_sizes_kernel(CodecParams p) {
   const u64 s = p.ext[i], e = p.ext[i + 1], len = e - s;
   const u32 tag = len ? p.src[e - 1] : 0u;
   if (tag == 3) {
+    if (p.claimed) {
+      // the size prefix (lz4::block::decompress allocates that much, compress.rs:108-111): the
+      // exact length of every stream the reference's compress wrote. A stream that decodes to
+      // another length or fails sets the decompress's sticky word (tpz_decompress_check); a
+      // claim no stream of this length can reach (LZ4 expands at most ~255x) takes the walk.
+      const int64_t c = lz4_prefix(p.src + s, len - 1);
+      if (c >= 0 && len > 5 && (u64)c <= 256 * (len - 5) + 64) {
+        p.size[i] = (u64)c + 1;
+        return;
+      }
+    }
     // the exact decoded length (LZ4 may decode fewer bytes than its prefix says); an Err
     // leaves a lone tag byte
     const int64_t r = p.src_bytes >= 16
@@ -673,6 +686,9 @@ __device__ __forceinline__ bool lz4_block(const CodecParams& p, u32 b, const Blo
   } else if (lane == 0) {
     if (dn) dst[dn - 1] = 0;                                   // decodes as BAD_TAG
     p.status[b] = (uint8_t)st;
+    // a range of 2+ bytes for a stream that failed or decoded to another length: only claimed
+    // sizes give one (the exact ones are 1 for an Err and the decoded length + 1 otherwise)
+    if (dn >= 2 && p.inexact) atomicOr(p.inexact, 1u);
   }
   __builtin_amdgcn_wave_barrier();
   return true;
@@ -1524,6 +1540,7 @@ void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream) {
   p.src_bytes = a.src_bytes;
   p.n_blocks = a.n_blocks;
   p.size = a.size;
+  p.claimed = a.claimed ? 1u : 0u;
   hipLaunchKernelGGL(codec_sizes_kernel, dim3((a.n_blocks + 255) / 256), dim3(256), 0, stream, p);
 }
 
@@ -1538,6 +1555,7 @@ void launch_decompress(const CodecLaunch& a, hipStream_t stream) {
   p.status = a.status;
   p.defer_list = a.defer_list;
   p.defer_count = a.defer_count;
+  p.inexact = a.inexact;
   if (a.n_blocks) {
     p.group_pass = 1;
     hipLaunchKernelGGL(snappy_ring_kernel, dim3((a.n_blocks + kRingWG - 1) / kRingWG), dim3(kRingWG),

@@ -128,6 +128,9 @@ enum TailCounter : int {
   // Sticky, past the counters the tail kernel zeroes: set when a tail workgroup's wait for the
   // big phase timed out (tpz_decode_check reports it and clears it)
   kTailError = kTailCounters,
+  // Sticky: set when tpz_decompress_blocks gave an LZ4 block a range that is not its exact length
+  // (claimed sizes, tpz_decompressed_sizes_claimed); tpz_decompress_check reports and clears it
+  kTailCodecInexact,
   kTailWords
 };
 __device__ __forceinline__ uint32_t tail_load(const uint32_t* c) {
@@ -315,6 +318,8 @@ struct CodecLaunch {
   uint32_t* defer_list;    // workspace: n_blocks entries
   uint32_t* defer_count;   // workspace: zeroed before the launch
   uint32_t num_cus;
+  bool claimed;            // tpz_decompressed_sizes_claimed
+  uint32_t* inexact;       // workspace: sticky, read and cleared by tpz_decompress_check
 };
 
 void launch_codec_sizes(const CodecLaunch& a, hipStream_t stream);
