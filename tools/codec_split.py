@@ -4,7 +4,7 @@ rocprofv3 --kernel-trace --stats run (diagnostic, GPU box):
 
     rocprofv3 --kernel-trace --stats -d OUT -o run -- python3 tools/codec_split.py --codec lz4
 
-Runs bench.codec_rate's codec() (tpz_decompressed_sizes + prefix sum + tpz_decompress_blocks)
+Runs bench.codec_rate's codec() (tpz_decompressed_sizes_claimed + prefix sum + tpz_decompress_blocks)
 --steps times after a settle, and prints the event-timed ms per step.
 """
 from __future__ import annotations
@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--codec", default="snappy", choices=["snappy", "lz4"])
     ap.add_argument("--blocks", type=int, default=1 << 18)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--exact", dest="claimed", action="store_false",
+                    help="exact sizes (the LZ4 walk) instead of the bench's claimed ones")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     nb = a.blocks
@@ -43,7 +45,8 @@ def main():
 
     def codec():
         ctx.decompressed_sizes_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb,
-                                    batch.src_bytes, size.data_ptr(), stream.cuda_stream)
+                                    batch.src_bytes, size.data_ptr(), stream.cuda_stream,
+                                    claimed=a.claimed)
         torch.cumsum(size, 0, out=out.ext[1:nb + 1])
         ctx.decompress_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), nb, batch.src_bytes,
                             out.src.data_ptr(), out.ext.data_ptr(), st.data_ptr(), stream.cuda_stream)
@@ -54,6 +57,7 @@ def main():
         codec()
     e1.record(stream)
     torch.cuda.synchronize()
+    assert ctx.decompress_check(stream.cuda_stream)
     assert int((st[:nb] != 0).sum()) == 0
     print(json.dumps({"codec": a.codec, "ms": round(e0.elapsed_time(e1) / a.steps, 4)}), flush=True)
     ctx.close()

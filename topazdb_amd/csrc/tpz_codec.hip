@@ -792,6 +792,10 @@ __global__ __launch_bounds__(kWave * kSmallWaves) void codec_wave_kernel(CodecPa
   for (u32 g = blockIdx.x * kSmallWaves + wid; g < p.n_blocks; g += kWave * S) {
     const u32 bj = g + lane * S;
     const u32 bc = bj < p.n_blocks ? bj : p.n_blocks - 1;
+    // after the lane kernels almost every block is final: one status load per 64 blocks, and
+    // the metadata loads only where a block was left (the three dependent loads per group cost
+    // 14 us over 2^18 blocks with nothing left)
+    if (p.group_pass && !__ballot(p.status[bc] == kLeftForWaveKernel)) continue;
     BlockMeta mj;
     mj.s = p.ext[bc];
     mj.e = p.ext[bc + 1];
@@ -1160,7 +1164,9 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
   // Every position is a 32-bit offset: live blocks need src_bytes and dst_bytes below 2^31.
   bool live = false;
   u32 s = 0, n = 0, ip = 0, want = 0, D0 = 0, dn = 0;
-  if (b < p.n_blocks) {
+  // (LZ4: the snappy pass marked every block it did not decode; the status first, so that a
+  // batch without LZ4 blocks costs this pass one load per lane)
+  if (b < p.n_blocks && (kCodec != 3 || p.status[b] == kLeftForWaveKernel)) {
 #ifdef TPZ_CODEC_ONCHIP
     const u32 bx = b & 4095u;   // timing build: the same 4096 blocks again and again (on chip)
 #else
@@ -1171,8 +1177,6 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     const u32 tag = len ? p.src[e64 - 1] : 0u;
     live = len > 1 && tag == (u32)kCodec && dn64 >= 2 && p.src_bytes >= 16 && dst_bytes >= 16 &&
            dst_bytes < 0x7FFFFFF0ull && p.src_bytes < 0x7FFFFFF0ull;
-    if constexpr (kCodec == 3)   // the snappy pass left it (every non-snappy block is 0xFF)
-      live = live && p.status[b] == kLeftForWaveKernel;
     if (live) {
       u64 want64 = 0;
       u32 h = 0;
