@@ -368,3 +368,30 @@ def test_long_blocks_crc_window_edges(ctx):
     ext = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
     g, o = assert_parity(ctx, src, ext)
     assert (o.status == O.OK).sum() == 3 * 5 * 6
+
+
+@pytest.mark.parametrize("n_rows", [1030, 1100, 1250, 1290, 1536, 2085])
+def test_batch_end_rows(ctx, n_rows):
+    """Batches that end a few rows past the first four rows of every workgroup (256 workgroups x
+    4 rows claimed at start): the rows claimed next, at the same moment in every workgroup, reach
+    the counter in any order, so a workgroup's later slot can hold a row inside the batch while
+    an earlier one holds a row past it. Every block must be decoded (one run lost a chunk of 2
+    blocks of 20,000 when a wave ended at the first row past the batch). Three runs per size."""
+    nb = 16 * n_rows - 5
+    src, ext = synth.make_region("4k", nb)
+    b = DeviceBatch(np.ascontiguousarray(src[:int(ext[nb])]), ext[:nb + 1])
+    from topazdb_amd.batch import SlottedColumns
+    cols = SlottedColumns(nb, b.src_bytes, 0)
+    n_ent = None
+    for _ in range(3):
+        cols.status.fill_(0xEE)                  # (a block the decode skips keeps these)
+        cols.count.fill_(-1)
+        decode_batch(ctx, b, cols)
+        cols.complete()
+        st = cols.status[:nb].cpu().numpy()
+        cnt = cols.count[:nb].cpu().numpy()
+        assert (st == _lib.BLOCK_OK).all(), np.nonzero(st != _lib.BLOCK_OK)[0][:8]
+        if n_ent is None:
+            n_ent = cnt.copy()
+            assert (n_ent > 0).all()
+        np.testing.assert_array_equal(cnt, n_ent)

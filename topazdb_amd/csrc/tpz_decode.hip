@@ -53,7 +53,8 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
 constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
 // wave path: a workgroup's rows are claimed kRowAhead row slots ahead, into a ring of kRowRing
-constexpr u32 kRowAhead = 4, kRowRing = 8;
+constexpr u32 kRowAhead = 4, kRowRing = 16;
+constexpr u32 kRowExit = 0xFFFFFFFFu;   // a slot that gets no row: the workgroup's rows are done
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
 
@@ -1509,7 +1510,9 @@ __device__ __forceinline__ T const_load(const T* base, u64 i) {
 // stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
 constexpr u32 kOnchipMask = 4095;
 #endif
-template <bool FLAT>
+// CS: log2 of the blocks a wave claims at a time (launch_decode's choice, a compile-time constant
+// so that the claim's shifts and masks take no registers)
+template <bool FLAT, u32 CS>
 __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
@@ -1518,9 +1521,14 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
   // row_slot[s % kRowRing] == s (see claim_chunk)
   __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
-  if (threadIdx.x < kRowAhead && p.chunk_shift < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
-    row_val[threadIdx.x] = atomicAdd(p.row_ctr, 1u);
+  // set once a row past the batch has been claimed: every later claim would be past it too
+  __shared__ u32 claims_done;
+  if (threadIdx.x == 0) claims_done = 0;   // (before the claims below: the same wave)
+  if (threadIdx.x < kRowAhead && CS < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
+    const u32 r0 = atomicAdd(p.row_ctr, 1u);
+    row_val[threadIdx.x] = r0;
     row_slot[threadIdx.x] = threadIdx.x;
+    if ((u64)r0 * kWavesPerWG >= p.n_blocks) claims_done = 1;
   } else if (threadIdx.x < kRowRing) {
     row_slot[threadIdx.x] = ~0u;
   }
@@ -1563,7 +1571,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
 #ifdef TPZ_WAVE_CHUNK
   const u32 cshift = __builtin_ctz((u32)TPZ_WAVE_CHUNK);
 #else
-  const u32 cshift = uni(p.chunk_shift);
+  const u32 cshift = CS;
 #endif
   const u32 kChunk = 1u << cshift, rshift = kRowShift - cshift;   // chunks per row: 2^rshift
   // claim_chunk returns the chunk's first block (saturated at n_blocks: a chunk past the batch
@@ -1577,6 +1585,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (pend_slot != ~0u) {
       if (lane == 0) {
         row_val[pend_slot % kRowRing] = pend_row;
+        if ((u64)pend_row * kWavesPerWG >= p.n_blocks) claims_done = 1;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __hip_atomic_store(&row_slot[pend_slot % kRowRing], pend_slot, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1588,37 +1597,54 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // blocks, a window of claimed rows buys nothing, and a row per claim would be a global atomic
   // per 16 blocks waited for by the next 16 waves; their rows stay static, r * grid + blockIdx.x.)
   const bool dyn_rows = rshift != 0;
+  // The rows of a workgroup's slots need not increase with the slots (two waves' claims can
+  // reach the counter in either order), so a chunk whose row lies past the batch is passed over,
+  // not taken for the end: the workgroup stops claiming rows once it has seen one past the batch
+  // (any later claim would be past it too) and marks the slots it no longer claims kRowExit; a
+  // wave ends at a kRowExit slot, and every later slot is one as well. (Ending at the first row
+  // past the batch lost a chunk when a later slot held a smaller row: 2 blocks of 20,000 once.)
   auto claim_chunk = [&]() -> u32 {
-    publish();
-    u32 q = 0;
-    if (lane == 0) q = atomicAdd(&chunk_next, 1u);
-    q = uni(q);
-    if (!dyn_rows) {
-      const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
-      return f < p.n_blocks ? (u32)f : p.n_blocks;
-    }
-    const u32 slot_q = q >> rshift;
-    if ((q & ((1u << rshift) - 1u)) == 0) {
-      pend_slot = slot_q + kRowAhead;
-      if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
-    }
-    u32 row = 0;
-    if (lane == 0) {
-      u32 spins = 0;
-      while (__hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP) != slot_q) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins == (1u << 22)) {   // never expected: report it, and end this wave's work
-          atomicOr(p.err, 2u);
-          break;
+    for (;;) {
+      publish();
+      u32 q = 0;
+      if (lane == 0) q = atomicAdd(&chunk_next, 1u);
+      q = uni(q);
+      if (!dyn_rows) {
+        const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
+        return f < p.n_blocks ? (u32)f : p.n_blocks;
+      }
+      const u32 slot_q = q >> rshift;
+      if ((q & ((1u << rshift) - 1u)) == 0) {
+        if (!uni(__hip_atomic_load(&claims_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+          pend_slot = slot_q + kRowAhead;
+          if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
+        } else if (lane == 0) {
+          const u32 sx = slot_q + kRowAhead;
+          row_val[sx % kRowRing] = kRowExit;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&row_slot[sx % kRowRing], sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      row = spins == (1u << 22) ? 0xFFFFFFFFu : row_val[slot_q % kRowRing];
+      u32 row = 0;
+      if (lane == 0) {
+        u32 spins = 0;
+        while (__hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP) != slot_q) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins == (1u << 22)) {   // never expected: report it, and end this wave's work
+            atomicOr(p.err, 2u);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        row = spins == (1u << 22) ? kRowExit : row_val[slot_q % kRowRing];
+      }
+      row = uni(row);
+      if (row == kRowExit) return p.n_blocks;
+      const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
+      if (f < p.n_blocks) return (u32)f;
+      // (a row past the batch, or a chunk past the last row's blocks: the next chunk)
     }
-    row = uni(row);
-    const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
-    return f < p.n_blocks ? (u32)f : p.n_blocks;
   };
   auto chunk_first = [](u32 f) -> u32 { return f; };
   // Lane l <= kChunk holds ext[first + l]: block j of the chunk spans lanes j and j + 1 (one
@@ -2214,15 +2240,23 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // 2.20 with 4, 2.78 with 1).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
   p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 1u;
+  // (the kernel takes it as a template argument, CS)
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
   u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
   u32 grid = a.num_cus;
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
-  if (a.keys)
-    hipLaunchKernelGGL(decode_wave_kernel<true>, dim3(grid), dim3(kWGThreads), 0, stream, p);
-  else
-    hipLaunchKernelGGL(decode_wave_kernel<false>, dim3(grid), dim3(kWGThreads), 0, stream, p);
+  if (a.keys) {
+    if (p.chunk_shift == 1u)
+      hipLaunchKernelGGL((decode_wave_kernel<true, 1u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+    else
+      hipLaunchKernelGGL((decode_wave_kernel<true, kRowShift>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+  } else {
+    if (p.chunk_shift == 1u)
+      hipLaunchKernelGGL((decode_wave_kernel<false, 1u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+    else
+      hipLaunchKernelGGL((decode_wave_kernel<false, kRowShift>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+  }
   if (a.bw_list)
     launch_bigwave(BigWaveLaunch{a.src, a.ext, a.src_bytes, a.rep, a.crc_tables, a.bw_list, a.data, a.ends,
                                  a.count, a.status, a.crc, a.spill_list, a.spill_count, a.defer_list,
