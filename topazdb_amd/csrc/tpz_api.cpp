@@ -486,7 +486,6 @@ tpz_err tpz_decompress_blocks(tpz_ctx* c, const tpz_batch* b, uint8_t* d_dst,
     if (r != TPZ_SUCCESS) return r;
   }
   hipStream_t s = (hipStream_t)stream;
-  TPZ_HIP(hipMemsetAsync(w->d_defer, 0, 4, s));
   tpz::CodecLaunch a{};
   a.src = b->d_src;
   a.ext = b->d_ext;

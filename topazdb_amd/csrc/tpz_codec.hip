@@ -1492,7 +1492,12 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
 #endif
 }
 
-__global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) { ring_body<2>(p); }
+// (the first kernel of the step zeroes the deferred-block counter the wave kernel appends to and
+// the big kernel reads: a memset of 4 bytes was a 4 us fill kernel of its own)
+__global__ __launch_bounds__(kRingWG) void snappy_ring_kernel(CodecParams p) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *p.defer_count = 0;
+  ring_body<2>(p);
+}
 __global__ __launch_bounds__(kRingWG) void lz4_ring_kernel(CodecParams p) { ring_body<3>(p); }
 
 __global__ __launch_bounds__(kWave) void codec_big_kernel(CodecParams p) {
