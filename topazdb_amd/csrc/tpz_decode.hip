@@ -53,7 +53,12 @@ constexpr int kWGThreads = kWave * kWavesPerWG;
 static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
 constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
 // wave path: a workgroup's rows are claimed kRowAhead row slots ahead, into a ring of kRowRing
-constexpr u32 kRowAhead = 4, kRowRing = 16;
+// (2^20 4k blocks: 2 slots 1.902 ms, 3 1.853-1.866, 4 1.859-1.878, 6 1.887; zipf 2.028 / 1.983-1.997
+// / 1.985-1.996 / 2.001: profiles/r5/row_ahead/)
+#ifndef TPZ_ROW_AHEAD
+#define TPZ_ROW_AHEAD 3
+#endif
+constexpr u32 kRowAhead = TPZ_ROW_AHEAD, kRowRing = 16;
 constexpr u32 kRowExit = 0xFFFFFFFFu;   // a slot that gets no row: the workgroup's rows are done
 constexpr int kTableBytes = kNumCrcTables * 256 * 4;  // 41 KiB
 constexpr int kGuard = 96;  // zeroed: the CRC's front lane reads up to 79+15 B before the payload
