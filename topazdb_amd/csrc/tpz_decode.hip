@@ -2237,14 +2237,18 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // Blocks claimed at a time by a wave of the wave path. Claims of single blocks balanced the
   // waves of a CU best with static rows (the first waves issue first; same box, 4k: 1.875 ms with
   // 1, 1.89 with 2 or 4, 1.95 with 16, 2.10 with a fixed split; zipf 2.04 against 2.28;
-  // profiles/r3/wave_chunks.jsonl); with rows claimed from the global counter, pairs are better
-  // (4k 1.872-1.877 against 1.881-1.890 ms, zipf 1.986 against 2.010, each in both orders; 4
-  // blocks 1.920 / 2.045: profiles/r5/chunk_ab.jsonl). A batch of long blocks (the 64k config,
+  // profiles/r3/wave_chunks.jsonl); with rows claimed from the global counter 4 slots ahead and
+  // the chunk shift a runtime value, pairs were better (4k 1.872-1.877 against 1.881-1.890 ms,
+  // zipf 1.986 against 2.010; 4 blocks 1.920 / 2.045: profiles/r5/chunk_ab.jsonl); see below for
+  // the shipped choice. A batch of long blocks (the 64k config,
   // where the wave path only routes blocks to the bigwave kernel) takes whole rows: its
   // per-chunk extent and header round trips are not hidden by any decode (64k: 2.07 ms with 16,
   // 2.20 with 4, 2.78 with 1).
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
-  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 1u;
+  // Rows claimed 3 slots ahead and the chunk shift a compile-time constant: single blocks per
+  // claim beat pairs in the slotted decode (4k 1.821 vs 1.827 ms and 1.824 vs 1.856 on two boxes,
+  // zipf equal), pairs stay better in the flat one (zipf 2.483 vs 2.506): profiles/r5/chunk_cs/.
+  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : (a.keys ? 1u : 0u);
   // (the kernel takes it as a template argument, CS)
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
@@ -2257,8 +2261,8 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
     else
       hipLaunchKernelGGL((decode_wave_kernel<true, kRowShift>), dim3(grid), dim3(kWGThreads), 0, stream, p);
   } else {
-    if (p.chunk_shift == 1u)
-      hipLaunchKernelGGL((decode_wave_kernel<false, 1u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+    if (p.chunk_shift == 0u)
+      hipLaunchKernelGGL((decode_wave_kernel<false, 0u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
     else
       hipLaunchKernelGGL((decode_wave_kernel<false, kRowShift>), dim3(grid), dim3(kWGThreads), 0, stream, p);
   }
