@@ -207,3 +207,32 @@ def test_claimed_sizes(ctx):
     # the check reads and clears the word: a later clean batch passes
     st, ok = decompress_with_sizes(ctx, good[:30], True)
     assert ok
+
+
+def test_claimed_acceptance(ctx):
+    """Claimed sizes with each stream prefixed by its own decoded length:
+    no acceptance walk runs, so the ring kernel applies liblz4's end-of-buffer rules itself.
+    Streams that end in a match, put a match into the last 5 output bytes or a literal run into
+    the last 12 before another sequence decode by the format but are an Err for
+    lz4::block::decompress (compress.rs:108-111): the claimed pass alone must give the oracle's
+    status for every block (CODEC_ERROR there, OK with the oracle's bytes elsewhere), and the
+    whole step (claimed, then the exact redo) the oracle's bytes. tests/lz4_streams.py builds the
+    cases; test_lz4_oracle.py::test_claimed_length_streams pins them against liblz4."""
+    import lz4_streams as Z
+    cases = Z.claimed_blocks(decode=O.lz4_decompress_safe)
+    blocks = [b for _n, b in cases]
+    want = [oracle_codec(b) for b in blocks]
+    n_err = sum(w[0] != O.OK for w in want)
+    assert n_err > 500 and len(blocks) - n_err > 500
+    st, ok = decompress_with_sizes(ctx, blocks, True)
+    for (name, b), w, s in zip(cases, want, st):
+        assert s == w[0], (name, b.hex(), s, w[0])
+    assert not ok                                          # the Err streams were claimed
+    good = [b for b, w in zip(blocks, want) if w[0] == O.OK]
+    st, ok = decompress_with_sizes(ctx, good, True)
+    assert ok and (st == _lib.BLOCK_OK).all()              # no redo for accepted streams
+    outs, st = device_codec(ctx, blocks)
+    for (name, b), w, o, s in zip(cases, want, outs, st):
+        assert s == w[0], (name, s, w[0])
+        if w[0] == O.OK:
+            assert o == w[1], name

@@ -145,6 +145,143 @@ def test_crafted_sequences():
 
 
 @needs_lib
+def test_claimed_length_streams():
+    """The claimed-size cases (tests/lz4_streams.py; the device test is
+    test_gpu_lz4.py::test_claimed_acceptance): every stream prefixed with its own format-decoded
+    length. liblz4 rejects a good share of them under that output limit (a stream ending in a
+    match, a match into the last 5 bytes, a literal run into the last 12 bytes that is not the
+    last sequence) and accepts the rest, with the format's bytes; the restatement agrees on each."""
+    import lz4_streams as Z
+    for name, s, n, ok in Z.crafted():
+        got = lib_decompress(s, n)
+        assert (got is not None) == ok, name
+        if ok:
+            assert len(got) == n, name
+        check(s, n)
+    rng = np.random.default_rng(31)
+    n_rej = n_ok = 0
+    for s, n in Z.format_streams(rng, 4000):
+        got = lib_decompress(s, n)
+        check(s, n)
+        if got is None:
+            n_rej += 1
+        else:
+            assert len(got) == n
+            n_ok += 1
+    assert n_rej > 500 and n_ok > 500, (n_rej, n_ok)
+    for s, n in Z.refixed(rng, 3000, lib_decompress):
+        check(s, n)
+
+
+def ring_rules(s: bytes, oend: int, want: int):
+    """A model of lz4_ring_kernel's acceptance (tpz_codec.hip, ring_body<3>): the format decode of
+    stream s plus liblz4's rules per sequence, applied as the ring applies them. Returns the
+    decoded bytes where the ring marks the block OK, None where it hands the block to the lane
+    kernel (which runs lz4_walk). Reads past the stream make the ring fail too (next > n)."""
+    I, O = len(s), oend
+    ip = d = 0
+    lzm = 0 if O >= 64 else 1
+    need_off = False
+    out = bytearray()
+    while True:
+        if ip >= I:
+            return bytes(out) if d == want and need_off else None
+        rej, o, is_lit, ln = False, 0, False, 0
+        if not need_off:
+            t = s[ip]
+            lit, mln, o = t >> 4, t & 15, 1
+            if lit == 15:
+                while True:
+                    if ip + o >= I:
+                        return None
+                    x = s[ip + o]
+                    lit += x
+                    o += 1
+                    if x != 255:
+                        break
+            ipt, ipL, L, op = ip, ip + o, lit, d
+            l15, sl = (t >> 4) == 15, False
+            if not lzm & 1:
+                if l15:
+                    rej = ipt + 1 >= I - 15
+                    sl = op + L > O - 32 or ipL + L > I - 32
+                else:
+                    sl = ipt + 1 > I - 17
+            elif not l15 and ipt + 1 < I - 16 and op <= O - 32:
+                lzm |= 2
+            else:
+                rej = l15 and ipt + 1 >= I - 15
+                sl = True
+            if sl:
+                lzm |= 1
+                if op + L > O - 12 or ipL + L > I - 8:
+                    rej = rej or ipL + L != I or op + L > O
+            if lit:
+                is_lit, ln = True, lit
+        off = 0
+        if not is_lit:
+            if ip + o + 2 > I:
+                return None
+            off = s[ip + o] | s[ip + o + 1] << 8
+            o += 2
+            ml = mln
+            if ml == 15:
+                while True:
+                    if ip + o >= I:
+                        return None
+                    x = s[ip + o]
+                    ml += x
+                    o += 1
+                    if x != 255:
+                        break
+            ln = ml + 4
+            ipM, M, op = ip + o, ln, d
+            late = mln == 15 and ipM >= I - 4
+            if not lzm & 1:
+                rej = rej or late
+                if op + M >= O - 64:
+                    lzm |= 1
+                    rej = rej or op + M > O - 5
+            elif not ((lzm & 2) and mln != 15 and off >= 8):
+                rej = rej or late or op + M > O - 5
+            lzm &= 1
+        nxt = ip + o + (ln if is_lit else 0)
+        if rej or d + ln > want or nxt > I or (not is_lit and (off == 0 or off > d)):
+            return None
+        if is_lit:
+            out += s[ip + o:nxt]
+        else:
+            for _ in range(ln):
+                out.append(out[-off])
+        need_off = is_lit
+        d += ln
+        ip = nxt
+
+
+@needs_lib
+def test_ring_rules_model():
+    """The ring kernel's acceptance rules (modelled by ring_rules) never accept a stream liblz4
+    rejects and give liblz4's bytes where they accept, under claimed limits (the prefix is the
+    output limit and the expected length) and exact ones (the limit larger than the length);
+    the streams they hand to the lane kernel are few among the accepted ones."""
+    import lz4_streams as Z
+    rng = np.random.default_rng(32)
+    cases = [(s, n) for _name, s, n, _ok in Z.crafted()] + Z.format_streams(rng, 4000)
+    cases += Z.refixed(rng, 3000, lib_decompress)
+    handed = accepted = 0
+    for s, n in cases:
+        for limit in (n, n + 7, n + 64):
+            want = lib_decompress(s, limit)
+            got = ring_rules(s, limit, n if want is None else len(want))
+            if got is not None:
+                assert got == want, (s.hex(), limit)
+            if want is not None:
+                accepted += 1
+                handed += got is None
+    assert accepted > 3000 and handed < accepted // 10, (handed, accepted)
+
+
+@needs_lib
 def test_kat_fixture_against_liblz4():
     kat = json.load(open(os.path.join(GOLDEN, "lz4_kat.json")))
     for k in kat:

@@ -34,6 +34,7 @@ def load(name: str):
     L = C.CDLL(path)
     L.tpz_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     L.tpz_decompressed_sizes.argtypes = [C.c_void_p, C.POINTER(_lib.Batch), C.c_void_p, C.c_void_p]
+    L.tpz_decompressed_sizes_claimed.argtypes = L.tpz_decompressed_sizes.argtypes
     L.tpz_decompress_blocks.argtypes = [C.c_void_p, C.POINTER(_lib.Batch), C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_void_p]
     h = C.c_void_p()
@@ -48,6 +49,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 18)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--claimed", action="store_true",
+                    help="tpz_decompressed_sizes_claimed (LZ4 blocks take their size prefix)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     nb = a.blocks
@@ -66,8 +69,8 @@ def main():
 
     def sizes(v):
         L, h = libs[v]
-        assert L.tpz_decompressed_sizes(h, C.byref(b), C.c_void_p(size.data_ptr()),
-                                        C.c_void_p(stream.cuda_stream)) == 0
+        fn = L.tpz_decompressed_sizes_claimed if a.claimed else L.tpz_decompressed_sizes
+        assert fn(h, C.byref(b), C.c_void_p(size.data_ptr()), C.c_void_p(stream.cuda_stream)) == 0
 
     def step(v):
         L, h = libs[v]
@@ -104,7 +107,8 @@ def main():
     for v in a.variants:
         t0, t1 = sorted(times[v][0]), sorted(times[v][1])
         print(json.dumps({"variant": v, "codec": a.codec, "sizes_ms": round(t0[len(t0) // 2], 4),
-                          "step_ms": round(t1[len(t1) // 2], 4), "sizes_equal_first": same[v]}),
+                          "step_ms": round(t1[len(t1) // 2], 4), "sizes_equal_first": same[v],
+                          "claimed": a.claimed}),
               flush=True)
 
 

@@ -1164,6 +1164,10 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
   // Every position is a 32-bit offset: live blocks need src_bytes and dst_bytes below 2^31.
   bool live = false;
   u32 s = 0, n = 0, ip = 0, want = 0, D0 = 0, dn = 0;
+  // LZ4: liblz4's output limit (the size prefix) and where its walk stands: bit 0 = the safe
+  // loop (entered for good once a sequence leaves the fast loop, or from the start when the
+  // limit is below 64), bit 1 = the current sequence took the safe loop's two-stage shortcut
+  u32 oend = 0, lzm = 0;
   // (LZ4: the snappy pass marked every block it did not decode; the status first, so that a
   // batch without LZ4 blocks costs this pass one load per lane)
   if (b < p.n_blocks && (kCodec != 3 || p.status[b] == kLeftForWaveKernel)) {
@@ -1184,13 +1188,18 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
         h = snappy_header(p.src + s64, len - 1, want64);
         live = h != 0 && want64 + 1 == dn64;
       } else {
-        // u32 LE size prefix, then the block stream (compress.rs:108-111); the sizes pass ran
-        // liblz4's acceptance walk: dn - 1 is the exact decoded length of an accepted stream
-        // (dn = 1 for an Err). A stream this pass finds anything unusual in is left to the
-        // lane kernel, which decodes it with liblz4's own control flow.
+        // u32 LE size prefix, then the block stream (compress.rs:108-111). dn - 1 is either the
+        // exact decoded length (tpz_decompressed_sizes ran liblz4's walk) or the size prefix
+        // itself (tpz_decompressed_sizes_claimed: no walk ran). So this pass applies liblz4's
+        // acceptance rules itself, sequence by sequence, with the walk's own output limit (the
+        // prefix: lz4_walk's oend); a block whose stream breaks one, or that this pass finds
+        // anything unusual in, is left to the lane kernel, which runs lz4_walk.
         want64 = dn64 - 1;
         h = 4;
-        live = lz4_prefix(p.src + s64, len - 1) >= 0 && len - 1 > 4;
+        const int64_t pre = lz4_prefix(p.src + s64, len - 1);
+        live = pre >= 0 && len - 1 > 4 && pre < 0x7FFFFFF0;
+        oend = live ? (u32)pre : 0u;
+        lzm = oend >= 64 ? 0u : 1u;
       }
       s = (u32)s64;
       ip = h;
@@ -1247,6 +1256,10 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
         auto hb = [&](u32 i) -> u32 { return (u32)(hv >> (8 * i)) & 0xFFu; };
         u32 o = 0, len = 0, off = 0;
         bool bad = false, is_lit = false;
+        // liblz4 1.9.3's acceptance (lz4_walk, oracle/tpz_lz4.c:53-173), in positions relative to
+        // the block (the stream's iend is n, its oend the prefix): rej = the walk returns Err
+        const int I = (int)n, O = (int)oend, op = (int)d;
+        bool rej = false;
         if (!need_off) {
           const u32 t = hb(0);
           u32 lit = t >> 4;
@@ -1260,6 +1273,29 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
               lit += x;
               o++;
             } while (x == 255 && !bad);
+          }
+          // the literal part. (Where the walk stops reading a length early, 15 bytes before the
+          // input end, its literal ends at the input end and this parse's runs past it: next > n.)
+          const int ipt = (int)ip, ipL = ipt + (int)o, L = (int)lit;
+          const bool l15 = (t >> 4) == 15;
+          bool sl = false;                    // goes to safe_literal_copy
+          if (!(lzm & 1u)) {                  // the fast loop
+            if (l15) {
+              rej = ipt + 1 >= I - 15;
+              sl = op + L > O - 32 || ipL + L > I - 32;
+            } else {
+              sl = ipt + 1 > I - 17;
+            }
+          } else if (!l15 && ipt + 1 < I - 16 && op <= O - 32) {
+            lzm |= 2u;                        // the two-stage shortcut: no end checks here
+          } else {
+            rej = l15 && ipt + 1 >= I - 15;
+            sl = true;
+          }
+          if (sl) {
+            lzm |= 1u;
+            // near either end the sequence must be the last: it consumes the input exactly
+            if (op + L > O - 12 || ipL + L > I - 8) rej = rej || ipL + L != I || op + L > O;
           }
           if (lit) {
             is_lit = true;
@@ -1281,9 +1317,25 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
             } while (x == 255 && !bad);
           }
           len = ml + 4;
+          // the match part: a length continuation must end 5 bytes before the input end, and a
+          // match checked against the output end (the fast loop checks it from 64 bytes before,
+          // the shortcut not at all) must leave the last 5 bytes to literals
+          const int ipM = (int)ip + (int)o, M = (int)len;
+          const bool m15 = mln == 15, late = m15 && ipM >= I - 4;
+          if (!(lzm & 1u)) {
+            rej = rej || late;
+            if (op + M >= O - 64) {
+              lzm |= 1u;
+              rej = rej || op + M > O - 5;
+            }
+          } else if (!((lzm & 2u) && !m15 && off >= 8)) {
+            rej = rej || late || op + M > O - 5;
+          }
+          lzm &= 1u;
         }
         const u32 next = ip + o + (is_lit ? len : 0u);
-        if (bad || d + len > want || next > n || next < ip || (!is_lit && (off == 0 || off > d))) {
+        if (bad || rej || d + len > want || next > n || next < ip ||
+            (!is_lit && (off == 0 || off > d))) {
           fail = true;
         } else {
           ek = is_lit ? 0u : 1u;
@@ -1433,7 +1485,9 @@ __device__ __forceinline__ void ring_body(CodecParams p) {
     }
     if (finish) {
       live = false;
-      if (d == want) {
+      // (LZ4: liblz4's walk ends only after a sequence's literals; after a match it reads a
+      // token past the input and fails)
+      if (d == want && (kCodec != 3 || need_off)) {
         // re-tagged Uncompress: the tag byte joins the frontier slot
         const u32 T = D0 + want;
         const u32 m = T & 15;
