@@ -385,8 +385,12 @@ tpz_err tpz_decode_check(tpz_ctx* c, void* stream) {
   TPZ_HIP(hipMemsetAsync(tail + tpz::kTailError, 0, 4, s));
   TPZ_HIP(hipStreamSynchronize(s));
   if (!flag) return TPZ_SUCCESS;
-  g_last_error = "tpz_decode_blocks: a tail workgroup's wait for the big path timed out; spill "
-                 "blocks of a batch on this stream may be undecoded";
+  // bit 0: a tail workgroup's bounded wait; bit 1: a wave path row wait; bit 2: a wave path row
+  // slot overwritten before its reader got to it (tpz_decode.hip claim_chunk)
+  g_last_error = (flag & 1u) ? "tpz_decode_blocks: a tail workgroup's wait for the big path timed out; "
+                               "spill blocks of a batch on this stream may be undecoded"
+                             : "tpz_decode_blocks: a wave path row claim timed out or was overwritten; "
+                               "blocks of a batch on this stream may be undecoded";
   return TPZ_ERR_INTERNAL;
 }
 

@@ -1510,6 +1510,23 @@ __device__ __forceinline__ T const_load(const T* base, u64 i) {
 }
 
 // ------------------------------------------------------------------ wave path kernel
+#ifdef TPZ_ABL_ROWLATE
+// Diagnostic build (tests/test_gpu_row_claims.py): near the end of the batch (the global row
+// counter within two rows per workgroup of the last row) some claimers (the waves that take the
+// first chunk of a slot) sleep ~100 us between taking it and reading claims_done (point 0: odd
+// waves), others between that read and their claim from the row counter (point 1: waves 2 mod
+// 4), while the rest of the workgroup goes on (a block per wave takes ~7 us): a later slot's
+// claim reaches the counter first and takes an earlier row, and a claimer reads claims_done after
+// later claimers have claimed rows and a row past the batch has been published: the orders a
+// fast box produces only rarely.
+__device__ __noinline__ void rowlate_delay(const Params& p, u32 wid, u32 point) {
+  const u32 rows = (p.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
+  const u32 ctr = __hip_atomic_load(p.row_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool late = point == 0 ? (wid & 1u) != 0 : (wid & 3u) == 2;
+  if (late && ctr + 2 * gridDim.x >= rows)
+    for (int i = 0; i < 30; i++) __builtin_amdgcn_s_sleep(127);
+}
+#endif
 #ifdef TPZ_ABL_ONCHIP
 // diagnostic (timing only): every wave decodes blocks 0..4095 over and over, so loads and stores
 // stay on chip (L2 / Infinity Cache) and the launch time is the kernel's compute time
@@ -1526,14 +1543,21 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
   // row_slot[s % kRowRing] == s (see claim_chunk)
   __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
-  // set once a row past the batch has been claimed: every later claim would be past it too
-  __shared__ u32 claims_done;
-  if (threadIdx.x == 0) claims_done = 0;   // (before the claims below: the same wave)
+  // claims_done: set once a row past the batch has been published (every later claim from the
+  // counter would be past it too). exit_slot: no slot from it on holds a row (see claim_chunk).
+  __shared__ u32 claims_done, exit_slot;
+  if (threadIdx.x == 0) {                  // (before the claims below: the same wave)
+    claims_done = 0;
+    exit_slot = ~0u;
+  }
   if (threadIdx.x < kRowAhead && CS < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
     const u32 r0 = atomicAdd(p.row_ctr, 1u);
     row_val[threadIdx.x] = r0;
     row_slot[threadIdx.x] = threadIdx.x;
-    if ((u64)r0 * kWavesPerWG >= p.n_blocks) claims_done = 1;
+    if ((u64)r0 * kWavesPerWG >= p.n_blocks) {
+      claims_done = 1;
+      atomicMin(&exit_slot, kRowAhead);    // every claim after the barrier sees claims_done
+    }
   } else if (threadIdx.x < kRowRing) {
     row_slot[threadIdx.x] = ~0u;
   }
@@ -1586,11 +1610,20 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // wave reaches that slot (kRowAhead - 1 rows of claims later); a reader that gets there first
   // waits for it (bounded; a timeout sets the sticky error word, tpz_decode_check).
   u32 pend_slot = ~0u, pend_row = 0;   // (uniform / lane 0) a claimed row not yet published
+  const u32 kq = 1u << rshift;           // chunks per row slot
   auto publish = [&]() {
     if (pend_slot != ~0u) {
       if (lane == 0) {
         row_val[pend_slot % kRowRing] = pend_row;
-        if ((u64)pend_row * kWavesPerWG >= p.n_blocks) claims_done = 1;
+        if ((u64)pend_row * kWavesPerWG >= p.n_blocks) {
+          // claims_done first, then the chunk counter: a chunk q >= Q was taken after this read,
+          // so its claimer reads claims_done = 1 and claims no row. Rows are claimed only for the
+          // slots of chunks q < Q, the last being slot (Q - 1) / kq + kRowAhead.
+          __hip_atomic_store(&claims_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const u32 Q = __hip_atomic_fetch_add(&chunk_next, 0u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          atomicMin(&exit_slot, Q == 0 ? kRowAhead : (Q - 1) / kq + kRowAhead + 1);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __hip_atomic_store(&row_slot[pend_slot % kRowRing], pend_slot, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1603,11 +1636,15 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // per 16 blocks waited for by the next 16 waves; their rows stay static, r * grid + blockIdx.x.)
   const bool dyn_rows = rshift != 0;
   // The rows of a workgroup's slots need not increase with the slots (two waves' claims can
-  // reach the counter in either order), so a chunk whose row lies past the batch is passed over,
-  // not taken for the end: the workgroup stops claiming rows once it has seen one past the batch
-  // (any later claim would be past it too) and marks the slots it no longer claims kRowExit; a
-  // wave ends at a kRowExit slot, and every later slot is one as well. (Ending at the first row
-  // past the batch lost a chunk when a later slot held a smaller row: 2 blocks of 20,000 once.)
+  // reach the counter in either order, and a claimer can read claims_done late), so neither a
+  // row past the batch nor a slot left without a row (kRowExit) ends a wave: both are passed
+  // over. A wave ends at its first chunk in a slot >= exit_slot, which the publisher of a row past
+  // the batch sets from the chunk counter (publish above): every slot with a row lies below it,
+  // and every chunk below it has been taken, by the order of the chunk counter. So no claimed row
+  // is left behind whatever the timing (tests/test_row_claims.py models the protocol; the
+  // diagnostic build TPZ_ABL_ROWLATE delays claimers to force the orders; round 5 ended a wave
+  // at the first kRowExit slot, which lost the rows of later slots claimed by an earlier read of
+  // claims_done: 2 blocks of 20,000 once).
   auto claim_chunk = [&]() -> u32 {
     for (;;) {
       publish();
@@ -1619,9 +1656,17 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
         return f < p.n_blocks ? (u32)f : p.n_blocks;
       }
       const u32 slot_q = q >> rshift;
+      if (slot_q >= uni(__hip_atomic_load(&exit_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+        return p.n_blocks;
       if ((q & ((1u << rshift) - 1u)) == 0) {
+#ifdef TPZ_ABL_ROWLATE
+        rowlate_delay(p, wid, 0);
+#endif
         if (!uni(__hip_atomic_load(&claims_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
           pend_slot = slot_q + kRowAhead;
+#ifdef TPZ_ABL_ROWLATE
+          rowlate_delay(p, wid, 1);
+#endif
           if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
         } else if (lane == 0) {
           const u32 sx = slot_q + kRowAhead;
@@ -1632,22 +1677,30 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       }
       u32 row = 0;
       if (lane == 0) {
-        u32 spins = 0;
-        while (__hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP) != slot_q) {
+        u32 spins = 0, rs;
+        // (a slot's entry is overwritten kRowRing slots later; a reader that finds a later slot
+        // there, or waits past the bound, reports it through the sticky error word: the launch
+        // fails loudly at tpz_decode_check instead of passing blocks over)
+        while ((rs = __hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP)) != slot_q) {
+          if (rs != ~0u && (int)(rs - slot_q) > 0) {
+            atomicOr(p.err, 4u);
+            break;
+          }
           __builtin_amdgcn_s_sleep(2);
-          if (++spins == (1u << 22)) {   // never expected: report it, and end this wave's work
+          if (++spins == (1u << 22)) {
             atomicOr(p.err, 2u);
             break;
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        row = spins == (1u << 22) ? kRowExit : row_val[slot_q % kRowRing];
+        row = rs != slot_q ? kRowExit : row_val[slot_q % kRowRing];
       }
       row = uni(row);
-      if (row == kRowExit) return p.n_blocks;
-      const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
-      if (f < p.n_blocks) return (u32)f;
+      if (row != kRowExit) {
+        const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
+        if (f < p.n_blocks) return (u32)f;
+      }
       // (a row past the batch, or a chunk past the last row's blocks: the next chunk)
     }
   };
