@@ -50,7 +50,12 @@ extern "C" {
  *      the exact ends layout (tpz_columns.d_entry_first, tpz_table.d_entry_first)
  *   5  the flat layout: tpz_flat_layout + tpz_decode_blocks_flat (tpz_flat_columns); no
  *      existing struct or status changed
- *   6  claimed LZ4 sizes: tpz_decompressed_sizes_claimed, tpz_decompress_check, TPZ_ERR_SIZES
+ *   6  claimed LZ4 sizes: tpz_decompressed_sizes_claimed, tpz_decompress_check, TPZ_ERR_SIZES;
+ *      tpz_verify_blocks_host (the host pipeline's verdict without the column downloads, for
+ *      Block views of the caller's bytes). Round 6, same ABI: tpz_decode_blocks_host /
+ *      tpz_verify_blocks_host return TPZ_ERR_NOMEM only for a short caller buffer (an internal
+ *      chunk overflow is TPZ_ERR_INTERNAL), and tpz_decode_check also fails for a wave path row
+ *      claim that timed out or was overwritten
  * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
 #define TPZ_ABI_VERSION 6
 int tpz_abi_version(void);
@@ -375,7 +380,7 @@ tpz_err tpz_decode_blocks_flat(tpz_ctx* ctx, const tpz_batch* batch, const tpz_f
  *             blocks' records (the library's device arenas grow as needed)
  * Returns TPZ_ERR_NOMEM when ends_cap, spill_cap or data_cap is too small: h_first[n],
  * *h_spill_used and h_dext[n] then hold the sizes needed (the call can be repeated with larger
- * buffers). chunk_blocks = 0 picks the default (8,192 blocks per chunk: 34 MB of 4 KiB blocks,
+ * buffers; NOMEM has no other cause, so a repeat with buffers of those sizes succeeds). chunk_blocks = 0 picks the default (8,192 blocks per chunk: 34 MB of 4 KiB blocks,
  * the fastest of 4K..64K on MI355X, profiles/r2/e2e_sweep.jsonl). The streams and device buffers
  * of a call are kept by the context and reused by its next calls (one set per concurrent
  * caller). */

@@ -94,9 +94,13 @@ impl GpuDecoder {
                 ffi::TPZ_ERR_NOMEM => {
                     let pairs = out.first[n] as usize;
                     let data = unsafe { ffi::tpz_layout_data_capacity(out.dext[n], n as u64) } as usize;
+                    let before = (out.ends.len(), out.spill.len(), out.data.len());
                     out.ends.resize(out.ends.len().max(2 * pairs), 0);
                     out.spill.resize(out.spill.len().max(out.spill_used as usize), 0);
                     out.data.resize(out.data.len().max(data), 0);
+                    if before == (out.ends.len(), out.spill.len(), out.data.len()) {
+                        bail!("tpz_decode_blocks_host: NOMEM with every buffer at the size it asked for");
+                    }
                 }
                 e => check(e, "tpz_decode_blocks_host")?,
             }
@@ -140,7 +144,9 @@ impl GpuDecoder {
             };
             match rc {
                 ffi::TPZ_SUCCESS => break,
-                ffi::TPZ_ERR_NOMEM if codec => plain.resize(plain.len().max(dext[n] as usize), 0),
+                // NOMEM: h_plain was short and dext[n] holds the bytes needed (grow only then:
+                // anything else is an error, never a retry)
+                ffi::TPZ_ERR_NOMEM if codec && dext[n] as usize > plain.len() => plain.resize(dext[n] as usize, 0),
                 e => check(e, "tpz_verify_blocks_host")?,
             }
         }
@@ -203,11 +209,21 @@ impl SsTable {
                 }
                 ffi::TPZ_BLOCK_MALFORMED => panic!("block {} is malformed", first + i),
                 st => {
-                    // the reference's own Err for these bytes (an error path only: the message
-                    // carries the stored CRC, which sits inside the decompressed form of a
-                    // snappy / lz4 block); the device status and CRC agree with it
-                    let b = &region[ext[i] as usize..ext[i + 1] as usize];
-                    Err(Block::decode(b).err().unwrap_or_else(|| block_error(st, 0, v.crc[i])))
+                    // the reference's Err from the device's verdict alone (no CPU decode): a
+                    // checksum mismatch names the stored CRC, the big-endian u32 before the tag of
+                    // the block's Uncompress form (the run's own bytes, or the device's
+                    // decompressed bytes for snappy / lz4, checksum.rs:12-21), and the device's
+                    // actual CRC; the other statuses carry no numbers (compress.rs:96-102)
+                    let u: &[u8] = match &v.plain {
+                        Some((dext, plain)) => &plain[dext[i] as usize..dext[i + 1] as usize],
+                        None => &region[ext[i] as usize..ext[i + 1] as usize],
+                    };
+                    let expected = if st == ffi::TPZ_BLOCK_CHECKSUM_MISMATCH && u.len() >= 5 {
+                        u32::from_be_bytes([u[u.len() - 5], u[u.len() - 4], u[u.len() - 3], u[u.len() - 2]])
+                    } else {
+                        0
+                    };
+                    Err(block_error(st, expected, v.crc[i]))
                 }
             })
             .collect()

@@ -117,3 +117,60 @@ def test_crafted_and_fuzzed_bad_entries():
         n_bad += d.status[b] == O.BAD_ENTRY
         check_block(blk, d, b, probes + [k for k, _ in d.entries(b)][:4])
     assert n_bad >= 100
+
+
+def read_blocks_err_rust(status: int, plain: bytes | None, crc_actual: int) -> str:
+    """read_blocks_gpu's Err for a rejected block (rust/topazdb-gpu/src/table/gpu.rs), restated:
+    built from the device's verdict alone, no CPU decode. A checksum mismatch names the stored
+    CRC, the big-endian u32 before the tag of the block's Uncompress form (`plain`: the run's
+    own bytes for tag 1, the device's decompressed bytes for tags 2 / 3), and the device's actual
+    CRC; the other statuses carry no numbers (tpz_format_block_error)."""
+    from topazdb_amd import _lib
+    expected = 0
+    if status == _lib.BLOCK_CHECKSUM_MISMATCH and plain is not None and len(plain) >= 5:
+        expected = struct.unpack(">I", plain[-5:-1])[0]
+    return _lib.format_block_error(status, expected, crc_actual)
+
+
+def test_error_texts_without_cpu_decode():
+    """the Rust drop-in's Err for every rejected block equals the reference's
+    text (checksum.rs:17-20, compress.rs:97,102; the oracle's expected / actual CRCs), for
+    corrupted payloads, CRCs and tags in all three codecs, empty blocks and bad tags."""
+    f = read_golden("sst_4k_k16_v100.sst")
+    ext, _, _ = O.sst_parse(f)
+    src = f[:int(ext[-1])]
+    base = [bytes(src[int(ext[i]):int(ext[i + 1])]) for i in range(min(len(ext) - 1, 12))]
+    rng = np.random.default_rng(41)
+    blocks = []
+    for i, b in enumerate(base):
+        for codec in (1, 2, 3):
+            for kind in ("payload", "crc", "ok"):
+                u = bytearray(b)
+                if kind == "payload":
+                    u[int(rng.integers(0, len(u) - 5))] ^= 1 << int(rng.integers(0, 8))
+                elif kind == "crc":
+                    u[len(u) - 2] ^= 0x5A
+                u = bytes(u)
+                blocks.append(u if codec == 1 else O.snappy_block(u) if codec == 2 else O.lz4_block(u))
+    blocks += [b"", b"\x00", base[0][:-1] + b"\x07", base[0][:-1] + b"\x00"]
+    n_mis = 0
+    for blk in blocks:
+        st, plain = O.decompress_block(blk)
+        if st != O.OK:                                   # the codec step's own statuses
+            plain = None
+        d = O.decode_batch(np.frombuffer(plain if plain is not None else blk, np.uint8) if (plain or blk) else np.zeros(1, np.uint8),
+                           np.array([0, len(plain) if plain is not None else len(blk)], np.uint64))
+        status = int(d.status[0]) if st == O.OK else int(st)
+        if status in (O.OK, O.BAD_ENTRY):
+            continue
+        if status == O.CHECKSUM:
+            n_mis += 1
+            want = "checksum: expected %d, actual %d" % (int(d.crc_expected[0]), int(d.crc_actual[0]))
+        elif status == O.EMPTY:
+            want = "data is empty"
+        elif status == O.BAD_TAG:
+            want = "invaild data"
+        else:
+            continue
+        assert read_blocks_err_rust(status, plain, int(d.crc_actual[0])) == want, (status, blk[:8])
+    assert n_mis >= 40

@@ -329,6 +329,9 @@ class Context:
         blocks the decoded extents and bytes (every block's Uncompress form). Returns
         (status, crc, count, dext, plain); dext / plain are None for an Uncompress run."""
         import numpy as np
+        if not hasattr(lib(), "tpz_verify_blocks_host"):
+            raise RuntimeError(f"{LIB_PATH} has no tpz_verify_blocks_host (ABI 6, round 5 on): "
+                               "a library built from an earlier tree")
         src = np.ascontiguousarray(np.frombuffer(bytes(region), np.uint8) if not isinstance(region, np.ndarray) else region, np.uint8)
         e = np.ascontiguousarray(ext, np.uint64)
         n = len(e) - 1
@@ -349,8 +352,9 @@ class Context:
                 C.c_void_p(status.ctypes.data), C.c_void_p(crc.ctypes.data),
                 C.c_void_p(count.ctypes.data), C.c_void_p(plain.ctypes.data if codec else None),
                 plain.size if codec else 0, C.c_void_p(dext.ctypes.data), chunk_blocks)
-            if rc == ERR_NOMEM and codec:
-                plain = np.zeros(max(int(dext[n]), plain.size + 1), np.uint8)
+            # (NOMEM means h_plain was short: dext[n] holds the bytes needed; grow only then)
+            if rc == ERR_NOMEM and codec and int(dext[n]) > plain.size:
+                plain = np.zeros(int(dext[n]), np.uint8)
                 continue
             check(rc, "tpz_verify_blocks_host")
             break

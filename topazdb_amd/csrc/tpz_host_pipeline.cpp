@@ -527,9 +527,10 @@ static tpz_err host_pipeline(tpz_ctx* ctx, const uint8_t* h_src, const uint64_t*
     }
     // still short after the tries (each grows the buffers to 1.25x what the chunk reported, so
     // this takes a device that keeps reporting more): the chunk's emptied extents must not be
-    // copied out as if they were its blocks
+    // copied out as if they were its blocks. TPZ_ERR_INTERNAL, not NOMEM: no caller buffer is
+    // short, so a caller that grows its buffers on NOMEM and calls again would loop for ever.
     if ((codec && S.h_meta.as<ChunkMeta>()->overflow) || *S.h_used.as<uint64_t>() > S.d_spill.n) {
-      return tpz_internal_fail(TPZ_ERR_NOMEM,
+      return tpz_internal_fail(TPZ_ERR_INTERNAL,
                                "tpz_decode_blocks_host: chunk buffers still overflow after 4 decodes");
     }
     const uint64_t used = *S.h_used.as<uint64_t>();
