@@ -429,7 +429,13 @@ def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream
     tensor); decode the former with decode_batch and take the codec status for blocks whose codec
     step failed. claimed: LZ4 blocks sized by their size prefix (tpz_decompressed_sizes_claimed,
     no acceptance walk); when tpz_decompress_check finds a block whose stream decoded to another
-    length or failed, the batch is sized exactly and decompressed again."""
+    length or failed, the batch is sized exactly and decompressed again.
+
+    This function synchronizes with the host either way: it reads the decoded total to allocate
+    the output, and in claimed mode tpz_decompress_check waits for the step. It cannot be
+    captured in a graph. A caller that must stay asynchronous (or capture the step) calls
+    tpz_decompressed_sizes (exact sizes: no check needed), a device prefix sum and
+    tpz_decompress_blocks on its stream into an output it sized itself."""
     dev = _dev(ctx.device)
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     nb = batch.n_blocks
