@@ -999,27 +999,27 @@ __device__ __forceinline__ u32 copy_crc_fused(const u32* tab, const S& src, cons
 // (more than 4096 B of keys and values) copy it afterwards with copy_fast.
 typedef u32 u32x2v __attribute__((ext_vector_type(2)));
 typedef u32 u32x4v __attribute__((ext_vector_type(4)));
+// the five 4-byte-aligned LDS words holding bytes [x, x + 16): two ds_read2_b32 and a ds_read_b32
+// (issued, not waited for); no dword select afterwards (three 8-byte-aligned ds_read_b64 need a
+// five-way dword select: 2.0 % slower, profiles/r6/ng/)
 struct Gath {
-  u32x2v a, b, c;
+  u32 d0, d1, d2, d3, d4;
 };
-// the three 8-byte-aligned LDS words holding bytes [x, x + 16) (issued, not waited for)
 __device__ __forceinline__ Gath gath_issue(const uint8_t* base, int x) {
-  const u32x2v* p = reinterpret_cast<const u32x2v*>(base + (x & ~7));
+  const u32* p = reinterpret_cast<const u32*>(base + (x & ~3));
   Gath g;
-  g.a = p[0];
-  g.b = p[1];
-  g.c = p[2];
+  g.d0 = p[0];
+  g.d1 = p[1];
+  g.d2 = p[2];
+  g.d3 = p[3];
+  g.d4 = p[4];
   return g;
 }
-// bytes [x, x + 16) from the gathered words: a one-bit dword select + alignbyte (lds_window16)
 __device__ __forceinline__ uint4 gath_finish(Gath g, int x) {
-  asm volatile("" : "+v"(g.a), "+v"(g.b), "+v"(g.c));
+  asm volatile("" : "+v"(g.d0), "+v"(g.d1), "+v"(g.d2), "+v"(g.d3), "+v"(g.d4));
   const u32 s = (u32)x & 3u;
-  const bool h = ((u32)x & 4u) != 0;
-  const u32 s0 = h ? g.a.y : g.a.x, s1 = h ? g.b.x : g.a.y, s2 = h ? g.b.y : g.b.x,
-            s3 = h ? g.c.x : g.b.y, s4 = h ? g.c.y : g.c.x;
-  return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, s), __builtin_amdgcn_alignbyte(s2, s1, s),
-                    __builtin_amdgcn_alignbyte(s3, s2, s), __builtin_amdgcn_alignbyte(s4, s3, s));
+  return make_uint4(__builtin_amdgcn_alignbyte(g.d1, g.d0, s), __builtin_amdgcn_alignbyte(g.d2, g.d1, s),
+                    __builtin_amdgcn_alignbyte(g.d3, g.d2, s), __builtin_amdgcn_alignbyte(g.d4, g.d3, s));
 }
 // the 16 lookups of a slice-by-16 step over (w0 ^ c, w1, w2, w3), issued
 struct Look16 {
@@ -1122,9 +1122,9 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   auto finish = [&](PWin& P, u32 w) {
     const u32 c = 64 * w + lane;
     const u32 x0 = 16 * c;
-    // a window where a lane needs copy_window's rare path is left to it whole
-    const bool rw = __ballot(P.act && (P.e0 <= x0 || (P.cross && P.e1 < x0 + 16 && P.j + 2 < F.nk))) != 0;
-    if (rw) rare |= 1u << w;
+    // (no rare path: this copy runs only for blocks whose non-empty segments are 16 bytes or
+    // longer, so no two segments end in one chunk and no chunk meets three segments)
+    constexpr bool rw = false;
     uint4 acc = gath_finish(P.ga, P.act ? (int)x0 + P.d0 : -kGuard);
     const uint4 nx = gath_finish(P.gn, P.cross ? (int)x0 + P.d1 : -kGuard);
     if (P.cross) acc = merge_at(acc, nx, (int)(P.e0 - x0));
@@ -1540,9 +1540,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   u32* tab = reinterpret_cast<u32*>(lds);
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
   __shared__ Out out_lds;             // the worklist pointers for the rare paths (see above)
-  // The row (of 16 blocks) of row slot s of this workgroup: row_val[s % kRowRing], valid when
-  // row_slot[s % kRowRing] == s (see claim_chunk)
-  __shared__ u32 row_val[kRowRing], row_slot[kRowRing];
+  // The row (of 16 blocks) of row slot s of this workgroup: row_ent[s % kRowRing] = row | s << 32
+  // once published (one 64-bit LDS access writes and reads both halves; see claim_chunk)
+  __shared__ u64 row_ent[kRowRing];
   // claims_done: set once a row past the batch has been published (every later claim from the
   // counter would be past it too). exit_slot: no slot from it on holds a row (see claim_chunk).
   __shared__ u32 claims_done, exit_slot;
@@ -1552,14 +1552,13 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   }
   if (threadIdx.x < kRowAhead && CS < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
     const u32 r0 = atomicAdd(p.row_ctr, 1u);
-    row_val[threadIdx.x] = r0;
-    row_slot[threadIdx.x] = threadIdx.x;
+    row_ent[threadIdx.x] = (u64)r0 | (u64)threadIdx.x << 32;
     if ((u64)r0 * kWavesPerWG >= p.n_blocks) {
       claims_done = 1;
       atomicMin(&exit_slot, kRowAhead);    // every claim after the barrier sees claims_done
     }
   } else if (threadIdx.x < kRowRing) {
-    row_slot[threadIdx.x] = ~0u;
+    row_ent[threadIdx.x] = ~0ull;
   }
   if (threadIdx.x == 0) {             // (load_tables' barrier publishes both)
     chunk_next = 0;
@@ -1614,7 +1613,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   auto publish = [&]() {
     if (pend_slot != ~0u) {
       if (lane == 0) {
-        row_val[pend_slot % kRowRing] = pend_row;
+
         if ((u64)pend_row * kWavesPerWG >= p.n_blocks) {
           // claims_done first, then the chunk counter: a chunk q >= Q was taken after this read,
           // so its claimer reads claims_done = 1 and claims no row. Rows are claimed only for the
@@ -1624,9 +1623,8 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
           atomicMin(&exit_slot, Q == 0 ? kRowAhead : (Q - 1) / kq + kRowAhead + 1);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __hip_atomic_store(&row_slot[pend_slot % kRowRing], pend_slot, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&row_ent[pend_slot % kRowRing], (u64)pend_row | (u64)pend_slot << 32,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       pend_slot = ~0u;
     }
@@ -1645,12 +1643,17 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   // diagnostic build TPZ_ABL_ROWLATE delays claimers to force the orders; round 5 ended a wave
   // at the first kRowExit slot, which lost the rows of later slots claimed by an earlier read of
   // claims_done: 2 blocks of 20,000 once).
+  // The chunk counter is read one claim ahead (a ticket): a claim takes the ticket its previous
+  // claim fetched and fetches the next, so the atomic's round trip is off the claim's chain. A
+  // wave's held ticket when it ends is past its last chunk, hence past exit_slot too.
+  u32 q_tk = 0;
+  if (lane == 0) q_tk = atomicAdd(&chunk_next, 1u);
   auto claim_chunk = [&]() -> u32 {
     for (;;) {
       publish();
-      u32 q = 0;
-      if (lane == 0) q = atomicAdd(&chunk_next, 1u);
-      q = uni(q);
+      const u32 q_old = q_tk;
+      if (lane == 0) q_tk = atomicAdd(&chunk_next, 1u);
+      const u32 q = uni(q_old);
       if (!dyn_rows) {
         const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
         return f < p.n_blocks ? (u32)f : p.n_blocks;
@@ -1670,19 +1673,20 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
           if (lane == 0) pend_row = atomicAdd(p.row_ctr, 1u);
         } else if (lane == 0) {
           const u32 sx = slot_q + kRowAhead;
-          row_val[sx % kRowRing] = kRowExit;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __hip_atomic_store(&row_slot[sx % kRowRing], sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&row_ent[sx % kRowRing], (u64)kRowExit | (u64)sx << 32, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       u32 row = 0;
       if (lane == 0) {
-        u32 spins = 0, rs;
+        u32 spins = 0;
+        u64 ent;
         // (a slot's entry is overwritten kRowRing slots later; a reader that finds a later slot
         // there, or waits past the bound, reports it through the sticky error word: the launch
         // fails loudly at tpz_decode_check instead of passing blocks over)
-        while ((rs = __hip_atomic_load(&row_slot[slot_q % kRowRing], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP)) != slot_q) {
+        while ((u32)((ent = __hip_atomic_load(&row_ent[slot_q % kRowRing], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) != slot_q) {
+          const u32 rs = (u32)(ent >> 32);
           if (rs != ~0u && (int)(rs - slot_q) > 0) {
             atomicOr(p.err, 4u);
             break;
@@ -1693,8 +1697,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
             break;
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        row = rs != slot_q ? kRowExit : row_val[slot_q % kRowRing];
+        row = (u32)(ent >> 32) != slot_q ? kRowExit : (u32)ent;
       }
       row = uni(row);
       if (row != kRowExit) {
@@ -1800,12 +1803,16 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
     const bool fits = (e - s) <= kWaveMaxLen;
     if (fits) {
-      const u32 rounds = (u32)((e - (s & ~15ull)) + 1023) >> 10;
-      v[0] = zero_head(v[0], lane == 0 ? (u32)(s & 15u) : 0u);  // the previous block's tail
+      // every round: the loads past the block's last piece returned zeros (the descriptor), and
+      // the window holds all of rounds 0-3 and the first 256 bytes of round 4 (no per-round
+      // conditions: 0.x % per block)
 #pragma unroll
-      for (int r = 0; r < kWinRounds; r++)
-        if ((u32)r < rounds && r * 1024 + lane * 16 < (u32)kWinBytes)
-          *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
+      for (int r = 0; r < kWinRounds - 1; r++) *reinterpret_cast<uint4*>(win + r * 1024 + lane * 16) = v[r];
+      static_assert(kWinBytes == 4 * 1024 + 256, "round 4 fills lanes 0-15");
+      if (lane < 16) *reinterpret_cast<uint4*>(win + 4 * 1024 + lane * 16) = v[4];
+      // the bytes of the first piece before the block (the previous block's tail) read as zero
+      // for the CRC (one byte store per lane, in LDS order after the piece)
+      if (lane < (u32)(s & 15u)) win[lane] = 0;
     }
     TPZ_STAMP(S, 0);
     const u32 bcur = b;
