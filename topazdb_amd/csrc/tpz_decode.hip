@@ -1074,8 +1074,11 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   const u32 nw = (F.npad + 63) >> 6;
   const int seg = (int)Pa - kCrcLaneBytes * (int)(lane + 1);
   const bool cact = seg + kCrcLaneBytes > 0;
+  // lanes before the payload read the guard at -kGuard + 16 t (within its 96 zero bytes), so
+  // every step's address is one base plus the instruction's offset
+  const int cbase = cact ? pb + seg : -kGuard;
   auto dread = [&](int t) -> u32x4v {   // CRC data of step t (lanes before the payload: the guard)
-    return *reinterpret_cast<const u32x4v*>(win + (cact ? pb + seg + 16 * t : -kGuard));
+    return *reinterpret_cast<const u32x4v*>(win + cbase + 16 * t);
   };
   PWin W[4];
   // A: map reads, CRC data of step 0
