@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-closing run: GPU suite, smoke, bench (the driver's command), profiles
 set -o pipefail
-OUT=gpurun_out/close9
+OUT=${1:-gpurun_out/close9}
 mkdir -p $OUT
 timeout -k 10 1000 python3 -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gputest.log 2>&1 || { tail -40 $OUT/gputest.log; exit 1; }
 tail -2 $OUT/gputest.log
