@@ -20,6 +20,7 @@
 //   pipe_meta3x  the same three stores exec-masked to lane 0
 //   pipe_meta1   one store instruction, lanes 0-2 to the three arrays
 //   pipe_metarow the three arrays written per row of 16 chunks (wave 0, lanes 0-15)
+//   pipe_meta8   one packed 8-byte record per chunk (lane 0): a row's 16 records fill one line
 //   (profiles/r5/ubench_meta.jsonl: 1.59 / 1.77 / 1.77 / 1.81 / 1.66 ms for pipe_lds / meta3 /
 //   meta3x / meta1 / metarow: each small store is a write request of its own whatever its lane
 //   count; batching per row recovers two thirds in this kernel, but not in the decode,
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
   {
     const __amdgpu_buffer_rsrc_t rz = rsrc(d, 0);
 #pragma unroll
-    for (int q = 0; q < (MODE == 2 ? 8 : MODE == 6 ? 7 : MODE == 7 ? 5 : MODE == 8 ? 7 : MODE == 9 ? 5 : 4); q++)
+    for (int q = 0; q < (MODE == 2 ? 8 : MODE == 6 ? 7 : MODE == 7 ? 5 : MODE == 8 ? 7 : MODE == 9 ? 5 : MODE == 11 ? 5 : 4); q++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, q * 256, 0, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -147,6 +148,12 @@ __global__ __launch_bounds__(1024) void pipe_k(const uint8_t* __restrict__ s, ui
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)i, rm, on ? i : 0x7FFFFFF8u, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(i, rm, on ? (u32)(0x200000 + 4 * i) : 0x7FFFFFF8u, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(i, rm, on ? (u32)(0x800000 + 4 * i) : 0x7FFFFFF8u, 0, 0);
+    }
+    if (MODE == 11) {   // one packed 8-byte record per chunk (status | count | crc): a row of 16
+                        // chunks fills one 128-B line, written by one workgroup
+      const __amdgpu_buffer_rsrc_t rm = rsrc(meta, 0x7FFFFFF0ull);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) u32, make_uint2((u32)c, (u32)c)),
+                                            rm, lane == 0 ? (u32)(8 * c) : 0x7FFFFFF8u, 0, 0);
     }
     if (MODE == 2 || MODE == 7) {
       // one 512-B ends store per chunk, into an ends region of its own (chunk c's at 512 c of d,
@@ -338,6 +345,7 @@ int main(int argc, char** argv) {
       else if (v == "pipe_meta3x") pipe_k<8><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe_meta1") pipe_k<9><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe_metarow") pipe_k<10><<<cus, 1024>>>(a, b, m, nch);
+      else if (v == "pipe_meta8") pipe_k<11><<<cus, 1024>>>(a, b, m, nch);
       else if (v == "pipe8") pipe_k<1><<<cus, 512>>>(a, b, m, nch);
       else if (v == "pipe_dyn") { (void)hipMemsetAsync(m, 0, 4); pipedyn_k<<<cus, 1024>>>(a, b, (u32*)m, nch); }
       else if (v == "pipe_rd") pipe_k<5><<<cus, 1024>>>(a, b, m, nch);
