@@ -105,6 +105,47 @@ def test_large_ranges(ctx):
     np.testing.assert_array_equal(gpu_crcs(ctx, buf, ext, 9), expected(buf, ext))
 
 
+@pytest.mark.parametrize("shift", [0, 7])
+def test_long_and_short_ranges(ctx, shift):
+    """Thirty 1-5 MiB ranges (~90 MiB: every wave of the grid folds whole windows of them and
+    chains them by Horner) with short and empty ranges between long ones, ranges that start and
+    end inside windows, and a range ending at the buffer's last byte."""
+    rng = np.random.default_rng(40 + shift)
+    lens = [int(x) for x in rng.integers(1 << 20, 5 << 20, 30)]
+    lens[3:3] = [0, 1, 5, 17, 8192, 8191]
+    lens[20:20] = [0, 16, 24577]
+    lens.append(3 * (1 << 20) + 5)
+    assert sum(lens) // len(lens) >= 2 << 20
+    buf = rng.bytes(sum(lens))
+    ext = ranges_of(lens)
+    np.testing.assert_array_equal(gpu_crcs(ctx, buf, ext, shift), expected(buf, ext))
+
+
+def test_verify_many_files(ctx):
+    """tpz_verify_files over 24 synthetic 3-5 MiB files with their BE CRC trailers, two of them
+    corrupted (one in the body, one in the trailer): statuses and CRCs against zlib."""
+    rng = np.random.default_rng(77)
+    files = []
+    for i in range(24):
+        body = rng.bytes(int(rng.integers(3 << 20, 5 << 20)))
+        files.append(bytearray(body + struct.pack(">I", zlib.crc32(body))))
+    files[5][12345] ^= 1
+    files[17][-3] ^= 0x80          # the trailer itself
+    buf = b"".join(bytes(f) for f in files)
+    ext = ranges_of([len(f) for f in files])
+    b, _keep = device_batch(buf, ext, 3)
+    crc, st = verify_files(ctx, b)
+    torch.cuda.synchronize()
+    crc = crc[:len(files)].cpu().numpy().view(np.uint32)
+    st = st[:len(files)].cpu().numpy()
+    for i, f in enumerate(files):
+        want = zlib.crc32(bytes(f[:-4]))
+        assert crc[i] == want, i
+        ok = want == struct.unpack(">I", bytes(f[-4:]))[0]
+        assert st[i] == (_lib.BLOCK_OK if ok else _lib.BLOCK_CHECKSUM_MISMATCH), i
+    assert st[5] == _lib.BLOCK_CHECKSUM_MISMATCH and st[17] == _lib.BLOCK_CHECKSUM_MISMATCH
+
+
 def test_zero_and_ones_patterns(ctx):
     """Zero runs leave a raw CRC unchanged: ranges of zeros / 0xFF exercise the init term."""
     lens = [16384 * 3, 16384 * 3 + 1, 100, 5]

@@ -83,7 +83,7 @@ def main():
                     host = buf[a.offset:].cpu().numpy()
                 for i in picks:
                     assert got[i] == zlib.crc32(host[e[i]:e[i + 1]].tobytes()), (v, name, i)
-            else:
+            elif not v.startswith(("il", "abl")):   # (timing-only ablation builds: no check)
                 assert (got == ref[name]).all(), (v, name)
     host = None
     b, _, crc = outs["files"]

@@ -10,6 +10,7 @@
 //   copy_wave4k     persistent, one wave per 4 KiB chunk, 1 KiB per wave instruction
 //   memcpy          hipMemcpyAsync device to device
 //   copy_small      copy of 128 MiB (fits the 256 MiB Infinity Cache): not an HBM number
+//   read_span / read_claim[4|16] / read_win   the whole-file CRC's read pattern (readwin_k)
 // Prints one JSON line per variant: bytes moved (read + written) / median time.
 #include <hip/hip_runtime.h>
 
@@ -93,6 +94,90 @@ __global__ __launch_bounds__(256) void read_k(const uint4* __restrict__ s, u64 n
   }
   for (; i < n16; i += stride) acc += s[i].x;
   if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+// The whole-file CRC's read pattern without its fold (tpz_crc.hip crc_window_kernel): 8 KiB
+// windows, lane l reads the 128-byte run 128 l bytes before the window end (8 x 16-B loads), the
+// next window's loads issued before the current one is consumed.
+//   MODE 0 read_span   persistent, 16 waves per CU, each wave a contiguous span of windows
+//   MODE 1 read_claim  persistent, each wave claims CL windows at a time from one global counter
+//   MODE 2 read_win    one window per wave, a grid covering the buffer (4 waves per workgroup)
+//   MODE 3 read_ilCL   persistent, wave g takes spans k * waves + g of CL windows (static)
+//   MODE 4 read_wgspan persistent, workgroup x a contiguous span, its waves every 16th window
+template <int MODE, int CL>
+__global__ __launch_bounds__(1024) void readwin_k(const uint8_t* __restrict__ s, u64 nwin, u32* ctr, u32* out) {
+  const u32 lane = threadIdx.x & 63;
+  const u64 wv = (u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const u64 nw = (u64)gridDim.x * (blockDim.x >> 6);
+  u32 acc = 0;
+  auto ld = [&](u64 g, uint4 (&v)[8]) {
+    const uint8_t* p = s + (g << 13) + 8192 - 128 * (lane + 1);
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = *reinterpret_cast<const uint4*>(p + 16 * c);
+  };
+  auto use = [&](const uint4 (&v)[8]) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc += v[c].x ^ v[c].y ^ v[c].z ^ v[c].w;
+  };
+  uint4 v[8], w[8];
+  if (MODE == 2) {
+    if (wv < nwin) { ld(wv, v); use(v); }
+  } else if (MODE == 0) {
+    const u64 per = (nwin + nw - 1) / nw, g0 = wv * per, g1 = min(nwin, g0 + per);
+    if (g0 < g1) ld(g0, v);
+    for (u64 g = g0; g < g1; g++) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) w[c] = v[c];
+      if (g + 1 < g1) ld(g + 1, v);
+      use(w);
+    }
+  } else if (MODE == 3) {
+    // static interleave: wave g takes spans k * nw + g of CL consecutive windows (no atomics)
+    const u64 nsp = (nwin + CL - 1) / CL;
+    u64 sp = wv, k = 0;
+    if (sp < nsp) ld(sp * CL, v);
+    while (sp < nsp) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) w[c] = v[c];
+      u64 gn;
+      if (k + 1 < CL && sp * CL + k + 1 < nwin) { k++; gn = sp * CL + k; }
+      else { sp += nw; k = 0; gn = sp * CL; }
+      if (sp < nsp) ld(gn, v);
+      use(w);
+    }
+  } else if (MODE == 4) {
+    // workgroup spans: workgroup x owns a contiguous span of windows, its waves take every
+    // (waves per workgroup)-th window of it (wave w: span start + k * W + w)
+    const u64 W = blockDim.x >> 6, wid = threadIdx.x >> 6, nwg = gridDim.x;
+    const u64 per = ((nwin + nwg - 1) / nwg + W - 1) / W * W;
+    const u64 g0 = blockIdx.x * per + wid, g1 = min(nwin, (u64)(blockIdx.x + 1) * per);
+    if (g0 < g1) ld(g0, v);
+    for (u64 g = g0; g < g1; g += W) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) w[c] = v[c];
+      if (g + W < g1) ld(g + W, v);
+      use(w);
+    }
+  } else {
+    u32 base = 0;
+    if (lane == 0) base = atomicAdd(ctr, 1u);
+    u64 c0 = (u64)__builtin_amdgcn_readfirstlane(base) * CL;
+    u32 nxt = 0;
+    if (lane == 0) nxt = atomicAdd(ctr, 1u);
+    u32 k = 0;
+    if (c0 < nwin) ld(c0, v);
+    while (c0 + k < nwin) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) w[c] = v[c];
+      u64 gn;
+      if (k + 1 < CL) { gn = c0 + k + 1; k++; }
+      else { c0 = (u64)__builtin_amdgcn_readfirstlane(nxt) * CL; k = 0; gn = c0; if (lane == 0) nxt = atomicAdd(ctr, 1u); }
+      if (gn < nwin) ld(gn, v);
+      use(w);
+      if (gn >= nwin) break;
+    }
+  }
+  if (acc == 0x9E3779B9u) out[16] = acc;
 }
 
 __global__ __launch_bounds__(256) void write_k(uint4* __restrict__ d, u64 n16) {
@@ -335,10 +420,23 @@ int main(int argc, char** argv) {
       else if (v == "pp32") pp_k<<<cus * 2, 1024>>>(a, b, PPN / 4096);
       else if (v == "pp_flat") flat_w4k_k<<<(u32)(PPN / 4096 / 4), 256>>>(s, d, PPN / 4096);
       else if (v == "flat_w4k") flat_w4k_k<<<(u32)(N / 4096 / 4), 256>>>(s, d, N / 4096);
+      else if (v == "read_span") readwin_k<0, 1><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_claim") readwin_k<1, 1><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_claim4") readwin_k<1, 4><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_claim16") readwin_k<1, 16><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_il1") readwin_k<3, 1><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_il4") readwin_k<3, 4><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_il16") readwin_k<3, 16><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_il64") readwin_k<3, 64><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_il16x2") readwin_k<3, 16><<<2 * cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_wgspan") readwin_k<4, 1><<<cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_wgspan8") readwin_k<4, 1><<<cus, 512>>>(a, N >> 13, o, o);
+      else if (v == "read_wgspan2x") readwin_k<4, 1><<<2 * cus, 1024>>>(a, N >> 13, o, o);
+      else if (v == "read_win") readwin_k<2, 1><<<(u32)((N >> 13) / 4), 256>>>(a, N >> 13, o, o);
       else if (v == "memcpy") (void)hipMemcpyAsync(b, a, N, hipMemcpyDeviceToDevice, 0);
       else if (v == "copy_small") copy_k<4, false, false><<<cus * 8, 256>>>(s, d, small16);
     };
-    if (v == "read" || v == "write") moved = (double)N;
+    if (v == "read" || v == "write" || v.rfind("read_", 0) == 0) moved = (double)N;
     if (v.rfind("pp", 0) == 0) moved = 2.0 * PPN;
     if (v == "copy_small") moved = 2.0 * (128ull << 20);
     for (int w = 0; w < 3; w++) { CHECK(hipMemsetAsync(o, 0, 4096)); launch(); }
