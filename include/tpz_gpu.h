@@ -55,7 +55,8 @@ extern "C" {
  *      Block views of the caller's bytes). Round 6, same ABI: tpz_decode_blocks_host /
  *      tpz_verify_blocks_host return TPZ_ERR_NOMEM only for a short caller buffer (an internal
  *      chunk overflow is TPZ_ERR_INTERNAL), and tpz_decode_check also fails for a wave path row
- *      claim that timed out or was overwritten
+ *      claim that timed out or was overwritten; new entry point tpz_verify_files_flat_layout
+ *      (open + flat layout from one read of the blocks)
  * A consumer compiled against one header checks tpz_abi_version() == TPZ_ABI_VERSION. */
 #define TPZ_ABI_VERSION 6
 int tpz_abi_version(void);
@@ -443,6 +444,26 @@ tpz_err tpz_crc32_ranges(tpz_ctx* ctx, const tpz_batch* ranges, uint32_t* d_crc,
  * `buf[size - CHECKSUM_SIZE..]` panics). Asynchronous on `stream`. */
 tpz_err tpz_verify_files(tpz_ctx* ctx, const tpz_batch* files, uint32_t* d_crc,
                          uint8_t* d_status, void* stream);
+
+/* SsTable::open for every file + tpz_flat_layout of their data blocks, from ONE read of the
+ * blocks (the reference's open reads every byte for FileObject::open's CRC, src/table.rs:91-112,
+ * src/table/file_object.rs:57-78, before the blocks are read again to decode them): the outputs of
+ * tpz_verify_files over the files and of tpz_flat_layout(blocks, d_first).
+ *   blocks : every file's data region (its blocks, [0, meta offset) of an SST), the files' regions
+ *            back to back: the batch tpz_decode_blocks_flat then decodes
+ *   d_file_block : n_files + 1 u32; file f's blocks are blocks d_file_block[f] ..
+ *            d_file_block[f + 1] - 1 (d_file_block[n_files] = n_blocks)
+ *   tails  : n_files ranges; tail f = the rest of file f after its data region (meta block,
+ *            bloom filter, offsets and the 4-byte CRC trailer), so that file f is its data region
+ *            followed by tail f. Each tail holds at least the trailer (a file whose tail is
+ *            shorter than 4 bytes reports TPZ_BLOCK_MALFORMED with crc 0, as a file shorter than
+ *            its trailer does in tpz_verify_files)
+ *   d_crc, d_status : n_files, as tpz_verify_files
+ * Both d_src 16-byte aligned. Asynchronous on `stream`; uses the stream's workspace. */
+tpz_err tpz_verify_files_flat_layout(tpz_ctx* ctx, const tpz_batch* blocks,
+                                     const uint32_t* d_file_block, const tpz_batch* tails,
+                                     uint32_t* d_crc, uint8_t* d_status, uint64_t* d_first,
+                                     void* stream);
 
 /* ---- codec step of compress::decode (src/block/compress.rs:95-113) ------------------------
  * Snappy (tag 2) and LZ4 (tag 3) blocks are decompressed on the device into their Uncompress

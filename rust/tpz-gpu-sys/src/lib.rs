@@ -181,6 +181,10 @@ extern "C" {
                             stream: *mut c_void) -> TpzErr;
     pub fn tpz_verify_files(ctx: *mut TpzCtx, files: *const TpzBatch, d_crc: *mut u32,
                             d_status: *mut u8, stream: *mut c_void) -> TpzErr;
+    pub fn tpz_verify_files_flat_layout(ctx: *mut TpzCtx, blocks: *const TpzBatch,
+                                        d_file_block: *const u32, tails: *const TpzBatch,
+                                        d_crc: *mut u32, d_status: *mut u8, d_first: *mut u64,
+                                        stream: *mut c_void) -> TpzErr;
     pub fn tpz_decompressed_sizes(ctx: *mut TpzCtx, batch: *const TpzBatch, d_size: *mut u64,
                                   stream: *mut c_void) -> TpzErr;
     pub fn tpz_decompressed_sizes_claimed(ctx: *mut TpzCtx, batch: *const TpzBatch,

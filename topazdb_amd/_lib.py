@@ -121,6 +121,12 @@ def lib() -> C.CDLL:
         L.tpz_verify_files.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p,
                                        C.c_void_p]
         L.tpz_verify_files.restype = C.c_int
+        try:   # (absent from diagnostic builds of earlier commits, TPZ_LIB_PATH)
+            L.tpz_verify_files_flat_layout.argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p,
+                                                       C.POINTER(Batch)] + [C.c_void_p] * 4
+            L.tpz_verify_files_flat_layout.restype = C.c_int
+        except AttributeError:
+            pass
         for f in ("tpz_decompressed_sizes", "tpz_decompressed_sizes_claimed"):
             getattr(L, f).argtypes = [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_void_p]
             getattr(L, f).restype = C.c_int
@@ -404,6 +410,23 @@ class Context:
         check(lib().tpz_verify_files(self.handle, C.byref(b), C.c_void_p(d_crc),
                                      C.c_void_p(d_status), C.c_void_p(stream)),
               "tpz_verify_files")
+
+    def open_flat_layout_ptrs(self, d_src: int, d_ext: int, n_blocks: int, src_bytes: int,
+                              d_file_block: int, d_tsrc: int, d_text: int, n_files: int,
+                              tail_bytes: int, d_crc: int, d_status: int, d_first: int,
+                              stream: int = 0) -> None:
+        """tpz_verify_files_flat_layout: tpz_verify_files over the files (data region + tail) and
+        tpz_flat_layout over their blocks from one read of the blocks (file_object.rs:57-78,
+        iterator.rs:74-82)."""
+        if not hasattr(lib(), "tpz_verify_files_flat_layout"):
+            raise RuntimeError("libtpz_gpu.so lacks tpz_verify_files_flat_layout (an older build)")
+        b = Batch(d_src, d_ext, n_blocks, src_bytes)
+        t = Batch(d_tsrc, d_text, n_files, tail_bytes)
+        check(lib().tpz_verify_files_flat_layout(self.handle, C.byref(b), C.c_void_p(d_file_block),
+                                                 C.byref(t), C.c_void_p(d_crc),
+                                                 C.c_void_p(d_status), C.c_void_p(d_first),
+                                                 C.c_void_p(stream)),
+              "tpz_verify_files_flat_layout")
 
     def seek_keys_ptrs(self, table: Table, d_keys: int, d_key_pos: int, n_keys: int,
                        d_block: int, d_entry: int, d_status: int, d_valid: int,

@@ -282,10 +282,12 @@ class FlatColumns:
     the whole batch, in SsTableIterator order, plus exact {kend, vend} pairs per block."""
 
     def __init__(self, ctx: Context, batch: DeviceBatch, spill_cap: int = 0,
-                 stream: torch.cuda.Stream | None = None):
+                 stream: torch.cuda.Stream | None = None, first: torch.Tensor | None = None):
+        """first: the batch's [3, n_blocks + 1] reservations when the caller has them already
+        (open_flat_layout); None: tpz_flat_layout computes them."""
         dev = _dev(ctx.device)
         self.device = ctx.device
-        self.first = flat_layout(ctx, batch, stream)
+        self.first = flat_layout(ctx, batch, stream) if first is None else first
         tot = self.first[:, batch.n_blocks].cpu().numpy()      # one sync: the column sizes
         self.n_pairs, self.key_bytes, self.value_bytes = (int(x) for x in tot)
         nb = max(batch.n_blocks, 1)
@@ -419,6 +421,30 @@ def verify_files(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | N
     ctx.verify_files_ptrs(batch.src.data_ptr(), batch.ext.data_ptr(), batch.n_blocks,
                           batch.src_bytes, crc.data_ptr(), st.data_ptr(), s.cuda_stream)
     return crc, st
+
+
+def open_flat_layout(ctx: Context, blocks: DeviceBatch, file_block: torch.Tensor,
+                     tails: DeviceBatch, stream: torch.cuda.Stream | None = None):
+    """SsTable::open (FileObject::open's whole-file CRC, src/table/file_object.rs:57-78) for every
+    file and tpz_flat_layout of its data blocks from one read of the blocks
+    (tpz_verify_files_flat_layout). blocks: every file's data region back to back (the batch
+    decode_flat takes); file_block: int32 device, n_files + 1 entries, file f's blocks are
+    file_block[f] .. file_block[f + 1] - 1; tails: n_files ranges, the rest of each file after
+    its data region (meta, bloom, offsets, CRC trailer). Returns (crc, status, first [3, n_blocks
+    + 1]); hand `first` to FlatColumns."""
+    dev = _dev(ctx.device)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    assert file_block.dtype == torch.int32 and file_block.is_cuda
+    assert file_block.numel() == tails.n_blocks + 1
+    with torch.cuda.stream(s):
+        crc = torch.empty(max(tails.n_blocks, 1), dtype=torch.int32, device=dev)
+        st = torch.empty(max(tails.n_blocks, 1), dtype=torch.uint8, device=dev)
+        first = torch.empty(3 * (blocks.n_blocks + 1), dtype=torch.int64, device=dev)
+    ctx.open_flat_layout_ptrs(blocks.src.data_ptr(), blocks.ext.data_ptr(), blocks.n_blocks,
+                              blocks.src_bytes, file_block.data_ptr(), tails.src.data_ptr(),
+                              tails.ext.data_ptr(), tails.n_blocks, tails.src_bytes,
+                              crc.data_ptr(), st.data_ptr(), first.data_ptr(), s.cuda_stream)
+    return crc, st, first.view(3, blocks.n_blocks + 1)
 
 
 def decompress_batch(ctx: Context, batch: DeviceBatch, stream: torch.cuda.Stream | None = None,

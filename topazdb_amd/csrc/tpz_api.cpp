@@ -91,7 +91,7 @@ std::vector<uint32_t> build_range_tables() {
     for (int i = 0; i < 8; i++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
     t0[b] = c;
   }
-  std::vector<uint32_t> out((size_t)tpz::kRangeTables * 256);
+  std::vector<uint32_t> out((size_t)tpz::kRangeTablesAll * 256);
   auto put = [&](int id, uint64_t k) {
     const uint32_t z = x8n(k);
     for (uint32_t b = 0; b < 256; b++) out[(size_t)id * 256 + b] = t0[b] ? multmodp(z, t0[b]) : 0u;
@@ -101,6 +101,9 @@ std::vector<uint32_t> build_range_tables() {
     const uint64_t n = 16ull << j;
     for (int i = 0; i < 4; i++) put(16 + 4 * j + i, n - 1 - (uint64_t)i);
   }
+  for (int i = 0; i < 4; i++)
+    for (uint64_t j = 0; j < 256; j++)
+      out[(size_t)(tpz::kPowTable + i) * 256 + j] = x8n(j << (8 * i));
   return out;
 }
 
@@ -636,6 +639,54 @@ tpz_err tpz_verify_files(tpz_ctx* c, const tpz_batch* f, uint32_t* d_crc, uint8_
                          void* stream) {
   if (!d_status) return TPZ_ERR_INVALID_ARG;
   return crc_ranges(c, f, 4, d_crc, d_status, stream);
+}
+
+tpz_err tpz_verify_files_flat_layout(tpz_ctx* c, const tpz_batch* blocks,
+                                     const uint32_t* d_file_block, const tpz_batch* tails,
+                                     uint32_t* d_crc, uint8_t* d_status, uint64_t* d_first,
+                                     void* stream) {
+  if (!c || !blocks || !tails || !d_first || !d_file_block) return TPZ_ERR_INVALID_ARG;
+  if (blocks->n_blocks && (!blocks->d_src || !blocks->d_ext ||
+                           (reinterpret_cast<uintptr_t>(blocks->d_src) & 15u)))
+    return TPZ_ERR_INVALID_ARG;
+  if (tails->n_blocks && (!tails->d_src || !tails->d_ext || !d_crc || !d_status ||
+                          (reinterpret_cast<uintptr_t>(tails->d_src) & 15u)))
+    return TPZ_ERR_INVALID_ARG;
+  if (blocks->n_blocks == 0 && tails->n_blocks == 0) {
+    TPZ_HIP(hipSetDevice(c->device));
+    TPZ_HIP(hipMemsetAsync(d_first, 0, 3 * 8, (hipStream_t)stream));
+    return TPZ_SUCCESS;
+  }
+  TPZ_HIP(hipSetDevice(c->device));
+  const uint64_t parts = tpz::flat_scan_parts_words(blocks->n_blocks);
+  const uint64_t words = 2 * parts + blocks->n_blocks;
+  if (words > 0xFFFFFFFFull) return TPZ_ERR_INVALID_ARG;
+  uint32_t* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    tpz_err e = get_acc(c, stream, (uint32_t)words, &ws);
+    if (e != TPZ_SUCCESS) return e;
+  }
+  tpz::OpenLaunch a{};
+  a.src = blocks->d_src;
+  a.bext = blocks->d_ext;
+  a.src_bytes = blocks->src_bytes;
+  a.n_blocks = blocks->n_blocks;
+  a.fblock = d_file_block;
+  a.n_files = tails->n_blocks;
+  a.tsrc = tails->d_src;
+  a.text = tails->d_ext;
+  a.first = d_first;
+  a.part = reinterpret_cast<uint64_t*>(ws);
+  a.cb = ws + 2 * parts;
+  a.dtab = c->d_tables;
+  a.rtab = c->d_range_tables;
+  a.crc = d_crc;
+  a.status = d_status;
+  a.num_cus = c->num_cus;
+  tpz::launch_open_flat(a, (hipStream_t)stream);
+  TPZ_HIP(hipGetLastError());
+  return TPZ_SUCCESS;
 }
 
 tpz_err tpz_seek_keys(tpz_ctx* c, const tpz_table* t, const uint8_t* d_keys,

@@ -39,6 +39,10 @@ constexpr uint32_t kBigMaxSlots = TPZ_LDS_BLOCK_BYTES / 6 + 16;
 // slice-by-4 table (4 x 256 x 32 u32).
 constexpr int kRangeShiftOps = 32;
 constexpr int kRangeTables = 16 + 4 * kRangeShiftOps;
+// ... followed by 4 power tables: id kPowTable + i, entry j = x^(8 j 256^i) mod P (the shift by
+// j * 256^i bytes as a GF(2)[x] factor: tpz_flat.hip open_finish_kernel)
+constexpr int kPowTable = kRangeTables;
+constexpr int kRangeTablesAll = kRangeTables + 4;
 constexpr int kCrcRepWords = 4 * 256 * 32;
 
 // Slotted layout (include/tpz_gpu.h), callable from device code.
@@ -300,6 +304,28 @@ void launch_compress(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes
 void launch_flat_layout(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
                         uint32_t n_blocks, uint64_t* first, uint64_t* part, uint32_t num_cus,
                         hipStream_t stream);
+// tpz_verify_files_flat_layout (tpz_flat.hip): the whole-file CRC of n_files SST files (data
+// region = blocks fblock[f] .. fblock[f + 1] - 1, then the tail) and the flat reservations of
+// their data blocks from one read of the blocks.
+struct OpenLaunch {
+  const uint8_t* src;
+  const uint64_t* bext;
+  uint64_t src_bytes;
+  uint32_t n_blocks;
+  const uint32_t* fblock;   // n_files + 1
+  uint32_t n_files;
+  const uint8_t* tsrc;      // the files' tails (meta, bloom, offsets, trailer)
+  const uint64_t* text;
+  uint64_t* first;        // 3 x (n_blocks + 1)
+  uint64_t* part;         // workspace: flat_scan_parts_words(n_blocks) u64
+  uint32_t* cb;           // workspace: n_blocks
+  const uint32_t* dtab;   // decode tables
+  const uint32_t* rtab;   // range tables
+  uint32_t* crc;
+  uint8_t* status;
+  uint32_t num_cus;
+};
+void launch_open_flat(const OpenLaunch& a, hipStream_t stream);
 void launch_entry_first(const uint8_t* src, const uint64_t* ext, uint64_t src_bytes,
                         uint32_t n_blocks, uint64_t* first, uint64_t* part, hipStream_t stream);
 // first[i] = exclusive prefix of count over decoded (OK / OK_SPILLED) blocks, first[n] = total.
