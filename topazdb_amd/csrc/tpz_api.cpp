@@ -659,7 +659,7 @@ tpz_err tpz_verify_files_flat_layout(tpz_ctx* c, const tpz_batch* blocks,
   }
   TPZ_HIP(hipSetDevice(c->device));
   const uint64_t parts = tpz::flat_scan_parts_words(blocks->n_blocks);
-  const uint64_t words = 2 * parts + blocks->n_blocks;
+  const uint64_t words = 2 * parts + blocks->n_blocks + tails->n_blocks;
   if (words > 0xFFFFFFFFull) return TPZ_ERR_INVALID_ARG;
   uint32_t* ws = nullptr;
   {
@@ -679,6 +679,11 @@ tpz_err tpz_verify_files_flat_layout(tpz_ctx* c, const tpz_batch* blocks,
   a.first = d_first;
   a.part = reinterpret_cast<uint64_t*>(ws);
   a.cb = ws + 2 * parts;
+  a.tacc = ws + 2 * parts + blocks->n_blocks;
+  a.rep = c->d_rep_tables;
+  a.tail_bytes = tails->src_bytes;
+  if (tails->n_blocks)
+    TPZ_HIP(hipMemsetAsync(a.tacc, 0, (size_t)tails->n_blocks * 4, (hipStream_t)stream));
   a.dtab = c->d_tables;
   a.rtab = c->d_range_tables;
   a.crc = d_crc;

@@ -314,7 +314,8 @@ void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream) {
   if (wgs > a.num_cus) wgs = a.num_cus;
   if (wgs == 0) wgs = 1;
   hipLaunchKernelGGL(crc_window_kernel, dim3((u32)wgs), dim3(kThreads), 0, stream, p);
-  hipLaunchKernelGGL(crc_finish_kernel, dim3((a.n_ranges + 255) / 256), dim3(256), 0, stream, p);
+  if (!a.acc_only)
+    hipLaunchKernelGGL(crc_finish_kernel, dim3((a.n_ranges + 255) / 256), dim3(256), 0, stream, p);
 }
 
 }  // namespace tpz

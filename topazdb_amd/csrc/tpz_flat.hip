@@ -226,7 +226,15 @@ constexpr int kOpWaves = 8;
 constexpr int kOpThreads = kOpWaves * 64;
 constexpr int kOpGuard = 96;                      // zeroed: a lane run may start up to 80 B before 0
 constexpr int kOpSlot = kOpGuard + kFlWin;
-constexpr int kOpLds = 16 * 1024 + kOpWaves * kOpSlot;
+#ifdef TPZ_OPEN_REP8
+// (diagnostic build) slice-by-4 tables replicated 8 times, lane l reading replica l % 8
+constexpr int kOpTabBytes = 4 * 256 * 8 * 4;
+constexpr int kOpWgsPerCu = 2;
+#else
+constexpr int kOpTabBytes = 16 * 1024;
+constexpr int kOpWgsPerCu = 3;
+#endif
+constexpr int kOpLds = kOpTabBytes + kOpWaves * kOpSlot;
 
 struct OpenParams {
   const uint8_t* src;
@@ -238,7 +246,8 @@ struct OpenParams {
   const uint8_t* tsrc;    // the tails: tail f = tsrc[text[f] .. text[f + 1])
   const u64* text;
   u64* first;             // 3 x (nb + 1): reservations (scanned afterwards)
-  u32* cb;                // nb: Z_{dend - e_b}(R0(block b))
+  u32* cb;                // nb: Z_{k_b}(R0(block b)) (open_blocks_kernel)
+  const u32* tacc;        // nf: R0 of each tail's main part (crc_window_kernel, trailer 4)
   const u32* dtab;        // the decode tables (ids 0..15 slice-by-16, kCrcInvTable)
   const u32* rtab;        // the range tables (shift-by-16*2^j operators)
   u32* crc;               // nf
@@ -314,10 +323,27 @@ __device__ __forceinline__ uint4 op_chunk(const uint8_t* src, int64_t x, u64 lo,
 __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kOpLds];
   u32* tab = reinterpret_cast<u32*>(lds);
+#ifdef TPZ_OPEN_REP8
+  for (int i = threadIdx.x; i < 4 * 256 * 8; i += kOpThreads) tab[i] = p.dtab[i >> 3];
+  const u32 rr = lane_id() & 7u;
+  auto fold = [&](u32 c, const uint4& w) {
+    u32 x = c ^ w.x;
+    auto s4 = [&](u32 v) {
+      return op_xor3(tab[((3u * 256u + (v & 0xFF)) << 3) + rr], tab[((2u * 256u + ((v >> 8) & 0xFF)) << 3) + rr],
+                     tab[((1u * 256u + ((v >> 16) & 0xFF)) << 3) + rr]) ^ tab[((v >> 24) << 3) + rr];
+    };
+    x = s4(x);
+    x = s4(x ^ w.y);
+    x = s4(x ^ w.z);
+    return s4(x ^ w.w);
+  };
+#else
   for (int i = threadIdx.x; i < 16 * 256 / 4; i += kOpThreads)
     reinterpret_cast<uint4*>(tab)[i] = reinterpret_cast<const uint4*>(p.dtab)[i];
+  auto fold = [&](u32 c, const uint4& w) { return op_slice16(tab, w.x ^ c, w.y, w.z, w.w); };
+#endif
   const u32 lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* slot = lds + 16 * 1024 + wid * kOpSlot;
+  uint8_t* slot = lds + kOpTabBytes + wid * kOpSlot;
   uint8_t* win = slot + kOpGuard;
   if (lane < kOpGuard / 16) reinterpret_cast<uint4*>(slot)[lane] = make_uint4(0, 0, 0, 0);
   __syncthreads();
@@ -379,7 +405,7 @@ __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
 #pragma unroll
           for (int t = 0; t < 5; t++) {
             const uint4 w = *reinterpret_cast<const uint4*>(win + r0 + 16 * t);
-            c = op_slice16(tab, w.x ^ c, w.y, w.z, w.w);
+            c = fold(c, w);
           }
         }
         X = op_wave_xor(op_gfmul(kl, c));
@@ -394,7 +420,7 @@ __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
 #pragma unroll
           for (int t = 0; t < 5; t++) {
             const uint4 w = op_chunk(p.src, r0 + 16 * t, s, e);
-            c = op_slice16(tab, w.x ^ c, w.y, w.z, w.w);
+            c = fold(c, w);
           }
           A = op_gfmul(p.round_shift, A) ^ c;   // Horner by one 5120-byte round
         }
@@ -415,9 +441,10 @@ __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
   }
 }
 
-// One workgroup per file: the XOR of its blocks' values, the fold of its tail's CRC bytes (thread
-// t a contiguous run of 16-byte chunks, shifted to the region's end), the init term, the trailer
-// compare (crc_finish_kernel's outcome; a file shorter than 4 bytes is MALFORMED, file_object.rs:69).
+// One workgroup per file: the XOR of its blocks' values, its tail's R0 (crc_window_kernel's main
+// part, then the last < 16 bytes), the init term, the trailer compare (crc_finish_kernel's
+// outcome; a file shorter than 4 bytes is MALFORMED, file_object.rs:69). (A first version folded
+// the tails here, one workgroup per 1 MiB tail: 0.29 ms of the open for the 4k shard.)
 constexpr int kFinThreads = 1024;
 __global__ __launch_bounds__(kFinThreads) void open_finish_kernel(OpenParams p) {
   __shared__ u32 red[kFinThreads / 64];
@@ -457,25 +484,19 @@ __global__ __launch_bounds__(kFinThreads) void open_finish_kernel(OpenParams p) 
     }
     D ^= C;
   }
-  const u64 x0 = tlo & ~15ull, e16 = (e + 15) & ~15ull;
-  const u64 J = e16 > x0 ? (e16 - x0) / 16 : 0, q = (J + kFinThreads - 1) / kFinThreads;
-  u32 c = 0;
-  const u64 j0 = (u64)t * q, j1 = min(J, j0 + q);
-  for (u64 j = j0; j < j1; j++) {
-    const uint4 w = op_chunk(p.tsrc, (int64_t)(x0 + 16 * j), tlo, e);
-    c = op_slice16(p.dtab, w.x ^ c, w.y, w.z, w.w);
-  }
-  // Y = Z_k2(R0(tail bytes)), k2 = e16 - e; the data region's share shifted to the same end
-  u32 Y = j1 > j0 ? op_zshift(p.rtab, c, 16 * (J - j1)) : 0u;
-  if (D) Y ^= op_zshift(p.rtab, D, e16 - tlo);   // (linear: each thread's share of D)
-  Y = op_wave_xor(Y);
-  if ((t & 63) == 0) red[t >> 6] = Y;
+  D = op_wave_xor(D);
+  if ((t & 63) == 0) red[t >> 6] = D;
   __syncthreads();
   if (t == 0) {
-    u32 W = 0;
-    for (int i = 0; i < kFinThreads / 64; i++) W ^= red[i];
+    D = 0;
+    for (int i = 0; i < kFinThreads / 64; i++) D ^= red[i];
+    // the tail's CRC bytes [tlo, e): crc_window_kernel's R0 of the main part [tlo, A),
+    // A = max(tlo, e & ~15), then the (< 16) bytes [A, e) one at a time (crc_finish_kernel)
+    const u64 A = (e & ~15ull) > tlo ? (e & ~15ull) : tlo;
+    u32 T = p.tacc[f];
+    for (u64 x = A; x < e; x++) T = (T >> 8) ^ p.dtab[(T ^ p.tsrc[x]) & 0xFF];
     const u64 len = (dend - dlo) + (e - tlo);
-    const u32 R = op_unshift(p.dtab, W, (u32)(e16 - e)) ^ op_zshift(p.rtab, 0xFFFFFFFFu, len);
+    const u32 R = op_zshift(p.rtab, D, e - tlo) ^ T ^ op_zshift(p.rtab, 0xFFFFFFFFu, len);
     const u32 crc = ~R;
     p.crc[f] = crc;
     const uint8_t* tr = p.tsrc + e;     // the trailer: big-endian u32 (file_object.rs:69)
@@ -537,6 +558,7 @@ void launch_open_flat(const OpenLaunch& a, hipStream_t stream) {
   p.rtab = a.rtab;
   p.crc = a.crc;
   p.status = a.status;
+  p.tacc = a.tacc;
   static const struct Shifts {
     u32 lane[64], round;
     Shifts() {
@@ -548,7 +570,7 @@ void launch_open_flat(const OpenLaunch& a, hipStream_t stream) {
   p.round_shift = sh.round;
   if (a.n_blocks) {
     u64 wgs = ((u64)a.n_blocks + kOpWaves - 1) / kOpWaves;
-    const u64 cap = 3ull * a.num_cus;     // three 8-wave workgroups per CU (52 KiB of LDS each)
+    const u64 cap = (u64)kOpWgsPerCu * a.num_cus;   // 8-wave workgroups per CU the LDS holds
     if (wgs > cap) wgs = cap;
     hipLaunchKernelGGL(open_blocks_kernel, dim3((u32)wgs), dim3(kOpThreads), 0, stream, p);
     const u32 np = (a.n_blocks + kScWg - 1) / kScWg;
@@ -558,7 +580,22 @@ void launch_open_flat(const OpenLaunch& a, hipStream_t stream) {
   } else {
     (void)hipMemsetAsync(a.first, 0, 3 * 8, stream);
   }
-  if (a.n_files) hipLaunchKernelGGL(open_finish_kernel, dim3(a.n_files), dim3(kFinThreads), 0, stream, p);
+  if (a.n_files) {
+    // the tails' main parts by the whole-file CRC kernel (trailer 4: [tlo, thi - 4))
+    CrcLaunch c{};
+    c.src = a.tsrc;
+    c.ext = a.text;
+    c.src_bytes = a.tail_bytes;
+    c.n_ranges = a.n_files;
+    c.trailer = 4;
+    c.tables = a.rtab;
+    c.rep = a.rep;
+    c.acc = a.tacc;
+    c.num_cus = a.num_cus;
+    c.acc_only = true;
+    launch_crc_ranges(c, stream);
+    hipLaunchKernelGGL(open_finish_kernel, dim3(a.n_files), dim3(kFinThreads), 0, stream, p);
+  }
 }
 
 }  // namespace tpz

@@ -223,6 +223,8 @@ struct CrcLaunch {
   uint32_t* crc;
   uint8_t* status;        // null for plain ranges
   uint32_t num_cus;
+  bool acc_only;          // leave R0 of every range's main part in acc (no finish kernel:
+                          // tpz_flat.hip open_finish_kernel finishes the files' tails)
 };
 
 void launch_crc_ranges(const CrcLaunch& a, hipStream_t stream);
@@ -316,9 +318,12 @@ struct OpenLaunch {
   uint32_t n_files;
   const uint8_t* tsrc;      // the files' tails (meta, bloom, offsets, trailer)
   const uint64_t* text;
+  uint64_t tail_bytes;
   uint64_t* first;        // 3 x (n_blocks + 1)
   uint64_t* part;         // workspace: flat_scan_parts_words(n_blocks) u64
   uint32_t* cb;           // workspace: n_blocks
+  uint32_t* tacc;         // workspace: n_files, zeroed (the tails' main-part R0, crc_window_kernel)
+  const uint32_t* rep;    // the replicated slice-by-4 tables (crc_window_kernel)
   const uint32_t* dtab;   // decode tables
   const uint32_t* rtab;   // range tables
   uint32_t* crc;
