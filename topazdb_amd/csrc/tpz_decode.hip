@@ -159,7 +159,17 @@ __device__ __forceinline__ uint4 lds_window16(const uint8_t* base, int x) {
 // ------------------------------------------------------------------ CRC-32 (table driven)
 // tab = kNumCrcTables x 256 u32 in LDS. T_k[b] = R0(b || 0^k): raw CRC (init 0, no xorout).
 // ids 0..15: T_0..T_15 (slice-by-16); ids 16+4j+i: T_{n_j-1-i}, n_j = kCrcShiftBytes[j].
+#ifdef TPZ_ABL_NOCF
+// timing build (wrong CRCs): every lookup of a half-wave hits its own bank (lane l reads word l %
+// 32 of the table), with the dependence on the byte kept; prices the bank conflicts of the CRC
+__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
+  u32 z = byte;
+  asm volatile("" : "+v"(z));
+  return tab[id * 256 + (((z & 0x10000u) + __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u)];
+}
+#else
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
+#endif
 
 // a ^ b ^ c in one v_bitop3_b32.
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
