@@ -226,14 +226,8 @@ constexpr int kOpWaves = 8;
 constexpr int kOpThreads = kOpWaves * 64;
 constexpr int kOpGuard = 96;                      // zeroed: a lane run may start up to 80 B before 0
 constexpr int kOpSlot = kOpGuard + kFlWin;
-#ifdef TPZ_OPEN_REP8
-// (diagnostic build) slice-by-4 tables replicated 8 times, lane l reading replica l % 8
-constexpr int kOpTabBytes = 4 * 256 * 8 * 4;
-constexpr int kOpWgsPerCu = 2;
-#else
-constexpr int kOpTabBytes = 16 * 1024;
-constexpr int kOpWgsPerCu = 3;
-#endif
+constexpr int kOpTabBytes = 16 * 1024;       // slice-by-16 (conflict-light replicated layouts:
+constexpr int kOpWgsPerCu = 3;                // slower)
 constexpr int kOpLds = kOpTabBytes + kOpWaves * kOpSlot;
 
 struct OpenParams {
@@ -323,25 +317,9 @@ __device__ __forceinline__ uint4 op_chunk(const uint8_t* src, int64_t x, u64 lo,
 __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kOpLds];
   u32* tab = reinterpret_cast<u32*>(lds);
-#ifdef TPZ_OPEN_REP8
-  for (int i = threadIdx.x; i < 4 * 256 * 8; i += kOpThreads) tab[i] = p.dtab[i >> 3];
-  const u32 rr = lane_id() & 7u;
-  auto fold = [&](u32 c, const uint4& w) {
-    u32 x = c ^ w.x;
-    auto s4 = [&](u32 v) {
-      return op_xor3(tab[((3u * 256u + (v & 0xFF)) << 3) + rr], tab[((2u * 256u + ((v >> 8) & 0xFF)) << 3) + rr],
-                     tab[((1u * 256u + ((v >> 16) & 0xFF)) << 3) + rr]) ^ tab[((v >> 24) << 3) + rr];
-    };
-    x = s4(x);
-    x = s4(x ^ w.y);
-    x = s4(x ^ w.z);
-    return s4(x ^ w.w);
-  };
-#else
   for (int i = threadIdx.x; i < 16 * 256 / 4; i += kOpThreads)
     reinterpret_cast<uint4*>(tab)[i] = reinterpret_cast<const uint4*>(p.dtab)[i];
   auto fold = [&](u32 c, const uint4& w) { return op_slice16(tab, w.x ^ c, w.y, w.z, w.w); };
-#endif
   const u32 lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* slot = lds + kOpTabBytes + wid * kOpSlot;
   uint8_t* win = slot + kOpGuard;
