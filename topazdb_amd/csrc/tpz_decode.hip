@@ -1067,7 +1067,7 @@ struct PWin {
   bool act, cross;
   Gath ga, gn;
 };
-// Window 0 of copy_crc_piped<K3>: the key window of a block with keys under 16 bytes (Zipf
+// Windows w < K3 of copy_crc_piped<K3>: the key windows of a block with keys under 16 bytes (Zipf
 // keys), copy_fast3's chunk rule: entries j .. j + 3, a lost map race taken back, up to three
 // segments per chunk; a chunk beyond that sends the window to copy_window afterwards.
 struct PWin3 {
@@ -1077,7 +1077,7 @@ struct PWin3 {
   Gath g2;
 };
 
-template <bool FLAT, bool K3>
+template <bool FLAT, u32 K3>
 __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
@@ -1139,7 +1139,10 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   u32 rare = 0;
   auto gissue = [&](PWin& P, u32 w) {
     const u32 x0 = 16 * (64 * w + lane);
-    if (K3 && w == 0) {
+    if (w < K3) {
+      // (window 0's entries j + 2, j + 3 were read with its others; a later window's are read
+      // here, into the same registers: window 0 has been stored by then)
+      if (w > 0) col.get2(min(P.j + 2, F.last), W3.e2, W3.d2, W3.e3, W3.d3);
       if (P.act && P.e0 <= x0) {      // a lost map race: the next entry holds the chunk start
         P.j++;
         P.e0 = P.e1, P.d0 = P.d1, P.e1 = W3.e2, P.d1 = W3.d2, W3.e2 = W3.e3, W3.d2 = W3.d3;
@@ -1147,7 +1150,7 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
       P.cross = P.act && P.j + 1 < F.nk && P.e0 < x0 + 16;
       W3.b2 = P.cross && P.j + 2 < F.nk && P.e1 < x0 + 16;
       if (__ballot(P.act && (P.e0 <= x0 || (W3.b2 && W3.e2 < x0 + 16 && P.j + 3 < F.nk))) != 0)
-        rare |= 1u;
+        rare |= 1u << w;
       W3.g2 = gath_issue(win, W3.b2 ? (int)x0 + W3.d2 : -kGuard);
     } else {
       P.cross = P.act && P.j + 1 < F.nk && P.e0 < x0 + 16;
@@ -1160,11 +1163,11 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
     const u32 x0 = 16 * c;
     // (no rare path outside a K3 window 0: the other windows hold values of 16 bytes or more,
     // so no two segments end in one chunk and no chunk meets three segments)
-    const bool rw = K3 && w == 0 && (rare & 1u);
+    const bool rw = w < K3 && (rare & (1u << w));
     uint4 acc = gath_finish(P.ga, P.act ? (int)x0 + P.d0 : -kGuard);
     const uint4 nx = gath_finish(P.gn, P.cross ? (int)x0 + P.d1 : -kGuard);
     if (P.cross) acc = merge_at(acc, nx, (int)(P.e0 - x0));
-    if (K3 && w == 0) {
+    if (w < K3) {
       const uint4 n2 = gath_finish(W3.g2, W3.b2 ? (int)x0 + W3.d2 : -kGuard);
       if (W3.b2) acc = merge_at(acc, n2, (int)(P.e1 - x0));
     }
@@ -1452,15 +1455,15 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       u32 lc;
       fin.on = false;      // the previous block's combine runs here, before pd is reused
       if (!f_short) {
-        lc = copy_crc_piped<FLAT, false>(tab, *reinterpret_cast<const ColSmall*>(&col),
+        lc = copy_crc_piped<FLAT, 0u>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                          reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                          fo, win, pb, P + k, o, pd);
-      } else if (!FLAT && f_w3 == 1u) {
-        // short keys within the first copy window, values of 16 bytes or more (the Zipf shape;
-        // slotted only: the flat kernel spills VGPRs with it)
-        lc = copy_crc_piped<FLAT, true>(tab, *reinterpret_cast<const ColSmall*>(&col),
-                                        reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
-                                        fo, win, pb, P + k, o, pd);
+      } else if (!FLAT && f_w3 <= 2u) {
+        // short keys within the first two copy windows, values of 16 bytes or more (the Zipf
+        // shape; slotted only: the flat kernel spills VGPRs with it)
+        lc = copy_crc_piped<FLAT, 2u>(tab, *reinterpret_cast<const ColSmall*>(&col),
+                                      reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
+                                      fo, win, pb, P + k, o, pd);
         f_short = false;   // (its combine ran interleaved: the next block need not run it early)
       } else
       {
