@@ -46,12 +46,19 @@ typedef uint64_t u64;
 
 // ------------------------------------------------------------------ LDS geometry
 constexpr int kWave = 64;
+#ifdef TPZ_ABL_W20
+// timing build (wrong CRCs: the shift and inverse tables alias T_0..T_15): two workgroups of 10
+// waves per CU (20 waves), 16 KiB of tables per workgroup, 64-entry tables, VGPRs capped at 96
+// (the compiler spills what does not fit); prices VERDICT r5's 18-20-wave shape
+constexpr int kWavesPerWG = 10;
+#else
 constexpr int kWavesPerWG = 16;
+#endif
 constexpr int kWGThreads = kWave * kWavesPerWG;
 // Blocks a wave of the wave path claims at a time (decode_wave_kernel): 2^chunk_shift, chosen
 // per launch (launch_decode); TPZ_WAVE_CHUNK forces one (diagnostic builds).
-static_assert(kWavesPerWG == 16 || kWavesPerWG == 8, "chunks of 2^k blocks tile a workgroup's row");
-constexpr u32 kRowShift = kWavesPerWG == 16 ? 4 : 3;
+// rows of 16 blocks (the claim unit of the wave path; chunks of 2^k blocks tile a row)
+constexpr u32 kRowShift = 4, kRowBlocks = 1u << kRowShift;
 // wave path: a workgroup's rows are claimed kRowAhead row slots ahead, into a ring of kRowRing
 // (2^20 4k blocks: 2 slots 1.902 ms, 3 1.853-1.866, 4 1.859-1.878, 6 1.887; zipf 2.028 / 1.983-1.997
 // / 1.985-1.996 / 2.001: profiles/r5/row_ahead/)
@@ -70,9 +77,15 @@ constexpr int kWinRounds = 5;                       // prefetch: 5 x 1 KiB loads
 constexpr int kWinBytes = 4352;
 constexpr u32 kWaveMaxLen = kWinBytes - 16;         // a0 (<=15) + len must fit the window
 // The wave path's CRC tables in LDS: the decode tables, ids 0..40 (tpz_internal.h).
+#ifdef TPZ_ABL_W20
+constexpr int kWaveTabBytes = 16 * 1024;
+constexpr u32 kWaveMaxN = 63;
+constexpr int kWaveTabSlots = 128;
+#else
 constexpr int kWaveTabBytes = kTableBytes;
 constexpr u32 kWaveMaxN = 255;                      // the table holds 2n + 1 <= 511 entries
 constexpr int kWaveTabSlots = 512;
+#endif
 constexpr int kWaveMapLen = 288;                    // >= (kWaveMaxLen + 2) / 16 + 3 map slots
 constexpr int kSlotBytes = kGuard + kWinBytes + 32 + kWaveTabSlots * 4 + 2 * kWaveMapLen;
 static_assert(kSlotBytes % 16 == 0 && kWaveMapLen % 8 == 0, "slot alignment");
@@ -167,6 +180,8 @@ __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) {
   asm volatile("" : "+v"(z));
   return tab[id * 256 + (((z & 0x10000u) + __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 31u)];
 }
+#elif defined(TPZ_ABL_W20)
+__device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[(id & 15) * 256 + byte]; }
 #else
 __device__ __forceinline__ u32 tlook(const u32* tab, int id, u32 byte) { return tab[id * 256 + byte]; }
 #endif
@@ -1501,10 +1516,10 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
   put_meta(o, b, st, cnt, crc);
 }
 
-__device__ __forceinline__ void load_tables(u32* tab, const u32* gtab) {
+__device__ __forceinline__ void load_tables(u32* tab, const u32* gtab, int bytes = kTableBytes) {
   const uint4* s = reinterpret_cast<const uint4*>(gtab);
   uint4* d = reinterpret_cast<uint4*>(tab);
-  for (int i = threadIdx.x; i < kTableBytes / 16; i += blockDim.x) d[i] = s[i];
+  for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
   __syncthreads();
 }
 
@@ -1570,7 +1585,7 @@ __device__ __forceinline__ T const_load(const T* base, u64 i) {
 // later claimers have claimed rows and a row past the batch has been published: the orders a
 // fast box produces only rarely.
 __device__ __noinline__ void rowlate_delay(const Params& p, u32 wid, u32 point) {
-  const u32 rows = (p.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
+  const u32 rows = (p.n_blocks + kRowBlocks - 1) / kRowBlocks;
   const u32 ctr = __hip_atomic_load(p.row_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool late = point == 0 ? (wid & 1u) != 0 : (wid & 3u) == 2;
   if (late && ctr + 2 * gridDim.x >= rows)
@@ -1585,7 +1600,12 @@ constexpr u32 kOnchipMask = 4095;
 // CS: log2 of the blocks a wave claims at a time (launch_decode's choice, a compile-time constant
 // so that the claim's shifts and masks take no registers)
 template <bool FLAT, u32 CS>
-__global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
+#if defined(TPZ_ABL_W20) && !defined(TPZ_ABL_NOCAP)
+__global__ __launch_bounds__(kWGThreads) __attribute__((amdgpu_waves_per_eu(5, 5)))
+#else
+__global__ __launch_bounds__(kWGThreads, 4)
+#endif
+void decode_wave_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWaveLds];
   u32* tab = reinterpret_cast<u32*>(lds);
   __shared__ u32 chunk_next;          // the workgroup's next unclaimed chunk
@@ -1603,7 +1623,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
   if (threadIdx.x < kRowAhead && CS < kRowShift) {   // slots 0 .. kRowAhead-1 (load_tables' barrier publishes)
     const u32 r0 = atomicAdd(p.row_ctr, 1u);
     row_ent[threadIdx.x] = (u64)r0 | (u64)threadIdx.x << 32;
-    if ((u64)r0 * kWavesPerWG >= p.n_blocks) {
+    if ((u64)r0 * kRowBlocks >= p.n_blocks) {
       claims_done = 1;
       atomicMin(&exit_slot, kRowAhead);    // every claim after the barrier sees claims_done
     }
@@ -1615,7 +1635,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     out_lds = p.out;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.spill_used = 0;   // the spill phase runs after
-  load_tables(tab, p.crc_tables);
+  load_tables(tab, p.crc_tables, kWaveTabBytes);
 
   const u32 wid = uni(threadIdx.x >> 6);
   const u32 lane = lane_id();
@@ -1664,7 +1684,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     if (pend_slot != ~0u) {
       if (lane == 0) {
 
-        if ((u64)pend_row * kWavesPerWG >= p.n_blocks) {
+        if ((u64)pend_row * kRowBlocks >= p.n_blocks) {
           // claims_done first, then the chunk counter: a chunk q >= Q was taken after this read,
           // so its claimer reads claims_done = 1 and claims no row. Rows are claimed only for the
           // slots of chunks q < Q, the last being slot (Q - 1) / kq + kRowAhead.
@@ -1705,7 +1725,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       if (lane == 0) q_tk = atomicAdd(&chunk_next, 1u);
       const u32 q = uni(q_old);
       if (!dyn_rows) {
-        const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kWavesPerWG;
+        const u64 f = ((u64)q * gridDim.x + blockIdx.x) * kRowBlocks;
         return f < p.n_blocks ? (u32)f : p.n_blocks;
       }
       const u32 slot_q = q >> rshift;
@@ -1751,7 +1771,7 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
       }
       row = uni(row);
       if (row != kRowExit) {
-        const u64 f = (u64)row * kWavesPerWG + ((q & ((1u << rshift) - 1u)) << cshift);
+        const u64 f = (u64)row * kRowBlocks + ((q & ((1u << rshift) - 1u)) << cshift);
         if (f < p.n_blocks) return (u32)f;
       }
       // (a row past the batch, or a chunk past the last row's blocks: the next chunk)
@@ -1845,9 +1865,16 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     }
   };
   PendingCrc pd{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#ifndef TPZ_ABL_NOPF
   issue(b, 0, s_cur, e_cur);
+#endif
 
   while (b < p.n_blocks) {
+#ifdef TPZ_ABL_NOPF
+    // timing build: no prefetch (the block's loads issued and waited for at its staging; frees
+    // the 20 VGPRs the prefetch holds across a block)
+    issue(b, j, s_cur, e_cur);
+#endif
     const u64 s = s_cur, e = e_cur;
     const u64 kf = kf_cur, vf = vf_cur, ef = ef_cur;
     const u32 len64 = (e - s) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)(e - s);
@@ -1876,7 +1903,9 @@ __global__ __launch_bounds__(kWGThreads, 4) void decode_wave_kernel(Params p) {
     }
     b = chunk_first(q_cur) + j;
     b = b < p.n_blocks ? b : p.n_blocks;
+#ifndef TPZ_ABL_NOPF
     issue(b, j, s_cur, e_cur);       // next block's loads fly while this one decodes
+#endif
     __builtin_amdgcn_wave_barrier();
     TPZ_STAMP(S, 1);
     if (fits) {
@@ -2362,8 +2391,12 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   // (the kernel takes it as a template argument, CS)
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
-  u32 wgs_needed = (a.n_blocks + kWavesPerWG - 1) / kWavesPerWG;
+  u32 wgs_needed = (a.n_blocks + kRowBlocks - 1) / kRowBlocks;
+#ifdef TPZ_ABL_W20
+  u32 grid = 2 * a.num_cus;
+#else
   u32 grid = a.num_cus;
+#endif
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   if (a.keys) {
     if (p.chunk_shift == 1u)
