@@ -50,7 +50,11 @@ constexpr int kWave = 64;
 // timing build (wrong CRCs: the shift and inverse tables alias T_0..T_15): two workgroups of 10
 // waves per CU (20 waves), 16 KiB of tables per workgroup, 64-entry tables, VGPRs capped at 96
 // (the compiler spills what does not fit); prices VERDICT r5's 18-20-wave shape
+#ifdef TPZ_ABL_W8
+constexpr int kWavesPerWG = 8;    // (two workgroups of 8: the co-residency check of DESIGN §4f)
+#else
 constexpr int kWavesPerWG = 10;
+#endif
 #else
 constexpr int kWavesPerWG = 16;
 #endif
@@ -211,6 +215,9 @@ __device__ __forceinline__ u32 crc_shift_small(const u32* tab, u32 a, u32 k) {
 // Inverse of shift_k: un-feed k zero bytes (crc' = (crc >> 8) ^ T_0[crc & 0xFF] is invertible
 // because the top byte of T_0[b] determines b). Only used to report a mismatching CRC.
 __device__ __forceinline__ u32 crc_unshift_small(const u32* tab, u32 r, u32 k) {
+#ifdef TPZ_ABL_W20
+  return r;   // (timing build: its CRCs mismatch by construction; no un-shift chain per block)
+#endif
   for (u32 i = 0; i < k; i++) {
     const u32 b = tlook(tab, kCrcInvTable, r >> 24);
     r = ((r ^ tlook(tab, 0, b)) << 8) | b;
@@ -1425,7 +1432,11 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
       const u32 tot = FLAT ? (vc ? vs + vc : (kc ? dk + kc : 0u)) : vs + vc;
 #ifndef TPZ_ABL_NOCOPY
 #if !defined(TPZ_ABL_NOCRC) && !defined(TPZ_ABL_MEMONLY)
+#ifdef TPZ_ABL_UNFUSED
+      if (false) {            // timing build: the copy, then the CRC (wave_crc), as the big path
+#else
       if (!BIG && P >= 4) {   // the copy runs fused with the CRC below
+#endif
         fuse = true;
         // short values: every window; short keys only: the windows of the key chunks (the
         // values start on a chunk of their own)
@@ -2392,7 +2403,7 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
   u32 wgs_needed = (a.n_blocks + kRowBlocks - 1) / kRowBlocks;
-#ifdef TPZ_ABL_W20
+#if defined(TPZ_ABL_W20) && !defined(TPZ_ABL_GRID1)
   u32 grid = 2 * a.num_cus;
 #else
   u32 grid = a.num_cus;
