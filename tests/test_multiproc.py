@@ -1,4 +1,4 @@
-"""Multi-rank path of bench.py on CPU: world_size 2 over gloo (127.0.0.1).
+"""Multi-rank path of bench.py on CPU: world_size 2 (and 4) over gloo (127.0.0.1).
 
 Covers what the N > 1 run does besides the kernel: every rank builds its own disjoint shard
 (no data-path collective), the shard decodes correctly on its own (checked on the oracle), and
@@ -40,17 +40,19 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_two_ranks_gloo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_gloo(world):
+    """world 4 rehearses the driver's N = 4 run (one rank per GPU) on the CPU."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    r0, r1 = out[0], out[1]
-    assert r0[0] and r1[0]                       # each shard decodes on its own
-    assert r0[1] == r1[1] == 2.0 and r0[2] == r1[2] == 1.0   # MAX over ranks
-    assert r0[4] != r1[4]                        # disjoint shards (different seeds)
-    expect = r0[3] * world * 3 / 2.0 / bench.GIB
-    assert r0[5] == pytest.approx(expect)
+    rs = [out[r] for r in range(world)]
+    assert all(r[0] for r in rs)                 # each shard decodes on its own
+    for r in rs:                                 # MAX over ranks, on every rank
+        assert r[1] == float(world) and r[2] == 0.5 * world
+    assert len({r[4] for r in rs}) == world      # disjoint shards (different seeds)
+    expect = rs[0][3] * world * 3 / float(world) / bench.GIB
+    assert rs[0][5] == pytest.approx(expect)
 
 
 def _e2e_worker(rank, world, port, out, fail_rank):
