@@ -581,40 +581,13 @@ struct SlotDst {
   }
 };
 
-// Bytes [lo, hi) of the 16-byte chunk v to p[lo .. hi) (p 16-aligned), in naturally aligned
-// pieces: the bytes around them belong to the neighbouring block's keys or values, which
-// another wave writes.
-__device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t r, u32 base, uint4 v, u32 lo,
-                                              u32 hi) {
-  const u64 q0 = (u64)v.y << 32 | v.x, q1 = (u64)v.w << 32 | v.z;
-  auto bytes = [&](u32 a) -> u64 {   // the 8 bytes from a (a < 16)
-    return a == 0 ? q0 : a >= 8 ? (q1 >> (8 * (a - 8))) : ((q0 >> (8 * a)) | (q1 << (64 - 8 * a)));
-  };
-  auto st = [&](u32 a, u32 w) {      // w bytes (1, 2, 4 or 8) from a, naturally aligned
-    const u64 x = bytes(a);
-    if (w == 1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)x, r, base + a, 0, 0);
-    else if (w == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)x, r, base + a, 0, 0);
-    else if (w == 4) __builtin_amdgcn_raw_buffer_store_b32((u32)x, r, base + a, 0, 0);
-    else __builtin_amdgcn_raw_buffer_store_b64(
-        __builtin_bit_cast(__attribute__((ext_vector_type(2))) u32, x), r, base + a, 0, 0);
-  };
-  u32 a = lo;
-  if ((a & 1u) && a + 1 <= hi) { st(a, 1); a += 1; }
-  if ((a & 2u) && a + 2 <= hi) { st(a, 2); a += 2; }
-  if ((a & 4u) && a + 4 <= hi) { st(a, 4); a += 4; }
-  if ((a & 8u) && a + 8 <= hi) { st(a, 8); a += 8; }
-  if (a + 8 <= hi) { st(a, 8); a += 8; }
-  if (a + 4 <= hi) { st(a, 4); a += 4; }
-  if (a + 2 <= hi) { st(a, 2); a += 2; }
-  if (a + 1 <= hi) st(a, 1);
-}
-
 // Flat layout: the block's keys go to keys[kf ..] and its values to vals[vf ..], back to back
 // with the neighbouring blocks'. The copy runs over a virtual stream whose chunks line up with
 // the columns' 16-byte chunks: key byte x at 16-aligned position dk + x (dk = kf mod 16), value
 // byte y at 16 kch + dv + y (kch = the key chunks, dv = vf mod 16). Whole chunks are stored
 // with one 16-byte store; a column's first and last chunk hold the neighbours' bytes too and
-// are stored piecewise (store_partial). The stores go through two descriptors that end at the
+// are stored byte by byte, one byte per lane (the neighbours' bytes belong to the waves that
+// decode those blocks). The stores go through two descriptors that end at the
 // block's last key / value chunk.
 struct FlatOut {
   __amdgpu_buffer_rsrc_t rk, rv;   // from the 16-aligned key / value chunk base, 16 kch / 16 vch bytes
@@ -635,11 +608,23 @@ struct FlatOut {
     __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (!skip && isk && full) ? 16 * c : kOob, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (!skip && isv && full) ? 16 * jv : kOob, 0, 0);
     const bool part = !skip && (isk || isv) && !full;
-    // (one copy of the byte-store cascade for both columns: the descriptor is wave-uniform)
-#pragma unroll 1
-    for (u32 col = 0; col < 2; col++) {
-      const bool mine = part && (col ? isv : isk);
-      if (__ballot(mine) && mine) store_partial(col ? rv : rk, 16 * (col ? jv : c), acc, lo, hi);
+    // A column's first and last chunk (at most four per block): the wave stores each one's bytes
+    // [lo, hi) one byte per lane (lanes 0-15, one store instruction), the chunk broadcast from
+    // its lane. (A per-lane cascade of naturally aligned pieces cost ~300 VALU per block.)
+    u64 pm = __ballot(part);
+    while (pm) {
+      const int L = __builtin_ctzll(pm);
+      pm &= pm - 1;
+      const u32 w0 = readlane(v4.x, L), w1 = readlane(v4.y, L), w2 = readlane(v4.z, L),
+                w3 = readlane(v4.w, L);
+      const u32 Lk = readlane(isk ? 1u : 0u, L);
+      const u32 Lbase = readlane(16 * (isk ? c : jv), L);
+      const u32 Llo = readlane(lo, L), Lhi = readlane(hi, L);
+      const u32 i = lane_id();
+      const u32 w = i < 8 ? (i < 4 ? w0 : w1) : (i < 12 ? w2 : w3);
+      const bool mine = i >= Llo && i < Lhi;
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * (i & 3u))), Lk ? rk : rv,
+                                           mine ? Lbase + i : kOob, 0, 0);
     }
   }
 };
