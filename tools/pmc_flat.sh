@@ -1,5 +1,5 @@
 set -o pipefail
-OUT=gpurun_out/pmcflat; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${1:-gpurun_out/pmcflat}; mkdir -p $OUT; export TMPDIR=/tmp
 for m in slot flat; do
   F=""; [ $m = flat ] && F="--flat"
   timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_WAVES -T --output-format csv -d $OUT/$m -o run -- python3 tools/decode_loop.py --config 4k --steps 8 $F > $OUT/$m.log 2>&1 || exit $?
