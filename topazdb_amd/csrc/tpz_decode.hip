@@ -591,35 +591,34 @@ struct SlotDst {
 // block's last key / value chunk.
 struct FlatOut {
   __amdgpu_buffer_rsrc_t rk, rv;   // from the 16-aligned key / value chunk base, 16 kch / 16 vch bytes
-  u32 ch;                          // kch | vch << 16: the chunks of each column
-  u32 lohi;                        // klo | khi << 8 | vlo << 16 | vhi << 24: the valid bytes
-                                   // [lo, hi) of a column's first / last chunk
+  u32 rgk, rgv;                    // the keys' / values' stream bytes [start, end): start | end << 16
+                                   // (the values start at 16 kch + dv; wave-path blocks: < 2^16)
   __device__ __forceinline__ void put(u32 c, uint4 acc, bool skip) const {
-    const u32 kch = ch & 0xFFFFu, vch = ch >> 16;
-    const bool isk = c < kch;
-    const u32 jv = c - kch;
-    const bool isv = !isk && jv < vch;
-    const u32 first = isk ? (c == 0) : (jv == 0), last = isk ? (c + 1 == kch) : (jv + 1 == vch);
-    const u32 sh = isk ? 0u : 16u;   // this column's byte pair in lohi
-    const u32 lo = first ? (lohi >> sh) & 0xFFu : 0u;
-    const u32 hi = last ? (lohi >> (sh + 8)) & 0xFFu : 16u;
-    const bool full = lo == 0 && hi == 16;
+    const int x0 = (int)(16 * c);
+    const int kb = (int)((rgv & 0xFFFFu) & ~15u);            // 16 kch
+    const bool isk = x0 < kb;
+    const u32 rg = isk ? rgk : rgv;
+    const int cs = (int)(rg & 0xFFFFu), ce = (int)(rg >> 16);
+    // the column's bytes [lo, hi) of this chunk (hi <= lo: none)
+    const int lo = max(cs, x0) - x0, hi = min(ce, x0 + 16) - x0;
+    const bool act = !skip && hi > lo;
+    const bool full = act && lo == 0 && hi == 16;
+    const u32 off = (u32)(isk ? x0 : x0 - kb);
     const auto v4 = __builtin_bit_cast(__attribute__((ext_vector_type(4))) u32, acc);
-    __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (!skip && isk && full) ? 16 * c : kOob, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (!skip && isv && full) ? 16 * jv : kOob, 0, 0);
-    const bool part = !skip && (isk || isv) && !full;
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rk, (full && isk) ? off : kOob, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v4, rv, (full && !isk) ? off : kOob, 0, 0);
     // A column's first and last chunk (at most four per block): the wave stores each one's bytes
     // [lo, hi) one byte per lane (lanes 0-15, one store instruction), the chunk broadcast from
     // its lane. (A per-lane cascade of naturally aligned pieces cost ~300 VALU per block.)
-    u64 pm = __ballot(part);
+    u64 pm = __ballot(act && !full);
     while (pm) {
       const int L = __builtin_ctzll(pm);
       pm &= pm - 1;
       const u32 w0 = readlane(v4.x, L), w1 = readlane(v4.y, L), w2 = readlane(v4.z, L),
                 w3 = readlane(v4.w, L);
       const u32 Lk = readlane(isk ? 1u : 0u, L);
-      const u32 Lbase = readlane(16 * (isk ? c : jv), L);
-      const u32 Llo = readlane(lo, L), Lhi = readlane(hi, L);
+      const u32 Lbase = readlane(off, L);
+      const u32 Llo = readlane((u32)lo, L), Lhi = readlane((u32)hi, L);
       const u32 i = lane_id();
       const u32 w = i < 8 ? (i < 4 ? w0 : w1) : (i < 12 ? w2 : w3);
       const bool mine = i >= Llo && i < Lhi;
@@ -634,11 +633,11 @@ __device__ __forceinline__ FlatOut flat_out(const Out& o, u64 kf, u64 vf, u32 K,
   const u32 dk = (u32)kf & 15u, dv = (u32)vf & 15u;
   const u32 kch = K ? (dk + K + 15) >> 4 : 0u;
   const u32 vch = V ? (dv + V + 15) >> 4 : 0u;
-  D.ch = kch | vch << 16;
   D.rk = __builtin_amdgcn_make_buffer_rsrc(o.keys + (kf & ~15ull), (short)0, (int)(16 * kch), 0x00020000);
   D.rv = __builtin_amdgcn_make_buffer_rsrc(o.vals + (vf & ~15ull), (short)0, (int)(16 * vch), 0x00020000);
-  const u32 khi = dk + K - 16 * (kch ? kch - 1 : 0u), vhi = dv + V - 16 * (vch ? vch - 1 : 0u);
-  D.lohi = dk | khi << 8 | dv << 16 | vhi << 24;
+  const u32 vs = 16 * kch + dv;
+  D.rgk = dk | (dk + K) << 16;
+  D.rgv = vs | (vs + V) << 16;
   return D;
 }
 // Where the virtual stream's values start: the key chunks, then dv (flat); value_start(K)
