@@ -786,7 +786,8 @@ struct CombLv {
 };
 template <int J>
 __device__ __forceinline__ CombLv comb_issue(const u32* tab, u32 A) {
-  CombLv c{0u, 0u, 0u, 0u};
+  // (lanes outside level J's set never read c: no zero fill, which cost four moves per level)
+  CombLv c;
   if (comb_lane<J>(lane_id())) {        // exec-masked: fewer lanes touch LDS at each level
     constexpr int b0 = 16 + 4 * J;
     c.r0 = tlook(tab, b0, A & 0xFF);
