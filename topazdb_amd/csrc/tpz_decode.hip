@@ -1469,9 +1469,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         lc = copy_crc_piped<FLAT, 0u>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                          reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                          fo, win, pb, P + k, o, pd);
-      } else if (!FLAT && f_w3 <= 2u) {
+      } else if (f_w3 <= 2u) {
         // short keys within the first two copy windows, values of 16 bytes or more (the Zipf
-        // shape; slotted only: the flat kernel spills VGPRs with it)
+        // shape)
         lc = copy_crc_piped<FLAT, 2u>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                       reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
                                       fo, win, pb, P + k, o, pd);
@@ -2382,8 +2382,10 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
   const u64 avg = a.n_blocks ? a.src_bytes / a.n_blocks : 0;
   // Rows claimed 3 slots ahead and the chunk shift a compile-time constant: single blocks per
   // claim beat pairs in the slotted decode (4k 1.821 vs 1.827 ms and 1.824 vs 1.856 on two boxes,
-  // zipf equal), pairs stay better in the flat one (zipf 2.483 vs 2.506): profiles/r5/chunk_cs/.
-  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : (a.keys ? 1u : 0u);
+  // zipf equal: profiles/r5/chunk_cs/). The flat decode kept pairs (zipf 2.483 vs 2.506) until its
+  // partial-chunk stores got cheaper; since then single blocks are 0.7 % faster there too (4k and
+  // zipf, two boxes: profiles/r6/flat_put/ab_cs0_*).
+  p.chunk_shift = avg > kWaveMaxLen ? kRowShift : 0u;
   // (the kernel takes it as a template argument, CS)
   p.row_ctr = a.tail + kTailRow;
   p.err = a.tail + kTailError;
@@ -2395,8 +2397,8 @@ void launch_decode(const LaunchArgs& a, hipStream_t stream) {
 #endif
   if (wgs_needed < grid) grid = wgs_needed ? wgs_needed : 1;
   if (a.keys) {
-    if (p.chunk_shift == 1u)
-      hipLaunchKernelGGL((decode_wave_kernel<true, 1u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
+    if (p.chunk_shift == 0u)
+      hipLaunchKernelGGL((decode_wave_kernel<true, 0u>), dim3(grid), dim3(kWGThreads), 0, stream, p);
     else
       hipLaunchKernelGGL((decode_wave_kernel<true, kRowShift>), dim3(grid), dim3(kWGThreads), 0, stream, p);
   } else {
