@@ -1088,7 +1088,8 @@ template <bool FLAT, u32 K3>
 __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& col,
                                               const uint16_t* map, u32 nk, u32 tot, uint8_t* dst,
                                               const FlatOut& D, const uint8_t* win, int pb, u32 Pa,
-                                              const Out& o, PendingCrc& pd) {
+                                              const Out& o, PendingCrc& pd, u32 k3n = K3) {
+  // (k3n <= K3, uniform: the windows that hold short keys; the others take the plain rule)
   const u32 lane = lane_id();
   FastWin F;
   F.nk = nk;
@@ -1146,7 +1147,7 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
   u32 rare = 0;
   auto gissue = [&](PWin& P, u32 w) {
     const u32 x0 = 16 * (64 * w + lane);
-    if (w < K3) {
+    if (w < K3 && w < k3n) {
       // (window 0's entries j + 2, j + 3 were read with its others; a later window's are read
       // here, into the same registers: window 0 has been stored by then)
       if (w > 0) col.get2(min(P.j + 2, F.last), W3.e2, W3.d2, W3.e3, W3.d3);
@@ -1170,11 +1171,11 @@ __device__ __forceinline__ u32 copy_crc_piped(const u32* tab, const ColSmall& co
     const u32 x0 = 16 * c;
     // (no rare path outside a K3 window 0: the other windows hold values of 16 bytes or more,
     // so no two segments end in one chunk and no chunk meets three segments)
-    const bool rw = w < K3 && (rare & (1u << w));
+    const bool rw = w < K3 && w < k3n && (rare & (1u << w));
     uint4 acc = gath_finish(P.ga, P.act ? (int)x0 + P.d0 : -kGuard);
     const uint4 nx = gath_finish(P.gn, P.cross ? (int)x0 + P.d1 : -kGuard);
     if (P.cross) acc = merge_at(acc, nx, (int)(P.e0 - x0));
-    if (w < K3) {
+    if (w < K3 && w < k3n) {
       const uint4 n2 = gath_finish(W3.g2, W3.b2 ? (int)x0 + W3.d2 : -kGuard);
       if (W3.b2) acc = merge_at(acc, n2, (int)(P.e1 - x0));
     }
@@ -1474,7 +1475,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
         // shape)
         lc = copy_crc_piped<FLAT, 2u>(tab, *reinterpret_cast<const ColSmall*>(&col),
                                       reinterpret_cast<const uint16_t*>(map), f_nk, f_tot, f_dst,
-                                      fo, win, pb, P + k, o, pd);
+                                      fo, win, pb, P + k, o, pd, FLAT ? 2u : f_w3);
+        // (slotted zipf 1.8699 -> 1.8614 ms with the window count; the flat kernel ran 0.4 %
+        // slower with it and keeps both windows: profiles/r6/decode_ab/k3n_*)
         f_short = false;   // (its combine ran interleaved: the next block need not run it early)
       } else
       {
