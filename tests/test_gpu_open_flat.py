@@ -153,3 +153,42 @@ def test_degenerate_files(ctx):
     # (file 4: four zero bytes, the CRC of nothing (0) stored as its trailer: OK)
     assert (st[[0, 3, 4]] == _lib.BLOCK_OK).all()
     assert st[1] == _lib.BLOCK_MALFORMED and st[2] == _lib.BLOCK_MALFORMED
+
+
+def test_offsets_past_2gib(ctx):
+    """A batch of 2.6 GB: blocks and file boundaries at offsets of 2 GiB and more (the open
+    kernel's uniform extents once sign-extended their low half there and faulted; the small
+    batches above never reach 2^31)."""
+    nb = 5 * (1 << 17)
+    src, ext = synth.make_region("4k", nb, seed=77)
+    assert int(ext[-1]) > (1 << 31) + (1 << 28)
+    rng = np.random.default_rng(5)
+    cuts = np.sort(rng.choice(np.arange(1, nb), 23, replace=False))
+    fblock = [0] + [int(c) for c in cuts] + [nb]
+    tails, text = bytearray(), [0]
+    for f in range(len(fblock) - 1):
+        body = src[int(ext[fblock[f]]):int(ext[fblock[f + 1]])]
+        t = rng.bytes(int(rng.integers(0, 300)))
+        crc = zlib.crc32(t, zlib.crc32(body))
+        if f == 7:
+            crc ^= 1                                   # one mismatching file
+        tails += t + struct.pack(">I", crc)
+        text.append(len(tails))
+    dev = torch.device("cuda:0")
+    blocks = DeviceBatch(np.ascontiguousarray(src[:int(ext[-1])]), ext)
+    tb = DeviceBatch(np.frombuffer(bytes(tails), np.uint8), np.asarray(text, np.uint64))
+    d_fb = torch.tensor(np.asarray(fblock, np.int32), device=dev)
+    crc, st, first = open_flat_layout(ctx, blocks, d_fb, tb)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    want = np.full(len(fblock) - 1, _lib.BLOCK_OK, np.uint8)
+    want[7] = _lib.BLOCK_CHECKSUM_MISMATCH
+    np.testing.assert_array_equal(st, want)
+    got = crc.cpu().numpy().view(np.uint32)
+    for f in (0, 7, len(fblock) - 2):
+        body = src[int(ext[fblock[f]]):int(ext[fblock[f + 1]])]
+        t = bytes(tails[text[f]:text[f + 1] - 4])
+        assert got[f] == zlib.crc32(t, zlib.crc32(body)), f
+    ref = flat_layout(ctx, blocks)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(first.cpu().numpy(), ref.cpu().numpy())

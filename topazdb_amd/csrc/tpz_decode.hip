@@ -1309,7 +1309,9 @@ __device__ __forceinline__ void decode_block(const u32* tab, uint8_t* win, const
     // (flat: the exact ends, n pairs reserved for every block by tpz_flat_layout)
     const bool slots_fit = FLAT || 6u * n <= len;
     // (flat: ef = efirst[b], loaded with the block's prefetch)
-    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + (FLAT ? ef : ends_base(o.efirst, ext_b, b));
+    // (uniform: readfirstlane'd, so that the store's descriptor is built in SGPRs; the compiler
+    // could not tell and wrapped the store in a waterfall loop)
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + uni64(FLAT ? ef : ends_base(o.efirst, ext_b, b));
     // whole 128-byte lines of {kend, vend} in the slotted layout; exactly n in the exact one
     const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
     {
@@ -2051,7 +2053,7 @@ __device__ __forceinline__ void big_block(const Params& p, const u32* tab, uint8
   } else {
     const u32 db = a0 + 2 + 2 * n, dl = P - 2 - 2 * n;
     const bool slots_fit = 6u * n <= len;
-    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + ends_base(o.efirst, ext_b, b);
+    uint2* ends_g = reinterpret_cast<uint2*>(o.ends) + uni64(ends_base(o.efirst, ext_b, b));
     const u32 n_pad = o.efirst ? n : (n + 15) & ~15u;
     const u32 G = (n + 63) >> 6;
     // pass 1: group sums (read back by the same wave when there is one group)

@@ -230,6 +230,16 @@ constexpr int kOpTabBytes = 16 * 1024;       // slice-by-16 (conflict-light repl
 constexpr int kOpWgsPerCu = 3;                // slower)
 constexpr int kOpLds = kOpTabBytes + kOpWaves * kOpSlot;
 
+// A wave-uniform 64-bit value loaded by a vector load, made visibly uniform (readfirstlane):
+// buffer descriptors built from it stay in SGPRs (otherwise the compiler wraps every buffer load
+// in a waterfall loop over the lanes' descriptors).
+// (readfirstlane returns int: each half goes through a u32, or the low half would be
+// sign-extended into the high one for offsets of 2 GiB and more)
+__device__ __forceinline__ u64 op_uni64(u64 x) {
+  const u32 lo = __builtin_amdgcn_readfirstlane((u32)x), hi = __builtin_amdgcn_readfirstlane((u32)(x >> 32));
+  return ((u64)hi << 32) | lo;
+}
+
 struct OpenParams {
   const uint8_t* src;
   const u64* bext;        // the blocks: block b = src[bext[b] .. bext[b + 1])
@@ -342,8 +352,8 @@ __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
   u64 b = (u64)blockIdx.x * kOpWaves + wid;
   u64 s = 0, e = 0;
   if (b < p.nb) {
-    s = p.bext[b];
-    e = p.bext[b + 1];
+    s = op_uni64(p.bext[b]);
+    e = op_uni64(p.bext[b + 1]);
     if (staged(s, e)) issue(s, e);
   }
   for (; b < p.nb; b += V) {
@@ -357,8 +367,8 @@ __global__ __launch_bounds__(kOpThreads) void open_blocks_kernel(OpenParams p) {
     const u64 bn = b + V;
     u64 sn = 0, en = 0;
     if (bn < p.nb) {
-      sn = p.bext[bn];
-      en = p.bext[bn + 1];
+      sn = op_uni64(p.bext[bn]);
+      en = op_uni64(p.bext[bn + 1]);
       if (staged(sn, en)) issue(sn, en);
     }
     Sizes z{0, 0, 0};
