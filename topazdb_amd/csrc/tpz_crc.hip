@@ -150,16 +150,6 @@ __device__ __forceinline__ u32 zshift_any(const u32* g, u32 a, u64 n) {
 // ------------------------------------------------------------------ window kernel
 __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
   __shared__ __attribute__((aligned(16))) u32 lds[kLdsWords];
-  {
-    const uint4* g = reinterpret_cast<const uint4*>(p.rep);
-    const uint4* o = reinterpret_cast<const uint4*>(gop(p.tables, kJLane));
-    const uint4* w = reinterpret_cast<const uint4*>(gop(p.tables, kJWin));
-    uint4* d = reinterpret_cast<uint4*>(lds);
-    constexpr int kRep4 = kRepWords / 4, kOps4 = kLaneOps * 256;
-    for (int i = threadIdx.x; i < kLdsWords / 4; i += kThreads)
-      d[i] = i < kRep4 ? g[i] : (i < kRep4 + kOps4 ? o[i - kRep4] : w[i - kRep4 - kOps4]);
-    __syncthreads();
-  }
   const u32* rep = lds;
   const u32* lop = lds + kRepWords;                 // lane-shift operator k at lop + 1024 k
   const u32* wop = lop + 1024 * kLaneOps;           // shift by one window
@@ -170,19 +160,12 @@ __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
   const u64 per = (p.n_windows + nw - 1) / nw;
   const u64 g0 = wave * per;
   const u64 g1 = min(p.n_windows, g0 + per);
-  if (g0 >= g1 || p.n_ranges == 0) return;
+  const bool live = g0 < g1 && p.n_ranges != 0;
 
-  // first range whose end (aligned space) lies beyond the span's start (ext is non-decreasing)
-  u32 r;
-  {
-    const u64 t = g0 << kWinLog;
-    u32 lo = 0, hi = p.n_ranges;  // smallest r with ext[r+1] + delta > t
-    while (lo < hi) {
-      const u32 mid = (lo + hi) >> 1;
-      if (uni64(p.ext[mid + 1]) + p.delta > t) hi = mid; else lo = mid + 1;
-    }
-    r = lo;
-  }
+  // The span's first range and first window are found and that window's loads issued before the
+  // tables are staged in LDS, so its HBM latency overlaps the staging (every workgroup stages
+  // 156 KiB at the start)
+  u32 r = 0;
   u32 cur = ~0u, acc = 0;   // the range being folded, R0 of its parts so far ending at `last`
   u64 last = 0, cur_A = 0;
   // the next window's runs, loaded while the current one is folded when the range covers it
@@ -192,8 +175,40 @@ __global__ __launch_bounds__(kThreads, 1) void crc_window_kernel(CrcParams p) {
   u32 pf_r = ~0u;
   // range r's geometry and end stay in registers: consecutive windows of one range (the common
   // case, files are MiBs) need no extent loads; range r + 1 starts where r ends
-  u64 hiX = uni64(p.ext[r + 1]) + p.delta;
-  RangeGeo Gr = range_geo(uni64(p.ext[r]), hiX - p.delta, p.delta, p.trailer);
+  u64 hiX = 0;
+  RangeGeo Gr = range_geo(0, 0, 0, 0);
+  if (live) {
+    // first range whose end (aligned space) lies beyond the span's start (ext is non-decreasing)
+    const u64 t = g0 << kWinLog;
+    u32 lo = 0, hi = p.n_ranges;  // smallest r with ext[r+1] + delta > t
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (uni64(p.ext[mid + 1]) + p.delta > t) hi = mid; else lo = mid + 1;
+    }
+    r = lo;
+    if (r < p.n_ranges) {
+      hiX = uni64(p.ext[r + 1]) + p.delta;
+      Gr = range_geo(uni64(p.ext[r]), hiX - p.delta, p.delta, p.trailer);
+      if (Gr.valid && t >= Gr.s && t + kWin <= Gr.A) {   // the first window lies inside range r
+        const uint8_t* x = p.base + t + kWin - (u64)kLaneRun * (lane + 1);
+#pragma unroll
+        for (int c = 0; c < kC; c++) pf[c] = *reinterpret_cast<const uint4*>(x + 16 * c);
+        pf_g = g0;
+        pf_r = r;
+      }
+    }
+  }
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(p.rep);
+    const uint4* o = reinterpret_cast<const uint4*>(gop(p.tables, kJLane));
+    const uint4* w = reinterpret_cast<const uint4*>(gop(p.tables, kJWin));
+    uint4* d = reinterpret_cast<uint4*>(lds);
+    constexpr int kRep4 = kRepWords / 4, kOps4 = kLaneOps * 256;
+    for (int i = threadIdx.x; i < kLdsWords / 4; i += kThreads)
+      d[i] = i < kRep4 ? g[i] : (i < kRep4 + kOps4 ? o[i - kRep4] : w[i - kRep4 - kOps4]);
+    __syncthreads();
+  }
+  if (!live) return;
   for (u64 g = g0; g < g1 && r < p.n_ranges; g++) {
     const u64 w0 = g << kWinLog, w1 = w0 + kWin;
     while (hiX <= w0 && r + 1 < p.n_ranges) {
